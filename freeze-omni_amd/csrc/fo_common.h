@@ -1,0 +1,85 @@
+// Shared helpers for the Freeze-Omni MI355X (gfx950) kernels.
+// Everything here is CDNA4-only: 64-lane waves, bf16 MFMA, no portability layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef uint16_t bf16_t;  // raw bf16 storage
+
+#define FO_WAVE 64
+
+// ---------------------------------------------------------------- error plumbing
+// Every C-ABI entry returns 0 on success or a negative code; the message is kept
+// per thread and read back with fo_last_error().
+namespace fo {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace fo
+
+#define FO_REQUIRE(cond, ...)            \
+  do {                                   \
+    if (!(cond)) {                       \
+      fo::set_error(__VA_ARGS__);        \
+      return -2;                         \
+    }                                    \
+  } while (0)
+
+#define FO_HIP(call)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      fo::set_error("%s failed: %s", #call, hipGetErrorString(e_));          \
+      return -1;                                                              \
+    }                                                                         \
+  } while (0)
+
+// ---------------------------------------------------------------- numeric helpers
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+__host__ __device__ __forceinline__ float round_f16(float f) {
+  return (float)(_Float16)f;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// block-wide sum for blockDim.x == 64*NW; lds must hold NW floats
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* lds) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) lds[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t += lds[i];
+  return t;
+}
+
+enum FoAct { FO_ACT_NONE = 0, FO_ACT_RELU = 1, FO_ACT_SILU = 2, FO_ACT_GELU = 3, FO_ACT_SWIGLU = 4 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case FO_ACT_RELU: return v > 0.f ? v : 0.f;
+    case FO_ACT_SILU: return v / (1.f + expf(-v));
+    case FO_ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    default: return v;
+  }
+}

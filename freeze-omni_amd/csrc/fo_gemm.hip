@@ -1,0 +1,308 @@
+// Weight-streaming GEMM for every linear layer on the Freeze-Omni hot path.
+//
+//   Y[M, N] = epilogue( X[M, K] (bf16) . W[N, K]^T (bf16, pre-packed) )
+//
+// The reference reaches these through torch.nn.Linear under bf16 autocast
+// (models/audioLLM.py:482 -> Qwen2 q/k/v/o/gate/up/down, models/encoder/attention.py:411-413,
+// models/adapter.py:679, models/decoder/decoder.py:346).  On the path M is tiny (one row per
+// user token: 1..~64) while W is 3..150 MB, so the kernel is an HBM weight stream:
+//  * W is packed once at load into MFMA fragment order [N/16][K/32][64 lanes][8 bf16] so every
+//    wave-instruction of the stream is one contiguous 1 KiB read.
+//  * one workgroup = 4 waves = 16 (or 2x16 for the SwiGLU pair) output columns x up to 64 rows;
+//    the 4 waves split the K range and reduce through LDS.
+//  * when there are too few column tiles to fill 256 CUs the K range is also split across
+//    workgroups; partial slabs go to a workspace and the LAST arriving workgroup (agent-scope
+//    ticket, MI355X_MICROARCH "splitk-seam") sums them in fixed order, so results are
+//    deterministic.
+//  * mfma_f32_16x16x32_bf16 accumulates in fp32; bias/activation/residual/SwiGLU are fused
+//    into the epilogue.
+#include "fo_common.h"
+
+namespace {
+
+struct GemmArgs {
+  const bf16_t* X;
+  const bf16_t* Wp;
+  const float* bias;
+  void* Y;
+  float* ws;
+  int* counters;
+  int ldx, ldy;
+  int M, K, N;     // N: logical output columns (after SwiGLU pairing)
+  int ntiles;      // packed 16-column tiles in Wp
+  int S;           // K split across workgroups
+  int act, out_bf16, residual;
+};
+
+template <int NT, int RB>
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
+  constexpr int ROWS = RB * 16;
+  __shared__ float red[4][NT][ROWS][17];
+  __shared__ int s_last;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tg = blockIdx.x, mt = blockIdx.y, sp = blockIdx.z;
+  const int KS = a.K >> 5;
+  const int kb = (int)((long)KS * sp / a.S), ke = (int)((long)KS * (sp + 1) / a.S);
+  const int len = ke - kb;
+  const int wb = kb + len * wave / 4, we = kb + len * (wave + 1) / 4;
+  const int m0 = mt * ROWS;
+  int rbeff = (a.M - m0 + 15) >> 4;
+  if (rbeff > RB) rbeff = RB;
+
+  f32x4 acc[NT][RB];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bf16x8* bp[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    bp[t] = reinterpret_cast<const bf16x8*>(a.Wp) + (size_t)(tg * NT + t) * KS * 64 + lane;
+  const bf16_t* xr[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    int row = m0 + r * 16 + (lane & 15);
+    if (row > a.M - 1) row = a.M - 1;  // clamp: rows >= M are computed but never stored
+    xr[r] = a.X + (size_t)row * a.ldx + 8 * (lane >> 4);
+  }
+
+  int ks = wb;
+  for (; ks + 4 <= we; ks += 4) {
+    bf16x8 bv[4][NT];
+    bf16x8 av[4][RB];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)(ks + u) * 64);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        if (r < rbeff) av[u][r] = *reinterpret_cast<const bf16x8*>(xr[r] + (size_t)(ks + u) * 32);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          if (r < rbeff) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+  }
+  for (; ks < we; ++ks) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      bf16x8 b = __builtin_nontemporal_load(bp[t] + (size_t)ks * 64);
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        if (r < rbeff) {
+          bf16x8 av = *reinterpret_cast<const bf16x8*>(xr[r] + (size_t)ks * 32);
+          acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc[t][r], 0, 0, 0);
+        }
+    }
+  }
+
+  // D layout (16x16x32): col = lane & 15, row = 4*(lane>>4) + i
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave][t][r * 16 + 4 * (lane >> 4) + i][lane & 15] = acc[t][r][i];
+  __syncthreads();
+
+  constexpr int NE = NT * ROWS * 16;
+  const int Mrows = gridDim.y * ROWS;
+  const int Ncols = a.ntiles * 16;
+  if (a.S > 1) {
+    float* slab = a.ws + (size_t)sp * Mrows * Ncols;
+    for (int e = threadIdx.x; e < NE; e += 256) {
+      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+      const float v = red[0][t][rr][c] + red[1][t][rr][c] + red[2][t][rr][c] + red[3][t][rr][c];
+      slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = v;
+    }
+    // publish: every storing wave drains, barrier, one release + ticket (Guideline 16 counter form)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int* cnt = a.counters + (size_t)mt * gridDim.x + tg;
+      const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (ticket == a.S - 1);
+      if (last) {
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int e = threadIdx.x; e < NE; e += 256) {
+      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+      float v = 0.f;
+      for (int q = 0; q < a.S; ++q) v += a.ws[((size_t)q * Mrows + m0 + rr) * Ncols + (tg * NT + t) * 16 + c];
+      red[0][t][rr][c] = v;
+    }
+  } else {
+    for (int e = threadIdx.x; e < NE; e += 256) {
+      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+      red[0][t][rr][c] = red[0][t][rr][c] + red[1][t][rr][c] + red[2][t][rr][c] + red[3][t][rr][c];
+    }
+  }
+  __syncthreads();
+
+  // epilogue
+  for (int e = threadIdx.x; e < ROWS * 16; e += 256) {
+    const int rr = e >> 4, c = e & 15;
+    const int m = m0 + rr;
+    const int n = tg * 16 + c;
+    if (m >= a.M || n >= a.N) continue;
+    float v;
+    if (NT == 2) {
+      const float g = red[0][0][rr][c], u = red[0][1][rr][c];
+      v = g / (1.f + expf(-g)) * u;
+    } else {
+      v = red[0][0][rr][c];
+      if (a.bias) v += a.bias[n];
+      v = apply_act(v, a.act);
+    }
+    const size_t o = (size_t)m * a.ldy + n;
+    if (a.out_bf16) {
+      bf16_t* y = reinterpret_cast<bf16_t*>(a.Y);
+      if (a.residual) v += bf2f(y[o]);
+      y[o] = f2bf(v);
+    } else {
+      float* y = reinterpret_cast<float*>(a.Y);
+      if (a.residual) v += y[o];
+      y[o] = v;
+    }
+  }
+}
+
+// Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
+// of the source to destination tile (tile_base + t * tile_stride).
+__global__ void k_pack(const void* W, int src_bf16, int N, int K, int ldw, bf16_t* out, int KSp,
+                       int tile_base, int tile_stride, int ntiles_src) {
+  const size_t total = (size_t)ntiles_src * KSp * 64;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int lane = i & 63;
+    const size_t rest = i >> 6;
+    const int ks = rest % KSp;
+    const int t = rest / KSp;
+    const int row = t * 16 + (lane & 15);
+    const int k0 = ks * 32 + 8 * (lane >> 4);
+    bf16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      float f = 0.f;
+      if (row < N && k < K) {
+        if (src_bf16) f = bf2f(reinterpret_cast<const bf16_t*>(W)[(size_t)row * ldw + k]);
+        else f = reinterpret_cast<const float*>(W)[(size_t)row * ldw + k];
+      }
+      v[j] = f2bf(f);
+    }
+    const size_t dt = (size_t)tile_base + (size_t)t * tile_stride;
+    bf16_t* d = out + ((dt * KSp + ks) * 64 + lane) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = v[j];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fo_gemm_pick_split(int M, int N_tiles_groups, int K) {
+  const int KS = K >> 5;
+  const int mt = (M + 63) / 64;
+  const int blocks = N_tiles_groups * mt;
+  int S = (512 + blocks - 1) / blocks;
+  int smax = KS / 8;
+  if (smax < 1) smax = 1;
+  if (S > smax) S = smax;
+  if (S > 16) S = 16;
+  if (S < 1) S = 1;
+  return S;
+}
+
+long long fo_gemm_workspace_floats(int M, int N, int K, int swiglu) {
+  const int ntiles = swiglu ? 2 * ((N + 15) / 16) : (N + 15) / 16;
+  const int NT = swiglu ? 2 : 1;
+  const int S = fo_gemm_pick_split(M, ntiles / NT, K);
+  const int RB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  const int mt = (M + RB * 16 - 1) / (RB * 16);
+  return S > 1 ? (long long)S * mt * RB * 16 * ntiles * 16 : 0;
+}
+
+// Y = act(X @ W^T + bias) (+Y if residual).  X bf16 [M][ldx], K % 32 == 0.
+// swiglu != 0: Wp holds interleaved (gate, up) tile pairs, Y[m][n] = silu(gate) * up, n < N.
+int fo_gemm(const void* X, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
+            void* Y, int ldy, int out_bf16, int act, int residual, float* ws, long long ws_floats,
+            int* counters, int splitk, hipStream_t stream) {
+  FO_REQUIRE(M > 0 && N > 0 && K > 0, "fo_gemm: bad shape M=%d N=%d K=%d", M, N, K);
+  FO_REQUIRE((K & 31) == 0, "fo_gemm: K=%d must be a multiple of 32", K);
+  FO_REQUIRE(ldx >= K, "fo_gemm: ldx=%d < K=%d", ldx, K);
+  FO_REQUIRE(ldy >= N, "fo_gemm: ldy=%d < N=%d", ldy, N);
+  FO_REQUIRE(!(swiglu && bias), "fo_gemm: swiglu with bias unsupported");
+  GemmArgs a;
+  a.X = (const bf16_t*)X;
+  a.Wp = (const bf16_t*)Wp;
+  a.bias = bias;
+  a.Y = Y;
+  a.ws = ws;
+  a.counters = counters;
+  a.ldx = ldx;
+  a.ldy = ldy;
+  a.M = M;
+  a.K = K;
+  a.N = N;
+  a.act = act;
+  a.out_bf16 = out_bf16;
+  a.residual = residual;
+  const int NT = swiglu ? 2 : 1;
+  a.ntiles = NT * ((N + 15) / 16);
+  const int groups = a.ntiles / NT;
+  int S = splitk > 0 ? splitk : fo_gemm_pick_split(M, groups, K);
+  if (S > (K >> 5)) S = K >> 5;
+  a.S = S;
+  const int RB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  const int mt = (M + RB * 16 - 1) / (RB * 16);
+  if (S > 1) {
+    const long long need = (long long)S * mt * RB * 16 * a.ntiles * 16;
+    FO_REQUIRE(ws && counters && need <= ws_floats, "fo_gemm: split-K workspace too small (%lld > %lld)", need,
+               ws_floats);
+  }
+  dim3 grid(groups, mt, S);
+#define FO_LAUNCH(NT_, RB_) hipLaunchKernelGGL((k_gemm<NT_, RB_>), grid, dim3(256), 0, stream, a)
+  if (NT == 1) {
+    if (RB == 1) FO_LAUNCH(1, 1);
+    else if (RB == 2) FO_LAUNCH(1, 2);
+    else FO_LAUNCH(1, 4);
+  } else {
+    if (RB == 1) FO_LAUNCH(2, 1);
+    else if (RB == 2) FO_LAUNCH(2, 2);
+    else FO_LAUNCH(2, 4);
+  }
+#undef FO_LAUNCH
+  return fo::check_launch("fo_gemm");
+}
+
+long long fo_pack_weight_elems(int N, int K) { return (long long)((N + 15) / 16) * 16 * ((K + 31) / 32) * 32; }
+
+// Pack W[N][K] into fragment order at tile offset tile_base with stride tile_stride (tiles of 16 rows).
+int fo_pack_weight(const void* W, int src_bf16, int N, int K, int ldw, void* out, int tile_base, int tile_stride,
+                   hipStream_t stream) {
+  FO_REQUIRE(N > 0 && K > 0 && ldw >= K, "fo_pack_weight: bad shape");
+  const int KSp = (K + 31) / 32;
+  const int nt = (N + 15) / 16;
+  const size_t total = (size_t)nt * KSp * 64;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 65535) blocks = 65535;
+  hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, stream, W, src_bf16, N, K, ldw, (bf16_t*)out, KSp,
+                     tile_base, tile_stride, nt);
+  return fo::check_launch("fo_pack_weight");
+}
+
+}  // extern "C"

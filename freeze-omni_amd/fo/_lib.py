@@ -1,0 +1,93 @@
+"""ctypes binding of libfo_hip.so (the C-ABI declared in include/fo_hip.h).
+
+torch is imported first on purpose: torch ships its own libamdhip64.so (soname
+libamdhip64.so.7); loading it first makes the dynamic linker resolve our library's HIP
+runtime to the same copy, so streams and device pointers are shared.
+
+There is no fallback: if the library is missing or the device is not gfx950 the hot path
+raises, it never silently reroutes to a CPU implementation.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfo_hip.so")
+
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_float = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "fo_version": (c_int, []),
+    "fo_last_error": (c_int, [ctypes.c_char_p, c_int]),
+    "fo_device_info": (c_int, [c_int, ctypes.c_char_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_ll)]),
+    "fo_graph_begin": (c_int, [c_vp]),
+    "fo_graph_end": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
+    "fo_graph_launch": (c_int, [c_vp, c_vp]),
+    "fo_graph_destroy": (c_int, [c_vp]),
+    "fo_event_create": (c_int, [ctypes.POINTER(c_vp)]),
+    "fo_event_record": (c_int, [c_vp, c_vp]),
+    "fo_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
+    "fo_event_destroy": (c_int, [c_vp]),
+    "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
+    "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
+    "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),
+    "fo_gemm_workspace_floats": (c_ll, [c_int, c_int, c_int, c_int]),
+    "fo_gemm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                        c_vp, c_ll, c_vp, c_int, c_vp]),
+}
+
+_lib = None
+
+
+def declared_symbols():
+    """Every symbol include/fo_hip.h declares (kept in sync by tests/test_capi_symbols.py)."""
+    return list(_SIGS.keys())
+
+
+def register(name, restype, argtypes):
+    _SIGS[name] = (restype, argtypes)
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+
+
+def load(path=None):
+    """Load the shared library (no device calls are made here)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"libfo_hip.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the Freeze-Omni MI355X path has no CPU fallback)")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    for name, (rt, at) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = rt
+        fn.argtypes = at
+    _lib = lib
+    return lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(1024)
+    load().fo_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc != 0:
+        raise RuntimeError(f"{what or 'libfo_hip'} failed ({rc}): {last_error()}")
+    return rc
+
+
+def call(name, *args):
+    """Call a C-ABI entry and raise RuntimeError with fo_last_error() on failure."""
+    return check(getattr(load(), name)(*args), name)

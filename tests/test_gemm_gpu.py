@@ -1,0 +1,78 @@
+"""fo_gemm (packed-weight MFMA GEMM) vs a plain fp32 reference of the same op."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x_bf, w_bf, bias, act, resid):
+    y = x_bf.float() @ w_bf.float().t()
+    if bias is not None:
+        y = y + bias
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "silu":
+        y = torch.nn.functional.silu(y)
+    if resid is not None:
+        y = y + resid
+    return y
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (3, 100, 96), (16, 4608, 3584), (17, 3584, 18944), (40, 1024, 9216),
+                                   (64, 896, 896), (130, 272, 160), (7, 152, 32)])
+@pytest.mark.parametrize("act", ["none", "relu"])
+def test_gemm_matches_fp32(dev, M, N, K, act):
+    from fo.ops import PackedLinear
+    g = torch.Generator(device="cpu").manual_seed(M * 1000 + N + K)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    lin = PackedLinear(w.to(dev), b.to(dev))
+    y = lin(x.to(dev), act=act).cpu()
+    ref = _ref(x, w, b, act, None)
+    torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_gemm_residual_bf16_out(dev):
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(7)
+    M, N, K = 5, 300, 640
+    w = (torch.randn(N, K, generator=g) / 25).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    r = torch.randn(M, N, generator=g)
+    lin = PackedLinear(w.to(dev))
+    out = r.clone().to(dev)
+    lin(x.to(dev), out=out, residual=True)
+    torch.testing.assert_close(out.cpu(), _ref(x, w, None, "none", r), rtol=1e-4, atol=1e-4)
+    outb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    lin(x.to(dev), out=outb)
+    torch.testing.assert_close(outb.float().cpu(), _ref(x, w, None, "none", None), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 8, 33])
+def test_gemm_swiglu(dev, M):
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M)
+    N, K = 4864, 896
+    wg = (torch.randn(N, K, generator=g) / 30).to(torch.bfloat16)
+    wu = (torch.randn(N, K, generator=g) / 30).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    lin = PackedLinear(wg.to(dev), swiglu_up=wu.to(dev))
+    y = lin(x.to(dev)).cpu()
+    ref = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
+    torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_gemm_deterministic_splitk(dev):
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 4, 3584, 18944
+    w = (torch.randn(N, K, generator=g) / 100).to(torch.bfloat16).to(dev)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    lin = PackedLinear(w)
+    ys = [lin(x).cpu() for _ in range(5)]
+    for y in ys[1:]:
+        assert torch.equal(y, ys[0])
+    y1 = lin(x, splitk=1).cpu()
+    torch.testing.assert_close(y1, ys[0], rtol=1e-5, atol=1e-5)
