@@ -1,0 +1,472 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE implementation.
+
+This script is the only place that imports /root/reference (TheDoctor-JI/Freeze-Omni). It runs
+on CPU in the build container (the reference never travels to the GPU box); its outputs are
+small .npz/.json files of inputs and expected outputs.  Weights are counter-hash synthetic
+weights (oracle/weights.py), so only I/O is stored and every consumer regenerates the weights.
+
+Harness-side shims (the reference files are untouched), SURVEY.md §8(c):
+  shortuuid / logger.logger / soundfile / librosa / web.* stubs; torchaudio.compliance.kaldi.fbank
+  -> transformers.audio_utils kaldi restatement (torchaudio 2.2.0 is absent: parity of the kaldi
+  fbank itself is therefore pinned to transformers' documented restatement, not to torchaudio);
+  Tensor.to('cuda') no-op (models/encoder/transformer.py:279); DynamicCache legacy indexing
+  (models/audioLLM.py:417) and from_legacy_cache(None) (models/decoder/decoder.py:321);
+  LlamaDecoderLayer 4.45 call convention (past_key_value=, tuple return) with eager attention.
+The reference runs in fp32 on CPU (autocast('cuda') is inert there).
+
+Usage:  python tests/golden/make_golden.py
+"""
+import copy
+import functools
+import json
+import logging
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+from oracle import configs as C  # noqa: E402
+from oracle.weights import synth_param  # noqa: E402
+
+torch.set_grad_enabled(False)
+SHAPES = {}
+torch.manual_seed(0)
+
+
+# ----------------------------------------------------------------------------- shims
+def _mod(name, **attrs):
+    import importlib.machinery
+    m = types.ModuleType(name)
+    m.__spec__ = importlib.machinery.ModuleSpec(name, None)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+def install_shims():
+    # import third-party modules before any stub module exists (their availability probes)
+    import transformers  # noqa: F401
+    from transformers import AutoModelForCausalLM, AutoTokenizer, Qwen2ForCausalLM  # noqa: F401
+    from transformers.models.llama import modeling_llama  # noqa: F401
+    from transformers.models.qwen2 import modeling_qwen2  # noqa: F401
+    from transformers import audio_utils  # noqa: F401
+    _mod("shortuuid", uuid=lambda: "golden")
+    lg = _mod("logger")
+    lg.logger = _mod("logger.logger", setup_logger=lambda name, **kw: logging.getLogger(name))
+    _mod("soundfile", read=None, write=None)
+    _mod("librosa", load=None)
+    web = _mod("web")
+    web.parms = _mod("web.parms", GlobalParams=object)
+    web.pool = _mod("web.pool", TTSObjectPool=object)
+
+    from transformers.audio_utils import mel_filter_bank, spectrogram, window_function
+
+    def kaldi_fbank(waveform, dither=0.0, frame_length=25.0, frame_shift=10.0, num_mel_bins=23,
+                    sample_frequency=16000.0, **kw):
+        assert dither == 0.0 and not kw
+        wl = int(sample_frequency * frame_length * 0.001)
+        ws = int(sample_frequency * frame_shift * 0.001)
+        nfft = 1 << (wl - 1).bit_length()
+        mel = mel_filter_bank(num_frequency_bins=nfft // 2 + 1, num_mel_filters=num_mel_bins, min_frequency=20.0,
+                              max_frequency=sample_frequency / 2, sampling_rate=int(sample_frequency), norm=None,
+                              mel_scale="kaldi", triangularize_in_mel_space=True)
+        x = waveform.squeeze(0).double().numpy()
+        fb = spectrogram(x, window_function(wl, "povey", periodic=False), frame_length=wl, hop_length=ws,
+                         fft_length=nfft, power=2.0, center=False, preemphasis=0.97, mel_filters=mel,
+                         log_mel="log", mel_floor=1.1920928955078125e-07, remove_dc_offset=True).T
+        return torch.from_numpy(np.ascontiguousarray(fb)).float()
+
+    ta = _mod("torchaudio")
+    ta.compliance = _mod("torchaudio.compliance")
+    ta.compliance.kaldi = _mod("torchaudio.compliance.kaldi", fbank=kaldi_fbank)
+    ta.transforms = _mod("torchaudio.transforms")
+
+    _orig_to = torch.Tensor.to
+
+    def _to(self, *a, **k):
+        if a and isinstance(a[0], str) and a[0].startswith("cuda"):
+            return self
+        if isinstance(k.get("device"), str) and k["device"].startswith("cuda"):
+            k = dict(k)
+            k.pop("device")
+            if not a and not k:
+                return self
+        return _orig_to(self, *a, **k)
+
+    torch.Tensor.to = _to
+
+    from transformers import cache_utils
+    from transformers.models.llama import modeling_llama
+
+    def _getitem(self, i):
+        return (self.layers[i].keys, self.layers[i].values)
+
+    cache_utils.DynamicCache.__getitem__ = _getitem
+    cache_utils.DynamicCache.from_legacy_cache = classmethod(lambda cls, x=None: cls())
+
+    orig_fwd = modeling_llama.LlamaDecoderLayer.forward
+
+    def layer_fwd(self, hidden_states, attention_mask=None, position_ids=None, past_key_value=None,
+                  output_attentions=False, use_cache=False, cache_position=None, position_embeddings=None, **kw):
+        self.self_attn.config._attn_implementation = "eager"
+        h = orig_fwd(self, hidden_states, attention_mask=attention_mask, position_ids=position_ids,
+                     past_key_values=past_key_value, use_cache=use_cache, position_embeddings=position_embeddings)
+        return (h, past_key_value)
+
+    modeling_llama.LlamaDecoderLayer.forward = layer_fwd
+    sys.path.insert(0, REF)
+
+
+# ----------------------------------------------------------------------------- helpers
+def init_module(mod, seed, prefix="", overrides=None):
+    """Overwrite every parameter/buffer of `mod` with counter-hash values keyed by state_dict name."""
+    sd = mod.state_dict()
+    new = {}
+    for k, v in sd.items():
+        name = prefix + k
+        if v.dtype in (torch.int64, torch.long):
+            new[k] = v
+            continue
+        new[k] = torch.from_numpy(synth_param(seed, name, tuple(v.shape), overrides))
+    mod.load_state_dict(new)
+
+
+def canonical_llm_name(k):
+    """AudioLLM aliases llm_decoder.transformer = .model, .model.h = .layers, .model.wte = .embed_tokens
+    (models/audioLLM.py:104-109); every alias of a shared parameter gets the canonical name's values."""
+    if not k.startswith("llm_decoder."):
+        return k
+    n = k[len("llm_decoder."):]
+    if n.startswith("transformer."):
+        n = "model." + n[len("transformer."):]
+    n = n.replace("model.h.", "model.layers.").replace("model.wte.", "model.embed_tokens.")
+    return n
+
+
+def wav_question():
+    from scipy.io import wavfile
+    sr, x = wavfile.read(os.path.join(REF, "assets/question.wav"))
+    assert sr == 16000 and x.dtype == np.int16
+    return x.astype(np.float64) / 32768.0
+
+
+def synth_pcm(n, seed):
+    """Band-limited noise x 4 Hz syllabic AM at -20 dBFS, int16-quantised."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 16000.0
+    w = rng.standard_normal(n + 64)
+    w = np.convolve(w, np.hanning(33), mode="same")[:n]
+    w = w / (np.abs(w).max() + 1e-9)
+    am = 0.5 * (1 + np.sin(2 * np.pi * 4 * t))
+    x = 0.1 * w * am
+    return np.round(x * 32767) / 32768.0
+
+
+def tokenizer_dir():
+    """Byte-level BPE tokenizer without merges + Qwen chat specials (fixture data)."""
+    d = os.path.join(HERE, "tiny_tokenizer")
+    if os.path.exists(os.path.join(d, "tokenizer.json")):
+        return d
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers
+    from transformers import PreTrainedTokenizerFast
+    alphabet = pre_tokenizers.ByteLevel.alphabet()
+    vocab = {ch: i for i, ch in enumerate(sorted(alphabet))}
+    tok = Tokenizer(models.BPE(vocab=vocab, merges=[]))
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    fast = PreTrainedTokenizerFast(tokenizer_object=tok)
+    fast.add_special_tokens({"additional_special_tokens": ["<|im_start|>", "<|im_end|>"],
+                             "eos_token": "<|endoftext|>"})
+    os.makedirs(d, exist_ok=True)
+    fast.save_pretrained(d)
+    return d
+
+
+def tiny_llm_dir(cfg, tmp):
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    qc = Qwen2Config(**cfg["llm"], torch_dtype="float32")
+    m = Qwen2ForCausalLM(qc)
+    init_module(m, cfg["seed"], "", cfg["overrides"])
+    m.save_pretrained(tmp)
+    import shutil
+    for f in os.listdir(tokenizer_dir()):
+        shutil.copy(os.path.join(tokenizer_dir(), f), tmp)
+    return tmp
+
+
+# ----------------------------------------------------------------------------- goldens
+def gold_fbank():
+    sys.argv = ["golden"]
+    import bin.inference as binf  # noqa: the reference offline driver (framing A)
+    from models.AudioFeatureGating import AudioFeatureGating
+    import yaml
+    out = {}
+    x = wav_question()
+    proc = binf.audioEncoderProcessor()
+    CH = proc.get_chunk_size()
+    n = int(np.ceil(len(x) / CH) * CH)
+    xin = np.zeros(n)
+    xin[:len(x)] = x
+    feats = [proc.process(torch.tensor(xin[i:i + CH])).numpy()[0] for i in range(0, n, CH)]
+    out["A_pcm"] = xin.astype(np.float32)
+    out["A_feats"] = np.stack(feats).astype(np.float32)   # [13, 19, 80]
+    ycfg = yaml.safe_load(open(os.path.join(REF, "configs/dialog_state_pred_config.yaml")))
+    g = AudioFeatureGating(16000, 10, 0, ycfg["audio_feature_gating"]["fbank"])
+    CB = g.expected_frames_per_audio_chunk
+    pcm = synth_pcm(CB * 6, 99)
+    fb = []
+    for i in range(6):
+        chunk = (pcm[i * CB:(i + 1) * CB] * 32767.0 / 32767.0).astype(np.float32) / np.float32(1.0)
+        fb.append(g._extract_fbank(chunk).numpy()[0].copy())
+    out["B_pcm"] = pcm.astype(np.float32)
+    out["B_feats"] = np.stack(fb).astype(np.float32)     # [6, 32, 80]
+    # gating semantics (status None -> history only; ipu_* -> forwarded)
+    g2 = AudioFeatureGating(16000, 3, 2, ycfg["audio_feature_gating"]["fbank"])
+    statuses = [None, None, "ipu_sl", "ipu_cl", None, "ipu_el"]
+    gate = []
+    for i, st in enumerate(statuses):
+        r = g2.process_and_gate({"audio": pcm[i * CB:(i + 1) * CB].astype(np.float32), "status": st})
+        gate.append(None if r is None else {"status": r["status"], "feature": r["feature"],
+                                            "feature_last_chunk": r["feature_last_chunk"]})
+    np.savez_compressed(os.path.join(HERE, "fbank.npz"), **out)
+    with open(os.path.join(HERE, "gating.json"), "w") as f:
+        json.dump({"statuses": statuses, "cache_history_size": 3, "onset": 2, "gate": gate}, f)
+    print("fbank: A", out["A_feats"].shape, "B", out["B_feats"].shape)
+    return out
+
+
+def gold_audiollm(cfg, feats_a):
+    import tempfile
+    sys.argv = ["golden"]
+    from models.utils import init_encoder_llm
+    from models.encoder.cmvn import GlobalCMVN  # noqa: F401
+    tmp = tempfile.mkdtemp()
+    llm_dir = tiny_llm_dir(cfg, tmp)
+    ty = copy.deepcopy(cfg["train_yaml"])
+    ty["cmvn_file"] = None
+    ty["model_conf"]["llm_path"] = llm_dir
+    model = init_encoder_llm(ty, device="cpu")
+    # cmvn: construct with hashed stats (json cmvn file format is exercised by the host loader tests)
+    from models.encoder.cmvn import GlobalCMVN
+    d = 80
+    for enc in (model.encoder_user, model.encoder_system):
+        enc.global_cmvn = GlobalCMVN(torch.zeros(d), torch.ones(d))
+    # every parameter from the counter hash, keyed by the reference state_dict names
+    sd = model.state_dict()
+    new = {}
+    for k, v in sd.items():
+        name = canonical_llm_name(k)
+        if v.dtype == torch.long:
+            new[k] = v
+        else:
+            new[k] = torch.from_numpy(synth_param(cfg["seed"], name, tuple(v.shape), cfg["overrides"]))
+    model.load_state_dict(new)
+    model.eval()
+    SHAPES["audiollm"] = {("llm_decoder." + canonical_llm_name(k)) if k.startswith("llm_decoder.") else k:
+                          list(v.shape) for k, v in sd.items() if v.dtype != torch.long}
+    model.init_template_compilation = lambda: None
+    sce, scm = model.initialize_chat_template_embeds("system")
+    uce, ucm = model.initialize_chat_template_embeds("user")
+    model.system_chat_prefix_embeds, model.system_chat_prefix_mask = sce, scm
+    model.user_chat_prefix_embeds, model.user_chat_prefix_mask = uce, ucm
+
+    # capture intermediate tensors
+    cap = {}
+    orig_core = model._llm_forward_core
+
+    def core(inputs):
+        cap["embeds"] = inputs["inputs_embeds"].float().numpy().copy()
+        h, pkv = orig_core(inputs)
+        cap["hidden"] = h.float().numpy().copy()
+        return h, pkv
+
+    model._llm_forward_core = core
+    enc_out = {}
+    for ident in ("user", "system"):
+        enc = getattr(model, f"encoder_{ident}")
+        orig_infer = enc.infer
+
+        def infer(*a, _o=orig_infer, _id=ident, **k):
+            r = _o(*a, **k)
+            cap["enc"] = r[0].float().numpy().copy()
+            return r
+
+        enc.infer = infer
+    role = "You are a helpful assistant."
+    extra = {"identity": "", "status": "pre", "past_key_values": None, "adapter_cache": None,
+             "encoder_cache": None, "pe_index": 0, "role_prompt": "<|im_start|>system\n" + role}
+    pkv = model.set_system_role(extra)
+    res = {"role_ids": model.tokenizer([extra["role_prompt"]])["input_ids"][0],
+           "user_prefix_ids": [int(model.tokenizer.eod_id)] +
+           model.chat_template["prefix_for_user_utterance"][0].tolist(),
+           "system_prefix_ids": model.chat_template["prefix_for_system_utterance"][0].tolist(),
+           "eod_id": int(model.tokenizer.eod_id), "steps": []}
+    pre_hidden = cap["hidden"]
+    script = [("user", "ipu_sl"), ("user", "ipu_cl"), ("user", "ipu_cl"), ("user", "ipu_cl"),
+              ("system", "ipu_sl"), ("system", "ipu_cl"), ("user", "ipu_sl"), ("user", "ipu_cl"),
+              ("user", "ipu_cl"), ("user", "ipu_el")]
+    caches = {i: {"encoder_cache": None, "adapter_cache": None, "pe_index": 0} for i in ("user", "system")}
+    arrays = {"pre_hidden": pre_hidden}
+    for si, (ident, status) in enumerate(script):
+        x = torch.from_numpy(feats_a[si % len(feats_a)]).unsqueeze(0)
+        e = {"identity": ident, "status": status, "past_key_values": pkv, **caches[ident]}
+        probs, pkv, ac, ec, pe = model.recognize(x, e)
+        caches[ident] = {"encoder_cache": ec, "adapter_cache": ac, "pe_index": pe}
+        res["steps"].append({"identity": ident, "status": status, "probs": probs, "pe_index": pe,
+                             "kv_len": int(pkv.get_seq_length())})
+        arrays[f"s{si}_enc"] = cap["enc"][0]
+        arrays[f"s{si}_embeds"] = cap["embeds"][0]
+        arrays[f"s{si}_hidden"] = cap["hidden"][0]
+    for li in range(len(pkv.layers)):
+        arrays[f"kv{li}_k"] = pkv.layers[li].keys[0].float().numpy()
+        arrays[f"kv{li}_v"] = pkv.layers[li].values[0].float().numpy()
+    np.savez_compressed(os.path.join(HERE, "audiollm_tiny.npz"), feats=feats_a, **arrays)
+    with open(os.path.join(HERE, "audiollm_tiny.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("audiollm: steps", len(script), "kv_len", res["steps"][-1]["kv_len"])
+
+    # encoder-only run with RelPE wrap-around (pe_index near max_len)
+    enc = model.encoder_user
+    buf = [None] * enc.enc[1].num_blocks
+    pe = enc.enc[1].pe.max_len - 2 * enc.enc[1].chunk_size + 1
+    pe0 = pe
+    outs = []
+    for i in range(5):
+        o, buf, _, _, pe = enc.infer(torch.from_numpy(feats_a[i]).unsqueeze(0), buf, 0, None, pe)
+        outs.append(o[0].numpy().copy())
+    np.savez_compressed(os.path.join(HERE, "encoder_wrap_tiny.npz"), feats=feats_a[:5], out=np.stack(outs),
+                        pe0=np.array(pe0), max_len=np.array(enc.enc[1].pe.max_len))
+
+
+def gold_tts(cfg):
+    import argparse
+    from models.decoder.decoder import LLM2TTSCodecAR
+    idim, odim, args = cfg["decoder_json"]
+    m = LLM2TTSCodecAR(idim, odim, argparse.Namespace(**args))
+    init_module(m, cfg["seed"], "tts.", cfg["overrides"])
+    m.eval()
+    SHAPES["tts"] = {"tts." + k: list(v.shape) for k, v in m.state_dict().items()}
+    rng = np.random.default_rng(5)
+    T1, T2 = 9, 24   # text embeds rows (4 per text token at real geometry), LLM hidden rows
+    hidden = torch.from_numpy(rng.standard_normal((1, T1, idim)).astype(np.float32) * 0.5)
+    prefix = torch.from_numpy(rng.standard_normal((1, T2, idim)).astype(np.float32) * 0.5)
+    logits = []
+    orig = m.out_fnn.forward
+
+    def hook(x):
+        y = orig(x)
+        if len(logits) < 6:
+            logits.append(y[0, -1].numpy().copy())
+        return y
+
+    m.out_fnn.forward = hook
+    ids = [int(t) for t in m.infer(hidden, 1, prefix, -1, 1.1, max_tokens=150)]
+    m.out_fnn.forward = orig
+    np.savez_compressed(os.path.join(HERE, "tts_tiny.npz"), hidden=hidden[0].numpy(), prefix=prefix[0].numpy(),
+                        ids=np.array(ids, dtype=np.int64), logits=np.stack(logits))
+    print("tts: ids", len(ids), ids[:12])
+    return m
+
+
+def gold_codec(cfg, tts_model):
+    from models.decoder.ticodec.models import Generator, Quantizer
+    from models.decoder.ticodec.vqvae import VQVAE, AttrDict
+    from models.decoder.llm2tts import llm2TTS
+    h = AttrDict(cfg["codec_json"])
+    vq = VQVAE.__new__(VQVAE)
+    torch.nn.Module.__init__(vq)
+    vq.h = h
+    vq.quantizer = Quantizer(h)
+    vq.generator = Generator(h)
+    vq.generator.remove_weight_norm()
+    init_module(vq.quantizer, cfg["seed"], "codec.quantizer.")
+    init_module(vq.generator, cfg["seed"], "codec.generator.")
+    vq.eval()
+    SHAPES["codec"] = {**{"codec.quantizer." + k: list(v.shape) for k, v in vq.quantizer.state_dict().items()},
+                       **{"codec.generator." + k: list(v.shape) for k, v in vq.generator.state_dict().items()}}
+    rng = np.random.default_rng(11)
+    ids = torch.from_numpy(rng.integers(0, h.n_codes, size=(1, 60, 1)))
+    gt = torch.tensor(h.global_tokens).unsqueeze(0).unsqueeze(0)
+    pcm = vq(ids, gt)
+    np.savez_compressed(os.path.join(HERE, "codec_tiny.npz"), ids=ids[0, :, 0].numpy(), pcm=pcm[0, 0].numpy())
+    print("codec: pcm", tuple(pcm.shape))
+
+    # llm2TTS.run end to end (AR decode + 40/10 codec chunking + silence cut)
+    fake = llm2TTS.__new__(llm2TTS)
+    fake.model = tts_model
+    fake.infer = functools.partial(tts_model.infer, max_tokens=130)
+    fake.codec_model = types.SimpleNamespace(vqvae=vq)
+    t = np.load(os.path.join(HERE, "tts_tiny.npz"))
+    hidden = torch.from_numpy(t["hidden"]).unsqueeze(0)
+    prefix = torch.from_numpy(t["prefix"]).unsqueeze(0)
+    segs = [s[0, 0].float().numpy().copy() for s in fake.run(hidden, 1, prefix, 40, 10, -1, 1.1, 2401, 0.01)]
+    out = {f"seg{i}": s for i, s in enumerate(segs)}
+    np.savez_compressed(os.path.join(HERE, "llm2tts_run_tiny.npz"), n=np.array(len(segs)), **out)
+    print("llm2tts.run: segments", [len(s) for s in segs])
+
+    # find_min_sum_index on synthetic audio (quiet gaps force both branches)
+    cases = {}
+    r = np.random.default_rng(3)
+    for ci in range(4):
+        syn = r.standard_normal(24000).astype(np.float32) * (0.2 if ci % 2 == 0 else 0.002)
+        if ci == 2:
+            syn[15000:19000] *= 0.001
+        buf = r.standard_normal(1000 * ci).astype(np.float32) * 0.1
+        b2, s2 = llm2TTS.find_min_sum_index(None, torch.from_numpy(buf).view(1, 1, -1),
+                                            torch.from_numpy(syn).view(1, 1, -1), 2401, 0.01)
+        cases[f"c{ci}_syn"] = syn
+        cases[f"c{ci}_buf"] = buf
+        cases[f"c{ci}_outbuf"] = b2[0, 0].numpy()
+        cases[f"c{ci}_out"] = np.zeros(0, np.float32) if s2 is None else s2[0, 0].numpy()
+        cases[f"c{ci}_none"] = np.array(s2 is None)
+    np.savez_compressed(os.path.join(HERE, "silence_cut.npz"), **cases)
+
+
+def gold_text():
+    sys.argv = ["golden"]
+    from models.pipeline import inferencePipeline
+    texts = ["Hello world", "1. First item 2. second", "你好、世界（测试）", "Use *bold* and `code`~",
+             "Numbers: 3.14 are fine.", "Ends with comma,", "问题：\n是什么", "Line\tbreak\r\nhere;", ""]
+    outs = [inferencePipeline.post_process(None, t) for t in texts]
+    from models.ContextSerializer import ContextSerializer
+    cs = ContextSerializer()
+    events = [(0.00, "user", "ipu_sl"), (0.05, "system", "ipu_sl"), (0.10, "user", "ipu_cl"),
+              (0.12, "system", "ipu_cl"), (0.20, "user", "ipu_el"), (0.25, "system", "ipu_cl"),
+              (0.30, "system", "ipu_cl"), (0.35, "user", "ipu_sl"), (0.36, "system", "ipu_el"),
+              (0.40, "user", "ipu_el"), (0.45, "system", "ipu_sl")]
+    for i, (ts, ident, st) in enumerate(events):
+        cs.add_feature_chunk({"time_stamp": ts, "identity": ident, "status": st, "feature": [i], "ipu_id": i})
+    sent = []
+    while True:
+        if not cs.feature_queue:
+            break
+        sent.append(cs.get_next_feature())
+    with open(os.path.join(HERE, "text_and_serializer.json"), "w") as f:
+        json.dump({"texts": texts, "post_process": outs, "events": events, "serialized": sent}, f,
+                  ensure_ascii=False, indent=1)
+
+
+def main():
+    install_shims()
+    cfg = C.get("tiny")
+    fb = gold_fbank()
+    gold_audiollm(cfg, fb["A_feats"])
+    m = gold_tts(cfg)
+    gold_codec(cfg, m)
+    gold_text()
+    with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
+        json.dump(SHAPES, f)
+    total = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith((".npz", ".json")))
+    print(f"fixtures: {total / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
