@@ -16,14 +16,18 @@
 //    deterministic.
 //  * mfma_f32_16x16x32_bf16 accumulates in fp32; bias/activation/residual/SwiGLU are fused
 //    into the epilogue.
+#include <type_traits>
+
 #include "fo_common.h"
 
 namespace {
 
 struct GemmArgs {
-  const bf16_t* X;
+  const void* X;
   const bf16_t* Wp;
   const float* bias;
+  const float* scale;  // optional per-column affine after bias (folded eval BatchNorm)
+  const float* shift;
   void* Y;
   float* ws;
   int* counters;
@@ -34,8 +38,29 @@ struct GemmArgs {
   int act, out_bf16, residual;
 };
 
-template <int NT, int RB>
+// XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
+// bf16 weight fragment), so activations keep ~16 mantissa bits at unchanged weight traffic.
+template <typename XT, bool XF32>
+__device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
+  if constexpr (XF32) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const __bf16 h = (__bf16)f[j];
+      hi[j] = h;
+      lo[j] = (__bf16)(f[j] - (float)h);
+    }
+  } else {
+    hi = *reinterpret_cast<const bf16x8*>(p);
+  }
+}
+
+template <int NT, int RB, bool XF32>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
+  using XT = typename std::conditional<XF32, float, bf16_t>::type;
+  constexpr int U = (XF32 && RB == 4) ? 2 : 4;
   constexpr int ROWS = RB * 16;
   __shared__ float red[4][NT][ROWS][17];
   __shared__ int s_last;
@@ -59,34 +84,38 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; ++t)
     bp[t] = reinterpret_cast<const bf16x8*>(a.Wp) + (size_t)(tg * NT + t) * KS * 64 + lane;
-  const bf16_t* xr[RB];
+  const XT* xr[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
     int row = m0 + r * 16 + (lane & 15);
     if (row > a.M - 1) row = a.M - 1;  // clamp: rows >= M are computed but never stored
-    xr[r] = a.X + (size_t)row * a.ldx + 8 * (lane >> 4);
+    xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
 
   int ks = wb;
-  for (; ks + 4 <= we; ks += 4) {
-    bf16x8 bv[4][NT];
-    bf16x8 av[4][RB];
+  for (; ks + U <= we; ks += U) {
+    bf16x8 bv[U][NT];
+    bf16x8 ah[U][RB], al[U][RB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int t = 0; t < NT; ++t) bv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)(ks + u) * 64);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < RB; ++r)
-        if (r < rbeff) av[u][r] = *reinterpret_cast<const bf16x8*>(xr[r] + (size_t)(ks + u) * 32);
+        if (r < rbeff) load_x<XT, XF32>(xr[r] + (size_t)(ks + u) * 32, ah[u][r], al[u][r]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < RB; ++r)
-          if (r < rbeff) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+          if (r < rbeff) {
+            acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+            if constexpr (XF32)
+              acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+          }
   }
   for (; ks < we; ++ks) {
 #pragma unroll
@@ -95,8 +124,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < RB; ++r)
         if (r < rbeff) {
-          bf16x8 av = *reinterpret_cast<const bf16x8*>(xr[r] + (size_t)ks * 32);
-          acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc[t][r], 0, 0, 0);
+          bf16x8 h, l;
+          load_x<XT, XF32>(xr[r] + (size_t)ks * 32, h, l);
+          acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, b, acc[t][r], 0, 0, 0);
+          if constexpr (XF32) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(l, b, acc[t][r], 0, 0, 0);
         }
     }
   }
@@ -165,6 +196,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
     } else {
       v = red[0][0][rr][c];
       if (a.bias) v += a.bias[n];
+      if (a.scale) v = v * a.scale[n] + a.shift[n];
       v = apply_act(v, a.act);
     }
     const size_t o = (size_t)m * a.ldy + n;
@@ -238,16 +270,19 @@ long long fo_gemm_workspace_floats(int M, int N, int K, int swiglu) {
 
 // Y = act(X @ W^T + bias) (+Y if residual).  X bf16 [M][ldx], K % 32 == 0.
 // swiglu != 0: Wp holds interleaved (gate, up) tile pairs, Y[m][n] = silu(gate) * up, n < N.
-int fo_gemm(const void* X, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
-            void* Y, int ldy, int out_bf16, int act, int residual, float* ws, long long ws_floats,
-            int* counters, int splitk, hipStream_t stream) {
+int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
+            const float* scale, const float* shift, void* Y, int ldy, int out_bf16, int act, int residual, float* ws,
+            long long ws_floats, int* counters, int splitk, hipStream_t stream) {
   FO_REQUIRE(M > 0 && N > 0 && K > 0, "fo_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   FO_REQUIRE((K & 31) == 0, "fo_gemm: K=%d must be a multiple of 32", K);
   FO_REQUIRE(ldx >= K, "fo_gemm: ldx=%d < K=%d", ldx, K);
   FO_REQUIRE(ldy >= N, "fo_gemm: ldy=%d < N=%d", ldy, N);
-  FO_REQUIRE(!(swiglu && bias), "fo_gemm: swiglu with bias unsupported");
+  FO_REQUIRE(!(swiglu && (bias || scale)), "fo_gemm: swiglu with bias/affine unsupported");
+  FO_REQUIRE(!scale == !shift, "fo_gemm: scale and shift go together");
   GemmArgs a;
-  a.X = (const bf16_t*)X;
+  a.X = X;
+  a.scale = scale;
+  a.shift = shift;
   a.Wp = (const bf16_t*)Wp;
   a.bias = bias;
   a.Y = Y;
@@ -275,7 +310,11 @@ int fo_gemm(const void* X, int ldx, int M, int K, const void* Wp, int N, int swi
                ws_floats);
   }
   dim3 grid(groups, mt, S);
-#define FO_LAUNCH(NT_, RB_) hipLaunchKernelGGL((k_gemm<NT_, RB_>), grid, dim3(256), 0, stream, a)
+#define FO_LAUNCH(NT_, RB_)                                                                \
+  do {                                                                                     \
+    if (x_f32) hipLaunchKernelGGL((k_gemm<NT_, RB_, true>), grid, dim3(256), 0, stream, a);  \
+    else hipLaunchKernelGGL((k_gemm<NT_, RB_, false>), grid, dim3(256), 0, stream, a);       \
+  } while (0)
   if (NT == 1) {
     if (RB == 1) FO_LAUNCH(1, 1);
     else if (RB == 2) FO_LAUNCH(1, 2);

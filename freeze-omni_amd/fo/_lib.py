@@ -37,8 +37,39 @@ _SIGS = {
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),
     "fo_gemm_workspace_floats": (c_ll, [c_int, c_int, c_int, c_int]),
-    "fo_gemm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
-                        c_vp, c_ll, c_vp, c_int, c_vp]),
+    "fo_gemm": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
+                        c_int, c_int, c_vp, c_ll, c_vp, c_int, c_vp]),
+    "fo_fill_hash": (c_int, [c_vp, c_int, c_ll, ctypes.c_ulonglong, c_float, c_float, c_vp]),
+    "fo_rmsnorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
+    "fo_layernorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
+    "fo_gather_rows": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp]),
+    "fo_im2col_3x3s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
+                                c_vp]),
+    "fo_tcf_permute": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "fo_im2col_conv1d": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp]),
+    "fo_conv_cache_update": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "fo_state_head": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "fo_scale": (c_int, [c_vp, c_ll, c_float, c_vp]),
+    "fo_attn_nsplit": (c_int, [c_int]),
+    "fo_rope_kv_write": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                 c_int, c_vp]),
+    "fo_attention": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_float,
+                             c_int, c_vp, c_vp, c_vp, c_vp]),
+    "fo_enc_kv_write": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "fo_relpos_attention": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                    c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),
+    "fo_fbank": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
+                         c_int, c_vp, c_vp]),
+    "fo_rows_shift": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "fo_conv1d": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_float, c_vp,
+                          c_int, c_int, c_vp]),
+    "fo_conv_transpose1d": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_vp,
+                                    c_vp]),
+    "fo_codec_embed": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp]),
+    "fo_axpy": (c_int, [c_vp, c_vp, c_ll, c_vp]),
+    "fo_scale_add_channel": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
+    "fo_silence_cut": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

@@ -1,0 +1,148 @@
+"""Paged KV cache for the decoder stacks (Qwen2 in AudioLLM, Llama layers of the AR speech decoder).
+
+The reference keeps one transformers DynamicCache per session and grows it with torch.cat on every
+chunk (models/audioLLM.py:416-419, models/decoder/decoder.py:321); sessions deep-copy the system
+prompt cache (bin/dialog_state_pred.py:110,218).  Here every layer's K/V live in one device pool of
+fixed-size pages ([layer][page][kv_head][slot][hd], fp32).  A sequence is a block list; `fork()`
+shares full pages copy-on-write (refcounts), so N sessions forked from one system prompt store it
+once, and appending never moves existing keys.
+"""
+import numpy as np
+import torch
+
+
+class KVPool:
+    def __init__(self, n_layers, n_kv, hd, n_pages, page_size, device):
+        self.n_layers, self.n_kv, self.hd, self.PS = n_layers, n_kv, hd, page_size
+        self.n_pages = n_pages
+        self.k = torch.empty(n_layers, n_pages, n_kv, page_size, hd, dtype=torch.float32, device=device)
+        self.v = torch.empty_like(self.k)
+        self.ref = np.zeros(n_pages, dtype=np.int32)
+        self.free = list(range(n_pages - 1, -1, -1))
+        self.device = torch.device(device)
+
+    @property
+    def bytes_per_token(self):
+        return self.n_layers * self.n_kv * self.hd * 4 * 2
+
+    def alloc(self):
+        if not self.free:
+            raise RuntimeError(f"KV pool exhausted ({self.n_pages} pages of {self.PS} tokens)")
+        p = self.free.pop()
+        self.ref[p] = 1
+        return p
+
+    def release(self, p):
+        self.ref[p] -= 1
+        if self.ref[p] == 0:
+            self.free.append(p)
+
+    def copy_page(self, src, dst):
+        self.k[:, dst].copy_(self.k[:, src])
+        self.v[:, dst].copy_(self.v[:, src])
+
+    def pages_in_use(self):
+        return self.n_pages - len(self.free)
+
+
+class KVSeq:
+    """One sequence's view of a KVPool (block list + length)."""
+
+    def __init__(self, pool):
+        self.pool = pool
+        self.pages = []
+        self.length = 0
+
+    def reserve(self, new_len):
+        """Make room for new_len tokens; the page about to be written is made private (COW)."""
+        PS = self.pool.PS
+        if new_len > self.length and self.length % PS:
+            li = (self.length - 1) // PS  # page holding the partial tail that is about to grow
+            last = self.pages[li]
+            if self.pool.ref[last] > 1:
+                fresh = self.pool.alloc()
+                self.pool.copy_page(last, fresh)
+                self.pool.release(last)
+                self.pages[li] = fresh
+        while len(self.pages) * PS < new_len:
+            self.pages.append(self.pool.alloc())
+
+    def slot(self, pos):
+        PS = self.pool.PS
+        return self.pages[pos // PS] * PS + pos % PS
+
+    def fork(self):
+        n = KVSeq(self.pool)
+        n.pages = list(self.pages)
+        n.length = self.length
+        for p in n.pages:
+            self.pool.ref[p] += 1
+        return n
+
+    def truncate(self, new_len):
+        PS = self.pool.PS
+        keep = (new_len + PS - 1) // PS
+        for p in self.pages[keep:]:
+            self.pool.release(p)
+        self.pages = self.pages[:keep]
+        self.length = new_len
+
+    def free(self):
+        for p in self.pages:
+            self.pool.release(p)
+        self.pages = []
+        self.length = 0
+
+    def __del__(self):
+        try:
+            if self.pages:
+                self.free()
+        except Exception:
+            pass
+
+
+class BatchMeta:
+    """Device-side metadata of one ragged forward over several sequences.
+
+    entries: list of (KVSeq, n_new, rope_pos_start, causal).  Reserves KV for the new tokens and
+    advances each sequence's length.
+    """
+
+    def __init__(self, entries, device):
+        T = sum(n for _, n, _, _ in entries)
+        tok_seq = np.empty(T, np.int32)
+        tok_pos = np.empty(T, np.int32)
+        tok_slot = np.empty(T, np.int32)
+        tok_nvis = np.empty(T, np.int32)
+        maxb = 1
+        t = 0
+        last_rows = []
+        max_keys = 0
+        for s, (seq, n, p0, causal) in enumerate(entries):
+            old = seq.length
+            seq.reserve(old + n)
+            for i in range(n):
+                tok_seq[t] = s
+                tok_pos[t] = p0 + i
+                tok_slot[t] = seq.slot(old + i)
+                tok_nvis[t] = old + i + 1 if causal else old + n
+                t += 1
+            seq.length = old + n
+            maxb = max(maxb, len(seq.pages))
+            last_rows.append(t - 1)
+            max_keys = max(max_keys, seq.length)
+        bt = np.zeros((len(entries), maxb), np.int32)
+        for s, (seq, _, _, _) in enumerate(entries):
+            bt[s, :len(seq.pages)] = seq.pages
+        host = np.concatenate([tok_seq, tok_pos, tok_slot, tok_nvis, np.asarray(last_rows, np.int32), bt.ravel()])
+        dev = torch.from_numpy(host).to(device, non_blocking=True)
+        S = len(entries)
+        self.T, self.S, self.maxb, self.max_keys = T, S, maxb, max_keys
+        self.tok_seq = dev[0:T]
+        self.tok_pos = dev[T:2 * T]
+        self.tok_slot = dev[2 * T:3 * T]
+        self.tok_nvis = dev[3 * T:4 * T]
+        self.last_rows = dev[4 * T:4 * T + S]
+        self.block_table = dev[4 * T + S:].view(S, maxb)
+        self.last_rows_host = last_rows
+        self._host = host  # keep the staging buffer alive until the copy is consumed

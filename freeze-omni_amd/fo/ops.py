@@ -80,17 +80,179 @@ class PackedLinear:
     def nbytes(self):
         return self.packed.numel() * 2
 
+    def set_affine(self, scale, shift):
+        """Per-column y*scale+shift after the bias (eval BatchNorm, models/adapter.py:103-104)."""
+        self.scale = scale.detach().to(device=self.device, dtype=F32).contiguous()
+        self.shift = shift.detach().to(device=self.device, dtype=F32).contiguous()
+
+    scale = None
+    shift = None
+
     def __call__(self, x, out=None, act="none", residual=False, out_dtype=F32, splitk=0, M=None):
-        """x: bf16 [M, >=Kp] (row stride x.stride(0)); returns out [M, N]."""
+        """x: fp32 or bf16 [M, >=Kp] (row stride x.stride(0)); returns out [M, N]."""
         _check_dev(x)
-        if x.dtype != BF16:
-            raise TypeError("PackedLinear input must be bf16")
+        if x.dtype not in (BF16, F32):
+            raise TypeError("PackedLinear input must be fp32 or bf16")
+        if x.stride(-1) != 1 or x.shape[-1] < self.Kp:
+            raise ValueError(f"PackedLinear input needs unit stride and >= {self.Kp} columns, got {tuple(x.shape)}")
         M = x.shape[0] if M is None else M
         if out is None:
             out = torch.empty(M, self.N, dtype=out_dtype, device=x.device)
         rt = Runtime.get(x.device)
-        _lib.call("fo_gemm", x.data_ptr(), x.stride(0), M, self.Kp, self.packed.data_ptr(), self.N,
-                  1 if self.swiglu else 0, ptr(self.bias), out.data_ptr(), out.stride(0),
-                  1 if out.dtype == BF16 else 0, ACT[act], 1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(),
-                  rt.counters.data_ptr(), splitk, stream(x.device))
+        _lib.call("fo_gemm", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                  self.packed.data_ptr(), self.N, 1 if self.swiglu else 0, ptr(self.bias), ptr(self.scale),
+                  ptr(self.shift), out.data_ptr(), out.stride(0), 1 if out.dtype == BF16 else 0, ACT[act],
+                  1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
+                  stream(x.device))
         return out
+
+
+# ---------------------------------------------------------------- kernel wrappers
+I32 = torch.int32
+
+
+def fill_hash(out, key, center, scale):
+    _check_dev(out)
+    _lib.call("fo_fill_hash", out.data_ptr(), 1 if out.dtype == BF16 else 0, out.numel(), key & 0xFFFFFFFFFFFFFFFF,
+              float(center), float(scale), stream(out.device))
+    return out
+
+
+def rmsnorm(x, w, eps, out=None, round_fp16=False, M=None):
+    M = x.shape[0] if M is None else M
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("fo_rmsnorm", x.data_ptr(), x.stride(0), M, x.shape[1], w.data_ptr(), float(eps), out.data_ptr(),
+              out.stride(0), 1 if round_fp16 else 0, stream(x.device))
+    return out
+
+
+def layernorm(x, w, b, eps=1e-5, out=None, relu=False, M=None):
+    M = x.shape[0] if M is None else M
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("fo_layernorm", x.data_ptr(), x.stride(0), M, x.shape[1], w.data_ptr(), b.data_ptr(), float(eps),
+              out.data_ptr(), out.stride(0), 1 if relu else 0, stream(x.device))
+    return out
+
+
+def gather_rows(table, idx, out=None, round_fp16=False, D=None, M=None):
+    """out[m] = table[idx[m]] (idx None: identity).  table f32 or bf16 2-D."""
+    D = table.shape[1] if D is None else D
+    M = (idx.numel() if idx is not None else table.shape[0]) if M is None else M
+    if out is None:
+        out = torch.empty(M, D, dtype=F32, device=table.device)
+    _lib.call("fo_gather_rows", table.data_ptr(), 1 if table.dtype == BF16 else 0, table.stride(0), ptr(idx), M, D,
+              out.data_ptr(), out.stride(0), 1 if round_fp16 else 0, stream(table.device))
+    return out
+
+
+def im2col_3x3s2(x, B, C, H, W, strides, out, mean=None, istd=None):
+    _lib.call("fo_im2col_3x3s2", x.data_ptr(), B, C, H, W, *strides, ptr(mean), ptr(istd), out.data_ptr(),
+              out.stride(0), stream(x.device))
+    return out
+
+
+def tcf_permute(x, B, T, F, C, out):
+    _lib.call("fo_tcf_permute", x.data_ptr(), B, T, F, C, out.data_ptr(), stream(x.device))
+    return out
+
+
+def im2col_conv1d(cache, slots, x, B, KC, T, D, K, S, out):
+    _lib.call("fo_im2col_conv1d", ptr(cache), ptr(slots), x.data_ptr(), B, KC, T, D, K, S, out.data_ptr(),
+              out.stride(0), stream(x.device))
+    return out
+
+
+def conv_cache_update(cache, slots, x, B, KC, T, D):
+    _lib.call("fo_conv_cache_update", cache.data_ptr(), ptr(slots), x.data_ptr(), B, KC, T, D, stream(x.device))
+
+
+def state_head(h, rows, W, b, out):
+    _lib.call("fo_state_head", h.data_ptr(), h.stride(0), rows.data_ptr(), rows.numel(), W.data_ptr(), b.data_ptr(),
+              h.shape[1], out.data_ptr(), stream(h.device))
+    return out
+
+
+def scale_(x, s):
+    _lib.call("fo_scale", x.data_ptr(), x.numel(), float(s), stream(x.device))
+    return x
+
+
+def attn_nsplit(max_keys):
+    return _lib.load().fo_attn_nsplit(int(max_keys))
+
+
+def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS):
+    _lib.call("fo_rope_kv_write", qkv.data_ptr(), qkv.stride(0), T, H, KVH, hd, pos.data_ptr(), slot.data_ptr(),
+              cos_t.data_ptr(), sin_t.data_ptr(), q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(), PS,
+              stream(qkv.device))
+
+
+def attention(q, T, tok_seq, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit, part_ml, part_o, out):
+    _lib.call("fo_attention", q.data_ptr(), T, tok_seq.data_ptr(), tok_nvis.data_ptr(), block_table.data_ptr(),
+              block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd, float(scale), nsplit,
+              part_ml.data_ptr(), part_o.data_ptr(), out.data_ptr(), stream(q.device))
+    return out
+
+
+def enc_kv_write(k, v, B, T, d, start, length, ring, cap, kr, vr):
+    _lib.call("fo_enc_kv_write", k.data_ptr(), v.data_ptr(), k.stride(0), B, T, d, start.data_ptr(),
+              length.data_ptr(), ptr(ring), cap, kr.data_ptr(), vr.data_ptr(), stream(k.device))
+
+
+def relpos_attention(q, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out):
+    _lib.call("fo_relpos_attention", q.data_ptr(), q.stride(0), kr.data_ptr(), vr.data_ptr(), cap, start.data_ptr(),
+              length.data_ptr(), ptr(ring), ptab.data_ptr(), pstart.data_ptr(), bu.data_ptr(), bv.data_ptr(), B, T, h,
+              dk, float(scale), out.data_ptr(), out.stride(0), stream(q.device))
+    return out
+
+
+def fbank(samples, B, n_samples, wl, ws, nfft, window, tw_cos, tw_sin, mel, out, row0, zero_rows=None):
+    """samples [B][ld] -> out [B][R*nmel] rows row0.. (one per frame); frames < zero_rows[b] are zeroed."""
+    _lib.call("fo_fbank", samples.data_ptr(), samples.stride(0), B, n_samples, wl, ws, nfft, window.data_ptr(),
+              tw_cos.data_ptr(), tw_sin.data_ptr(), mel.data_ptr(), mel.shape[0], out.data_ptr(), out.stride(0),
+              row0, ptr(zero_rows), stream(samples.device))
+
+
+def rows_shift(feats, B, R, ov, D):
+    _lib.call("fo_rows_shift", feats.data_ptr(), B, R, ov, D, stream(feats.device))
+
+
+def conv1d(x, B, Cin, Tin, w, bias, Cout, K, dil, pad, out, pre_leaky=None, residual=False, post_tanh=False):
+    _lib.call("fo_conv1d", x.data_ptr(), B, Cin, Tin, w.data_ptr(), ptr(bias), Cout, K, dil, pad,
+              0 if pre_leaky is None else 1, 0.0 if pre_leaky is None else float(pre_leaky), out.data_ptr(),
+              1 if residual else 0, 1 if post_tanh else 0, stream(x.device))
+    return out
+
+
+def conv_transpose1d(x, B, Cin, Tin, w, bias, Cout, K, stride_, pad, out, slope=1.0):
+    _lib.call("fo_conv_transpose1d", x.data_ptr(), B, Cin, Tin, w.data_ptr(), ptr(bias), Cout, K, stride_, pad,
+              float(slope), out.data_ptr(), stream(x.device))
+    return out
+
+
+def codec_embed(table, ids, B, T, out):
+    _lib.call("fo_codec_embed", table.data_ptr(), table.shape[1], ids.data_ptr(), B, T, out.data_ptr(),
+              stream(table.device))
+    return out
+
+
+def axpy_(y, x):
+    _lib.call("fo_axpy", y.data_ptr(), x.data_ptr(), y.numel(), stream(y.device))
+    return y
+
+
+def scale_add_channel_(y, B, C, T, s, g=None):
+    _lib.call("fo_scale_add_channel", y.data_ptr(), B, C, T, float(s), ptr(g), stream(y.device))
+    return y
+
+
+def silence_cut(x, N, res):
+    _lib.call("fo_silence_cut", x.data_ptr(), x.numel(), N, res.data_ptr(), stream(x.device))
+    return res
+
+
+def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None):
+    B = logits.shape[0] if B is None else B
+    _lib.call("fo_sample", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), out_ids.data_ptr(), ptr(out_max), stream(logits.device))
+    return out_ids

@@ -1,0 +1,278 @@
+"""Streaming speech front end on the MI355X kernels: kaldi fbank framing, speech encoder, adapter.
+
+* Framer: the reference keeps a sample ring and a 3-frame feature carry per user
+  (bin/inference.py:43-80 framing A; models/AudioFeatureGating.py:33-75 framing B).  Here the host
+  keeps only the recent samples; the GPU recomputes the carried frames from them (identical values)
+  so no device feature state exists; the first chunk after reset carries zero frames, as the
+  reference's zero-initialised input_chunk does.
+* SpeechEncoderEngine: speechEncoder.infer (models/encoder/encoder.py:149-155) = GlobalCMVN +
+  Conv2dSubsampling4 (im2col + MFMA GEMMs) + rel-pos Transformer with a left-chunk KV ring per user
+  (models/encoder/transformer.py:266-285, attention.py:407-459).  linear_pos(sinusoid(p)) is
+  precomputed for every position at load (memory for compute: ~0.5 GB per encoder at REAL size).
+* AdapterEngine: CNNSubsampling single-conv branch with carried frames (models/adapter.py:112-157),
+  eval BatchNorm as a per-column affine GEMM epilogue.
+Batched: one launch sequence serves all users of a replica; per-user state lives in slot pools.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops, tables
+from .ops import F32, I32, PackedLinear
+
+FRAMINGS = {
+    # name: (chunk_frames, carried_frames, win, shift, nfft, scale)
+    "A": (16, 3, 400, 160, 512, 32768.0),   # bin/inference.py:44-52, x32768 (:74)
+    "B": (28, 4, 256, 128, 256, 32767.0),   # configs/dialog_state_pred_config.yaml:24-29, x32767 (AudioFeatureGating.py:58)
+}
+
+
+class Framer:
+    """Per-user host sample history for one framing."""
+
+    def __init__(self, kind="A"):
+        self.kind = kind
+        nf, ov, wl, ws, nfft, scale = FRAMINGS[kind]
+        self.chunk = nf * ws
+        self.R = nf + ov
+        self.window_len = (self.R - 1) * ws + wl
+        self.scale = np.float32(scale)
+        self.reset()
+
+    def reset(self):
+        self.hist = np.zeros(self.window_len, np.float32)
+        self.first = True
+
+    def push(self, pcm):
+        """pcm: one chunk of float samples in [-1, 1) (len == chunk).  Returns (window, first)."""
+        x = np.asarray(pcm, dtype=np.float32).reshape(-1)
+        if x.shape[0] != self.chunk:
+            raise ValueError(f"framing {self.kind}: expected {self.chunk} samples, got {x.shape[0]}")
+        self.hist = np.concatenate([self.hist[self.chunk:], x * self.scale])
+        first = self.first
+        self.first = False
+        return self.hist, first
+
+
+class FbankGPU:
+    def __init__(self, kind, device):
+        nf, ov, wl, ws, nfft, _ = FRAMINGS[kind]
+        self.nf, self.ov, self.wl, self.ws, self.nfft = nf, ov, wl, ws, nfft
+        self.R = nf + ov
+        self.n_samples = (self.R - 1) * ws + wl
+        w, c, s, m = tables.kaldi_tables(wl, nfft)
+        self.device = torch.device(device)
+        self.window, self.tw_cos, self.tw_sin, self.mel = (t.to(self.device) for t in (w, c, s, m))
+
+    def __call__(self, windows, firsts):
+        """windows: np.float32 [B][n_samples]; firsts: list[bool] -> device feats [B, R, 80]."""
+        B = len(firsts)
+        host = np.concatenate([np.ascontiguousarray(windows, np.float32).reshape(-1),
+                               np.asarray([self.ov if f else 0 for f in firsts], np.float32)])
+        dev = torch.from_numpy(host).to(self.device)
+        samples = dev[:B * self.n_samples].view(B, self.n_samples)
+        zero_rows = dev[B * self.n_samples:].to(I32)
+        out = torch.empty(B, self.R * 80, dtype=F32, device=self.device)
+        ops.fbank(samples, B, self.n_samples, self.wl, self.ws, self.nfft, self.window, self.tw_cos, self.tw_sin,
+                  self.mel, out, 0, zero_rows)
+        return out.view(B, self.R, 80)
+
+
+class SlotPool:
+    def __init__(self, n):
+        self.free = list(range(n - 1, -1, -1))
+        self.n = n
+
+    def get(self):
+        if not self.free:
+            raise RuntimeError(f"session slot pool exhausted ({self.n})")
+        return self.free.pop()
+
+    def put(self, s):
+        self.free.append(s)
+
+
+class EncoderCache:
+    """Caller-owned encoder state (the reference's `encoder_cache` buffer list): a ring slot."""
+
+    def __init__(self, engine):
+        self.engine, self.slot = engine, engine.slots.get()
+        self.start, self.len = 0, 0
+
+    def __del__(self):
+        try:
+            self.engine.slots.put(self.slot)
+        except Exception:
+            pass
+
+
+class SpeechEncoderEngine:
+    def __init__(self, src, cfg, ident, device, max_sessions=64):
+        ty = cfg["train_yaml"]
+        sub = ty["encoder_conf"]["para_conf"]["subsampling"]
+        tr = ty["encoder_conf"]["para_conf"]["transformer"]
+        p = f"encoder_{ident}."
+        self.device = torch.device(device)
+        self.C = sub["subsampling-output-dim"]
+        self.F = ((sub["subsampling-input-dim"] - 1) // 2 - 1) // 2
+        self.d = tr["transformer-attention-dim"]
+        self.h = tr["transformer-attention-heads"]
+        self.dk = self.d // self.h
+        self.nb = tr["transformer-num-blocks"]
+        self.chunk = tr["transformer-chunk_size"]
+        self.left = tr["transformer-left_chunks"]
+        self.buffersize = self.chunk * self.left
+        self.full_chunk = (self.left + 1) * self.chunk
+        self.max_len = self.chunk * (5000 // self.chunk) - self.full_chunk
+        self.cap = self.buffersize + 8
+        g = lambda n, dt=F32: src.get(p + n, dt)  # noqa: E731
+        self.mean, self.istd = g("global_cmvn.mean"), g("global_cmvn.istd")
+        self.conv1 = PackedLinear(g("enc.0.core.conv.0.weight", torch.bfloat16).reshape(self.C, 9),
+                                  g("enc.0.core.conv.0.bias"))
+        self.conv2 = PackedLinear(g("enc.0.core.conv.2.weight", torch.bfloat16).reshape(self.C, self.C * 9),
+                                  g("enc.0.core.conv.2.bias"))
+        self.out = PackedLinear(g("enc.0.core.out.0.weight", torch.bfloat16), g("enc.0.core.out.0.bias"))
+        self.embed = PackedLinear(g("enc.1.embed.0.weight", torch.bfloat16), g("enc.1.embed.0.bias"))
+        self.embed_ln = (g("enc.1.embed.1.weight"), g("enc.1.embed.1.bias"))
+        self.after = (g("enc.1.after_norm.weight"), g("enc.1.after_norm.bias"))
+        sinus = tables.relpos_sinusoid(self.max_len, self.d).to(self.device)
+        self.ptab = torch.empty(self.nb, self.max_len, self.d, dtype=F32, device=self.device)
+        self.layers = []
+        for i in range(self.nb):
+            q = f"enc.1.encoders.{i}."
+            L = {
+                "ln1": (g(q + "norm1.weight"), g(q + "norm1.bias")),
+                "ln2": (g(q + "norm2.weight"), g(q + "norm2.bias")),
+                "qkv": PackedLinear(torch.cat([g(q + f"self_attn.linear_{n}.weight", torch.bfloat16)
+                                               for n in "qkv"]),
+                                    torch.cat([g(q + f"self_attn.linear_{n}.bias") for n in "qkv"])),
+                "out": PackedLinear(g(q + "self_attn.linear_out.weight", torch.bfloat16),
+                                    g(q + "self_attn.linear_out.bias")),
+                "bu": g(q + "self_attn.pos_bias_u"), "bv": g(q + "self_attn.pos_bias_v"),
+                "ff1": PackedLinear(g(q + "feed_forward.w_1.weight", torch.bfloat16), g(q + "feed_forward.w_1.bias")),
+                "ff2": PackedLinear(g(q + "feed_forward.w_2.weight", torch.bfloat16), g(q + "feed_forward.w_2.bias")),
+            }
+            PackedLinear(g(q + "self_attn.linear_pos.weight", torch.bfloat16))(sinus, out=self.ptab[i])
+            self.layers.append(L)
+        del sinus
+        self.kr = torch.zeros(self.nb, max_sessions, self.cap, self.d, dtype=F32, device=self.device)
+        self.vr = torch.zeros_like(self.kr)
+        self.slots = SlotPool(max_sessions)
+
+    @property
+    def weight_bytes(self):
+        n = self.conv1.nbytes + self.conv2.nbytes + self.out.nbytes + self.embed.nbytes
+        for L in self.layers:
+            n += L["qkv"].nbytes + L["out"].nbytes + L["ff1"].nbytes + L["ff2"].nbytes
+        return n
+
+    def new_cache(self):
+        return EncoderCache(self)
+
+    def infer(self, feats, caches, pe_indices):
+        """feats: device [B, R, 80]; caches: list[EncoderCache]; pe_indices: list[int].
+        Returns (out [B*T, d] device fp32, T, new pe_indices)."""
+        B, R, _ = feats.shape
+        dev = self.device
+        H1, W1 = (R - 3) // 2 + 1, (80 - 3) // 2 + 1
+        H2, W2 = (H1 - 3) // 2 + 1, (W1 - 3) // 2 + 1
+        T = H2
+        assert W2 == self.F and T <= 8
+        C = self.C
+        x1 = torch.empty(B * H1 * W1, 32, dtype=F32, device=dev)
+        ops.im2col_3x3s2(feats, B, 1, R, 80, (R * 80, 0, 80, 1), x1, self.mean, self.istd)
+        y1 = self.conv1(x1, act="relu")
+        x2 = torch.empty(B * H2 * W2, self.conv2.Kp, dtype=F32, device=dev)
+        ops.im2col_3x3s2(y1, B, C, H1, W1, (H1 * W1 * C, 1, W1 * C, C), x2)
+        y2 = self.conv2(x2, act="relu")
+        z = torch.empty(B * T, C * self.F, dtype=F32, device=dev)
+        ops.tcf_permute(y2, B, T, self.F, C, z)
+        x = self.out(z)
+        x = self.embed(x)
+        ops.layernorm(x, *self.embed_ln, out=x, relu=True)
+        ops.scale_(x, math.sqrt(self.d))
+        # per-user ring / position metadata (host ints -> one small upload)
+        starts, lens, rings, pstarts, new_pe = [], [], [], [], []
+        for c, pe in zip(caches, pe_indices):
+            pe = pe % self.max_len
+            starts.append(c.start)
+            lens.append(c.len)
+            rings.append(c.slot)
+            pstarts.append(max(0, pe - self.full_chunk))
+            new_pe.append(pe + self.chunk)
+        meta = torch.from_numpy(np.asarray(starts + lens + rings + pstarts, np.int32)).to(dev)
+        st, ln, rg, ps = meta[:B], meta[B:2 * B], meta[2 * B:3 * B], meta[3 * B:]
+        h = torch.empty_like(x)
+        qkv = torch.empty(B * T, 3 * self.d, dtype=F32, device=dev)
+        att = torch.empty(B * T, self.d, dtype=F32, device=dev)
+        f = None
+        scale = 1.0 / math.sqrt(self.dk)
+        for i, L in enumerate(self.layers):
+            ops.layernorm(x, *L["ln1"], out=h)
+            L["qkv"](h, out=qkv)
+            ops.enc_kv_write(qkv[:, self.d:], qkv[:, 2 * self.d:], B, T, self.d, st, ln, rg, self.cap,
+                             self.kr[i], self.vr[i])
+            ops.relpos_attention(qkv, self.kr[i], self.vr[i], self.cap, st, ln, rg, self.ptab[i], ps, L["bu"],
+                                 L["bv"], B, T, self.h, self.dk, scale, att)
+            L["out"](att, out=x, residual=True)
+            ops.layernorm(x, *L["ln2"], out=h)
+            f = L["ff1"](h, out=f, act="relu")
+            L["ff2"](f, out=x, residual=True)
+        ops.layernorm(x, *self.after, out=x)
+        for c in caches:
+            total = c.len + T
+            keep = min(total, self.buffersize)
+            c.start = (c.start + total - keep) % self.cap
+            c.len = keep
+        return x, T, new_pe
+
+
+class AdapterCache:
+    """Caller-owned adapter state (the reference's `adapter_cache`): carried conv input frames."""
+
+    def __init__(self, engine):
+        self.engine, self.slot = engine, engine.slots.get()
+        engine.cache[self.slot].zero_()
+
+    def __del__(self):
+        try:
+            self.engine.slots.put(self.slot)
+        except Exception:
+            pass
+
+
+class AdapterEngine:
+    def __init__(self, src, cfg, ident, device, max_sessions=64):
+        mc = cfg["train_yaml"]["model_conf"]
+        self.d, self.L, self.k = mc["enc_out_dim"], mc["llm_embed_dim"], mc["kernel_size"]
+        p = f"adpter_{ident}."
+        self.device = torch.device(device)
+        w = src.get(p + "conv1d2.weight", torch.bfloat16)  # [2d, d, k] -> [2d, d*k] (col = c*k + j)
+        self.conv = PackedLinear(w.reshape(2 * self.d, self.d * self.k), src.get(p + "conv1d2.bias"))
+        g, b = src.get(p + "bn2.weight"), src.get(p + "bn2.bias")
+        rm, rv = src.get(p + "bn2.running_mean"), src.get(p + "bn2.running_var")
+        sc = g / torch.sqrt(rv + 1e-3)
+        self.conv.set_affine(sc, b - rm * sc)
+        self.project = PackedLinear(src.get(p + "project.weight", torch.bfloat16), src.get(p + "project.bias"))
+        self.cache = torch.zeros(max_sessions, self.k - 1, self.d, dtype=F32, device=self.device)
+        self.slots = SlotPool(max_sessions)
+
+    @property
+    def weight_bytes(self):
+        return self.conv.nbytes + self.project.nbytes
+
+    def new_cache(self):
+        return AdapterCache(self)
+
+    def __call__(self, x, T, caches):
+        """x: device [B*T, d]; returns (out [B*To, L], To)."""
+        B = len(caches)
+        KC = self.k - 1
+        To = (KC + T - self.k) // 2 + 1
+        slots = torch.tensor([c.slot for c in caches], dtype=I32).to(self.device)
+        cols = torch.empty(B * To, self.conv.Kp, dtype=F32, device=self.device)
+        ops.im2col_conv1d(self.cache, slots, x, B, KC, T, self.d, self.k, 2, cols)
+        ops.conv_cache_update(self.cache, slots, x, B, KC, T, self.d)
+        y = self.conv(cols, act="relu")
+        return self.project(y), To

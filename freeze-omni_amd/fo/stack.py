@@ -1,0 +1,80 @@
+"""Decoder-layer stacks on the MI355X kernels: Qwen2 (AudioLLM backbone) and the Llama layers of
+the AR speech decoder (pre_nn / layers_prefix / layers).
+
+Per layer (transformers Qwen2DecoderLayer / LlamaDecoderLayer, the call sites are
+models/audioLLM.py:479-484 and models/decoder/decoder.py:127-188,294-312):
+  rmsnorm -> fused QKV GEMM (+bias) -> RoPE + paged-KV append -> split-KV attention ->
+  O GEMM (+residual, in place) -> rmsnorm -> fused gate/up GEMM with SiLU*up epilogue ->
+  down GEMM (+residual, in place).
+The residual stream is fp32; GEMMs read it as fp32 (bf16 hi/lo split) against bf16 weights.
+"""
+import torch
+
+from . import ops
+from .kv import BatchMeta
+from .ops import F32, PackedLinear
+
+
+class Layer:
+    __slots__ = ("ln1", "ln2", "qkv", "o", "gu", "down")
+
+
+class DecoderStack:
+    def __init__(self, src, prefix, n_layers, D, H, KVH, eps, bias, rope, pool, kv_layer0=0, first_fp16=False):
+        self.n, self.D, self.H, self.KVH, self.hd, self.eps = n_layers, D, H, KVH, D // H, eps
+        self.cos, self.sin = rope
+        self.pool, self.kv_layer0, self.first_fp16 = pool, kv_layer0, first_fp16
+        self.layers = []
+        for i in range(n_layers):
+            q = f"{prefix}{i}."
+            L = Layer()
+            L.ln1 = src.get(q + "input_layernorm.weight")
+            L.ln2 = src.get(q + "post_attention_layernorm.weight")
+            wq = src.get(q + "self_attn.q_proj.weight", torch.bfloat16)
+            wk = src.get(q + "self_attn.k_proj.weight", torch.bfloat16)
+            wv = src.get(q + "self_attn.v_proj.weight", torch.bfloat16)
+            b = None
+            if bias:
+                b = torch.cat([src.get(q + "self_attn.q_proj.bias"), src.get(q + "self_attn.k_proj.bias"),
+                               src.get(q + "self_attn.v_proj.bias")])
+            L.qkv = PackedLinear(torch.cat([wq, wk, wv]), b)
+            del wq, wk, wv
+            L.o = PackedLinear(src.get(q + "self_attn.o_proj.weight", torch.bfloat16))
+            L.gu = PackedLinear(src.get(q + "mlp.gate_proj.weight", torch.bfloat16),
+                                swiglu_up=src.get(q + "mlp.up_proj.weight", torch.bfloat16))
+            L.down = PackedLinear(src.get(q + "mlp.down_proj.weight", torch.bfloat16))
+            self.layers.append(L)
+
+    @property
+    def weight_bytes(self):
+        return sum(L.qkv.nbytes + L.o.nbytes + L.gu.nbytes + L.down.nbytes for L in self.layers)
+
+    def forward(self, x, meta: BatchMeta):
+        """x: fp32 [T, D] residual stream, updated in place; KV for meta's tokens is appended."""
+        T = meta.T
+        H, KVH, hd = self.H, self.KVH, self.hd
+        dev = x.device
+        h = torch.empty(T, self.D, dtype=F32, device=dev)
+        qkv = torch.empty(T, (H + 2 * KVH) * hd, dtype=F32, device=dev)
+        q = torch.empty(T, H * hd, dtype=F32, device=dev)
+        att = torch.empty(T, H * hd, dtype=F32, device=dev)
+        nsplit = ops.attn_nsplit(meta.max_keys)
+        part_ml = torch.empty(T * H * nsplit * 2, dtype=F32, device=dev)
+        part_o = torch.empty(T * H * nsplit * hd, dtype=F32, device=dev)
+        m = None
+        scale = hd ** -0.5
+        for i, L in enumerate(self.layers):
+            li = self.kv_layer0 + i
+            ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=(self.first_fp16 and i == 0))
+            L.qkv(h, out=qkv)
+            ops.rope_kv_write(qkv, T, H, KVH, hd, meta.tok_pos, meta.tok_slot, self.cos, self.sin, q,
+                              self.pool.k[li], self.pool.v[li], self.pool.PS)
+            ops.attention(q, T, meta.tok_seq, meta.tok_nvis, meta.block_table, self.pool.PS, self.pool.k[li],
+                          self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o, att)
+            L.o(att, out=x, residual=True)
+            ops.rmsnorm(x, L.ln2, self.eps, out=h)
+            if m is None:
+                m = torch.empty(T, L.gu.N, dtype=F32, device=dev)
+            L.gu(h, out=m)
+            L.down(m, out=x, residual=True)
+        return x

@@ -41,9 +41,86 @@ int fo_pack_weight(const void* W, int src_bf16, int N, int K, int ldw, void* out
                    hipStream_t stream);
 int fo_gemm_pick_split(int M, int n_tile_groups, int K);
 long long fo_gemm_workspace_floats(int M, int N, int K, int swiglu);
-int fo_gemm(const void* X, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias, void* Y,
-            int ldy, int out_bf16, int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
-            hipStream_t stream);
+/* X: bf16 (x_f32=0) or fp32 (x_f32=1, split into bf16 hi+lo MFMA passes).  Epilogue order:
+ * +bias, *scale+shift (per column), activation (0 none,1 relu,2 silu,3 gelu), +Y if residual. */
+int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
+            const float* scale, const float* shift, void* Y, int ldy, int out_bf16, int act, int residual, float* ws,
+            long long ws_floats, int* counters, int splitk, hipStream_t stream);
+
+/* ---------------------------------------------------------------- memory-bound helpers (fo_elem.hip) */
+/* counter-hash synthetic weights, bit-identical to oracle/weights.py hash_uniform */
+int fo_fill_hash(void* out, int out_bf16, long long n, unsigned long long key, float center, float scale,
+                 hipStream_t s);
+/* Qwen2RMSNorm / LlamaRMSNorm (transformers, reached from models/audioLLM.py:482 and
+ * models/decoder/decoder.py:299-311,343); round_fp16 mirrors the cast back to an fp16 input dtype. */
+int fo_rmsnorm(const float* x, int ldx, int M, int D, const float* w, float eps, float* out, int ldo, int round_fp16,
+               hipStream_t s);
+/* torch.nn.LayerNorm (+ReLU) of the speech encoder (models/encoder/transformer.py:343-346,261,278,287) */
+int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const float* b, float eps, float* out, int ldo,
+                 int relu, hipStream_t s);
+/* embedding / row gather (wte at models/audioLLM.py:303,330; decoder embedding decoder.py:318,336) */
+int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,
+                   int ldo, int round_fp16, hipStream_t s);
+/* Conv2dSubsampling4 front end as im2col (+ fused GlobalCMVN) (models/encoder/subsampling.py:67-73,
+ * models/encoder/cmvn.py:24-35) */
+int fo_im2col_3x3s2(const float* in, int B, int C, int H, int W, long long sb, long long sc, long long sh,
+                    long long sw, const float* mean, const float* istd, float* out, int ldo, hipStream_t s);
+int fo_tcf_permute(const float* in, int B, int T, int F, int C, float* out, hipStream_t s);
+/* CNNSubsampling causal strided conv1d with carried frames (models/adapter.py:112-157) */
+int fo_im2col_conv1d(const float* cache, const int* slots, const float* x, int B, int KC, int T, int D, int K, int S,
+                     float* out, int ldo, hipStream_t s);
+int fo_conv_cache_update(float* cache, const int* slots, const float* x, int B, int KC, int T, int D, hipStream_t s);
+/* dialog-state head + 3-class softmax (models/audioLLM.py:486-493) */
+int fo_state_head(const float* h, int ldh, const int* rows, int S, const float* W, const float* bias, int D,
+                  float* probs, hipStream_t s);
+int fo_scale(float* x, long long n, float sc, hipStream_t s);
+
+/* ---------------------------------------------------------------- attention (fo_attn.hip) */
+int fo_attn_nsplit(int max_keys);
+/* RoPE (rotate_half, host cos/sin tables) + paged KV append: transformers apply_rotary_pos_emb +
+ * DynamicCache.update (models/audioLLM.py:416-419, models/decoder/decoder.py:146,305) */
+int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, const int* pos, const int* slot,
+                     const float* cos_t, const float* sin_t, float* q_out, float* kc, float* vc, int PS,
+                     hipStream_t s);
+/* GQA attention over paged KV for a ragged batch; token t sees the first tok_nvis[t] keys of its
+ * sequence (causal: own cache index + 1, full/unmasked: all).  Split-KV + combine. */
+int fo_attention(const float* q, int T, const int* tok_seq, const int* tok_nvis, const int* block_table, int maxb,
+                 int PS, const float* kc, const float* vc, int H, int KVH, int hd, float scale, int nsplit,
+                 float* part_ml, float* part_o, float* out, hipStream_t s);
+/* encoder MultiHeadedAttention.infer left-chunk buffer as a ring + rel-pos scores
+ * (models/encoder/attention.py:407-459) */
+int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,
+                    const int* ring, int cap, float* kr, float* vr, hipStream_t s);
+int fo_relpos_attention(const float* q, int ldq, const float* kr, const float* vr, int cap, const int* start,
+                        const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
+                        const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,
+                        hipStream_t s);
+
+/* ---------------------------------------------------------------- audio front end (fo_audio.hip) */
+/* kaldi fbank (torchaudio.compliance.kaldi.fbank at bin/inference.py:77-78, AudioFeatureGating.py:65-69) */
+int fo_fbank(const float* samples, int ld_s, int B, int n_samples, int wl, int ws, int nfft, const float* window,
+             const float* tw_cos, const float* tw_sin, const float* mel, int nmel, float* out, int ld_b, int row0,
+             const int* zero_rows, hipStream_t s);
+int fo_rows_shift(float* feats, int B, int R, int ov, int D, hipStream_t s);
+
+/* ---------------------------------------------------------------- codec (fo_codec.hip) */
+/* Generator convs (models/decoder/ticodec/models.py:59-166,211-242) */
+int fo_conv1d(const float* x, int B, int Cin, int Tin, const void* w, const float* bias, int Cout, int K, int dil,
+              int pad, int pre_leaky, float slope, float* out, int residual, int post_tanh, hipStream_t s);
+int fo_conv_transpose1d(const float* x, int B, int Cin, int Tin, const void* w, const float* bias, int Cout, int K,
+                        int stride, int pad, float slope, float* out, hipStream_t s);
+/* Quantizer.embed (models/decoder/ticodec/models.py:661-702) */
+int fo_codec_embed(const void* table, int E, const int* ids, int B, int T, float* out, hipStream_t s);
+int fo_axpy(float* y, const float* x, long long n, hipStream_t s);
+int fo_scale_add_channel(float* y, int B, int C, int T, float sc, const float* g, hipStream_t s);
+/* llm2TTS.find_min_sum_index window search (models/decoder/llm2tts.py:70-112): res = {min_sum, cut} */
+int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s);
+
+/* ---------------------------------------------------------------- sampling (fo_sample.hip) */
+/* AudioLLM._post_decode (models/audioLLM.py:431-477) / decoder top-k (models/decoder/decoder.py:353-359) */
+int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
+              const float* top_p, unsigned long long seed, const int* step, int* out_ids, float* out_maxlogit,
+              hipStream_t s);
 
 #ifdef __cplusplus
 }

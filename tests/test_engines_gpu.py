@@ -1,0 +1,198 @@
+"""HIP path (through the C-ABI) vs the CPU oracle, tiny geometry, bit-identical synthetic weights.
+
+Tolerances: the GPU keeps fp32 activations (bf16 hi/lo split into MFMA) against bf16 weights,
+so hidden states agree with the fp32 oracle to ~1e-4 relative; token ids must match exactly.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import audio, configs, host, nets
+from oracle.params import all_shapes
+from oracle.weights import SynthCheckpoint
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+CFG = configs.get("tiny")
+
+
+@pytest.fixture(scope="module")
+def W():
+    return SynthCheckpoint(CFG["seed"], all_shapes(CFG), CFG["overrides"])
+
+
+@pytest.fixture(scope="module")
+def src(dev):
+    from fo.weights import SynthSource
+    return SynthSource(CFG["seed"], all_shapes(CFG), dev, CFG["overrides"])
+
+
+def close(a, b, rtol=2e-3, atol=2e-4):
+    a = a.detach().float().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+def test_synth_weights_bit_identical(src, W):
+    for name in ["model.layers.0.self_attn.q_proj.weight", "encoder_user.global_cmvn.mean", "tts.out_fnn.weight",
+                 "codec.generator.ups.1.weight", "adpter_user.bn2.running_var"]:
+        g = src.get(name).cpu().numpy()
+        assert np.array_equal(g, W[name]), name
+
+
+@pytest.mark.parametrize("kind", ["A", "B"])
+def test_fbank_gpu_matches_oracle(dev, kind):
+    from fo.speech import FbankGPU, Framer
+    g = np.load(os.path.join(G, "fbank.npz"))
+    pcm = g[f"{kind}_pcm"]
+    fr = Framer(kind)
+    fb = FbankGPU(kind, dev)
+    ref = audio.EncoderFraming() if kind == "A" else audio.framing_b()
+    for i in range(len(pcm) // fr.chunk):
+        chunk = pcm[i * fr.chunk:(i + 1) * fr.chunk]
+        win, first = fr.push(chunk)
+        out = fb(win[None], [first])[0]
+        close(out, ref.process(chunk)[0], rtol=1e-4, atol=2e-3)
+        close(out, g[f"{kind}_feats"][i], rtol=1e-4, atol=2e-3)
+
+
+def test_encoder_adapter_stream_matches_oracle(dev, src, W):
+    from fo.speech import AdapterEngine, SpeechEncoderEngine
+    feats = np.load(os.path.join(G, "audiollm_tiny.npz"))["feats"]
+    enc = SpeechEncoderEngine(src, CFG, "user", dev, max_sessions=4)
+    ada = AdapterEngine(src, CFG, "user", dev, max_sessions=4)
+    oe, oa = nets.Encoder(W, CFG, "user"), nets.Adapter(W, CFG, "user")
+    # two interleaved users, different start positions (exercises batching, ring wrap, pe offsets)
+    caches = [enc.new_cache(), enc.new_cache()]
+    acs = [ada.new_cache(), ada.new_cache()]
+    pes = [0, 4980]
+    ost = [nets.new_encoder_state(oe.nb), nets.new_encoder_state(oe.nb)]
+    ost[1]["pe"] = 4980
+    oac = [None, None]
+    for step in range(8):
+        x = torch.from_numpy(np.stack([feats[step], feats[(step + 5) % 13]])).to(dev)
+        out, T, pes = enc.infer(x, caches, pes)
+        emb, To = ada(out, T, acs)
+        for u in range(2):
+            e = oe.infer(feats[step] if u == 0 else feats[(step + 5) % 13], ost[u])
+            a, oac[u] = oa(e, oac[u])
+            close(out[u * T:(u + 1) * T], e)
+            close(emb[u * To:(u + 1) * To], a, atol=5e-4)
+            assert pes[u] == ost[u]["pe"]
+
+
+def test_llm_streaming_state_probs_match_golden(dev, src, W):
+    """Replays the reference's AudioLLM golden (system role, user/system chunks) on the GPU engines."""
+    from fo.llm import LLMEngine
+    meta = json.load(open(os.path.join(G, "audiollm_tiny.json")))
+    g = np.load(os.path.join(G, "audiollm_tiny.npz"))
+    llm = LLMEngine(src, CFG["llm"], dev, kv_tokens=1024, page_size=16)
+    seq = llm.new_seq()
+    x = llm.embed(meta["role_ids"], round_fp16=True)
+    h, _ = llm.forward(x, [(seq, x.shape[0])])
+    close(h, g["pre_hidden"][0], atol=5e-4)
+    for si, step in enumerate(meta["steps"]):
+        emb = torch.from_numpy(g[f"s{si}_embeds"]).to(dev)  # adapter output (+prefix) from the reference
+        x = emb.half().float()
+        h, bm = llm.forward(x, [(seq, x.shape[0])])
+        close(h, g[f"s{si}_hidden"], atol=1e-3)
+        assert seq.length == step["kv_len"]
+        if step["probs"] is not None:
+            p = llm.state_probs(h, [x.shape[0] - 1]).cpu().numpy()[0]
+            assert abs(p[1] - step["probs"]["state_1"]) < 2e-4
+            assert abs(p[2] - step["probs"]["state_2"]) < 2e-4
+
+
+def test_llm_batched_sequences_independent(dev, src, W):
+    """Two sessions forked from one system prompt (COW pages) match the oracle run separately."""
+    from fo.llm import LLMEngine
+    meta = json.load(open(os.path.join(G, "audiollm_tiny.json")))
+    llm = LLMEngine(src, CFG["llm"], dev, kv_tokens=2048, page_size=16)
+    base = llm.new_seq()
+    x = llm.embed(meta["role_ids"], round_fp16=True)
+    llm.forward(x, [(base, x.shape[0])])
+    a, b = base.fork(), base.fork()
+    q = nets.Qwen2(W, CFG)
+    okv = nets.KV(CFG["llm"]["num_hidden_layers"])
+    q.forward(q.embed(meta["role_ids"]), okv)
+    okv_a, okv_b = okv.copy(), okv.copy()
+    rng = np.random.default_rng(0)
+    for it in range(3):
+        ea = rng.standard_normal((2 + it, 128)).astype(np.float32)
+        eb = rng.standard_normal((7, 128)).astype(np.float32)
+        xx = torch.from_numpy(np.concatenate([ea, eb])).to(dev).half().float()
+        h, bm = llm.forward(xx, [(a, ea.shape[0]), (b, eb.shape[0])])
+        ha, hb = q.forward(ea, okv_a), q.forward(eb, okv_b)
+        close(h[:ea.shape[0]], ha, atol=1e-3)
+        close(h[ea.shape[0]:], hb, atol=1e-3)
+    lg = llm.logits(h, [ea.shape[0] - 1, h.shape[0] - 1]).cpu().numpy()
+    np.testing.assert_allclose(lg[0], q.logits(ha[-1:])[0], rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(lg[1], q.logits(hb[-1:])[0], rtol=1e-3, atol=1e-3)
+    a.free()
+    b.free()
+    base.free()
+    assert llm.pool.pages_in_use() == 0
+
+
+def test_tts_greedy_ids_match_golden(dev, src, W):
+    from fo.tts import TTSEngine
+    t = np.load(os.path.join(G, "tts_tiny.npz"))
+    eng = TTSEngine(src, CFG["decoder_json"], dev, kv_tokens=4096)
+    seqs = eng.start([(torch.from_numpy(t["hidden"]).to(dev), torch.from_numpy(t["prefix"]).to(dev))])
+    cur = torch.full((1,), eng.sos, dtype=torch.int32, device=dev)
+    ids = []
+    from fo import ops
+    for i in range(150):
+        lg = eng.step(seqs, cur)
+        if i < 6:
+            close(lg[0], t["logits"][i], atol=5e-4)
+        nxt = ops.sample(lg, eng.vocab + 4, torch.empty(1, dtype=torch.int32, device=dev))
+        v = int(nxt.item())
+        if v == eng.eos:
+            break
+        ids.append(v)
+        cur = nxt
+    assert ids == t["ids"].tolist()
+    eng.free(seqs)
+
+
+def test_codec_matches_golden(dev, src, W):
+    from fo.codec import CodecEngine
+    g = np.load(os.path.join(G, "codec_tiny.npz"))
+    eng = CodecEngine(src, CFG["codec_json"], dev)
+    ids = torch.from_numpy(np.stack([g["ids"], g["ids"][::-1].copy()])).to(dev, torch.int32)
+    pcm = eng(ids)
+    close(pcm[0], g["pcm"], atol=5e-5)
+    close(pcm[1], nets.Codec(W, CFG)(g["ids"][::-1]), atol=5e-5)
+
+
+def test_silence_cut_kernel_matches_golden(dev):
+    from fo import ops
+    g = np.load(os.path.join(G, "silence_cut.npz"))
+    for ci in range(4):
+        syn = g[f"c{ci}_syn"]
+        res = ops.silence_cut(torch.from_numpy(syn).to(dev), 2401, torch.empty(2, device=dev)).cpu().numpy()
+        b2, s2 = host.find_min_sum_index(g[f"c{ci}_buf"], syn, 2401, 0.01)
+        assert (res[0] / 2401 < 0.01) == (s2 is not None)
+        if s2 is not None:
+            assert int(res[1]) == len(s2) - len(g[f"c{ci}_buf"])
+
+
+def test_sampler_topk_topp(dev):
+    from fo import ops
+    V = 1000
+    lg = torch.randn(4, V, device=dev)
+    ids = ops.sample(lg, V, torch.empty(4, dtype=torch.int32, device=dev)).cpu()
+    assert torch.equal(ids.long(), lg.argmax(-1).cpu())
+    k = torch.tensor([5, 5, 1, 64], dtype=torch.int32, device=dev)
+    T = torch.tensor([0.7, 1.0, 1.0, 1.0], device=dev)
+    p = torch.tensor([0.8, 0.0, 0.0, 0.9], device=dev)
+    for step in range(20):
+        st = torch.full((4,), step, dtype=torch.int32, device=dev)
+        ids = ops.sample(lg, V, torch.empty(4, dtype=torch.int32, device=dev), k, T, p, seed=1, step=st).cpu()
+        for r in range(4):
+            topk = lg[r].topk(int(k[r])).indices.cpu()
+            assert int(ids[r]) in topk.tolist()
+        assert int(ids[2]) == int(lg[2].argmax())

@@ -64,6 +64,24 @@ def test_gemm_swiglu(dev, M):
     torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 3584, 3584), (9, 4608, 3584), (40, 1024, 9216), (100, 64, 288)])
+def test_gemm_fp32_activations_split(dev, M, N, K):
+    """fp32 X is split into bf16 hi+lo: error vs an fp64 reference ~1e-5 relative (not bf16's ~4e-3)."""
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M + N)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g)
+    b = torch.randn(N, generator=g)
+    sc = torch.rand(N, generator=g) + 0.5
+    sh = torch.randn(N, generator=g)
+    lin = PackedLinear(w.to(dev), b.to(dev))
+    lin.set_affine(sc, sh)
+    y = lin(x.to(dev), act="relu").cpu().double()
+    ref = torch.relu((x.double() @ w.double().t() + b.double()) * sc.double() + sh.double())
+    err = (y - ref).abs().max().item()
+    assert err < 2e-4 * ref.abs().max().item(), err
+
+
 def test_gemm_deterministic_splitk(dev):
     from fo.ops import PackedLinear
     g = torch.Generator().manual_seed(3)
