@@ -1,0 +1,364 @@
+#!/usr/bin/env python3
+"""Freeze-Omni MI355X benchmark: streaming speech-to-speech turns for N users per GPU.
+
+metric (BASELINE.json): real-time factor + p50 first-audio-chunk latency, Qwen2-7B, N users/GPU.
+
+One "step" = one full dialogue turn for every user on every rank (SURVEY.md §8(d) config 3 per GPU):
+  listen : 10 s of synthetic 16 kHz PCM per user streamed in 160 ms chunks (framing A, 63 chunks);
+           each chunk = fbank -> speech encoder -> adapter -> Qwen2-7B chunk prefill (per-user paged KV
+           forked from a shared system prompt) -> dialog-state head (host read each chunk, as the reference)
+  speak  : dialog_ss -> assistant-prefix prefill + 8 text tokens (benchmark policy: one sentence of 8
+           tokens) -> AR speech decoder (EOS masked until 400 codec tokens = 10 s of 24 kHz audio) ->
+           TiCodec vocoder per 40(+10+10) tokens -> silence-cut emission.
+value = seconds of 24 kHz speech emitted by all users on all ranks / max-over-ranks wall seconds
+(aggregate real-time factor, higher is better).  Also reported: per-user RTF (audio / (dialog_ss ->
+last PCM)), p50/p90 first-audio latency (dialog_ss -> first PCM yield).
+Weights: counter-hash synthetic weights at Qwen2-7B / paper geometry (configs/real), generated on
+device; no checkpoint is on the box.  Launch for N>1 with torch.distributed.run (one rank per GPU).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "freeze-omni_amd"))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--users", type=int, default=8, help="concurrent users per GPU")
+    ap.add_argument("--config", default="real", choices=["real", "tiny"])
+    ap.add_argument("--input-sec", type=float, default=10.0)
+    ap.add_argument("--text-tokens", type=int, default=8)
+    ap.add_argument("--codec-tokens", type=int, default=400)
+    ap.add_argument("--top-k", type=int, default=1, help="speech decoder top_k (1 = parity/greedy)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def synth_pcm(n, seed):
+    """band-limited noise x 4 Hz syllabic AM at -20 dBFS, int16-quantised."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 16000.0
+    w = np.convolve(rng.standard_normal(n + 64), np.hanning(33), mode="same")[:n]
+    w = w / (np.abs(w).max() + 1e-9)
+    x = 0.1 * w * 0.5 * (1 + np.sin(2 * np.pi * 4 * t))
+    return (np.round(x * 32767) / 32768.0).astype(np.float32)
+
+
+class Turn:
+    """Per-user state of one dialogue turn."""
+
+    def __init__(self, engine, base_kv, pcm):
+        from fo.speech import Framer
+        self.kv = base_kv.fork()
+        self.framer = Framer("A")
+        self.pcm = pcm
+        self.enc_cache = self.ada_cache = None
+        self.pe = 0
+
+
+def run_turn(engine, base_kv, pcms, args, sync):
+    import torch
+    from fo.speak import speak
+    B = len(pcms)
+    turns = [Turn(engine, base_kv, p) for p in pcms]
+    fb = engine.fbank("A")
+    CH = turns[0].framer.chunk
+    n_chunks = int(math.ceil(len(pcms[0]) / CH))
+    for c in range(n_chunks):
+        wins, firsts = [], []
+        for t in turns:
+            seg = t.pcm[c * CH:(c + 1) * CH]
+            if len(seg) < CH:
+                seg = np.pad(seg, (0, CH - len(seg)))
+            w, f = t.framer.push(seg)
+            wins.append(w)
+            firsts.append(f)
+        feats = fb(np.stack(wins), firsts)
+        items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=feats[b], kv=t.kv,
+                      enc_cache=t.enc_cache, ada_cache=t.ada_cache, pe_index=t.pe) for b, t in enumerate(turns)]
+        res = engine.listen(items)
+        for t, r in zip(turns, res):
+            t.enc_cache, t.ada_cache, t.pe = r["enc_cache"], r["ada_cache"], r["pe_index"]
+    # ---- dialog_ss (benchmark policy forces it at end of input, as bin/inference.py:138 does)
+    sync()
+    t_ss = time.perf_counter()
+    eod = engine.tokenizer.eod_id
+    pre = engine.prefix_ids["system"]
+    text_ids = [[] for _ in turns]
+    hiddens = []
+    nxt, hid = engine.text_step([(t.kv, pre) for t in turns])
+    for _ in range(args.text_tokens):
+        hiddens.append(hid)
+        for b in range(B):
+            text_ids[b].append(nxt[b] if nxt[b] != eod else 0)
+        if len(hiddens) == args.text_tokens:
+            break
+        nxt, hid = engine.text_step([(t.kv, [text_ids[b][-1]]) for b, t in enumerate(turns)])
+    D = engine.llm.D
+    idim = engine.cfg["decoder_json"][0]
+    items = []
+    ids_d = torch.tensor(text_ids, dtype=torch.int32).to(engine.device)
+    emb = engine.llm.embed(ids_d.view(-1))
+    hs = torch.stack(hiddens, 1)  # [B, T', D]
+    for b in range(B):
+        e = emb[b * args.text_tokens:(b + 1) * args.text_tokens].reshape(-1, idim).contiguous()
+        p = hs[b].reshape(-1, idim).contiguous()
+        items.append((e, p))
+    first = [None] * B
+    last = [None] * B
+    samples = [0] * B
+    for i, seg in speak(engine, items, top_k=args.top_k, min_tokens=args.codec_tokens,
+                        max_tokens=args.codec_tokens):
+        now = time.perf_counter()  # the segment's length is known on the host: the cut index was read back
+        if first[i] is None:
+            first[i] = now
+        last[i] = now
+        samples[i] += seg.numel()
+    for t in turns:
+        t.kv.free()
+    return dict(t_ss=t_ss, first=first, last=last, samples=samples)
+
+
+def cpu_baseline(cfg_name, threads, seconds_audio, n_chunks, text_tokens, codec_tokens):
+    """Oracle (numpy port) timed on host cores on a bounded sample at REAL geometry, scaled to the
+    metric: per-unit costs U1 (chunk step), U2 (text token), U3 (codec token), U4 (vocoder call)
+    measured on a subset of layers and extrapolated linearly in layer count."""
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    sys.path.insert(0, ROOT)
+    from oracle import configs, nets, params
+    cfg = configs.get(cfg_name)
+    rng = np.random.default_rng(0)
+    n_llm = cfg["llm"]["num_hidden_layers"]
+    n_enc = cfg["train_yaml"]["encoder_conf"]["para_conf"]["transformer"]["transformer-num-blocks"]
+    sub = {"llm": 2, "enc": 2}
+    c2 = configs.get(cfg_name)
+    c2["llm"]["num_hidden_layers"] = sub["llm"]
+    c2["train_yaml"]["encoder_conf"]["para_conf"]["transformer"]["transformer-num-blocks"] = sub["enc"]
+
+    class Rand(dict):
+        def __init__(self, shapes):
+            super().__init__()
+            self.shapes = shapes
+
+        def __missing__(self, k):
+            shp = self.shapes[k]
+            v = (rng.standard_normal(shp, dtype=np.float32) * (0.02 if len(shp) > 1 else 0.1)).astype(np.float32)
+            if k.endswith(("norm.weight", "norm1.weight", "norm2.weight", "layernorm.weight")) or "running_var" in k \
+                    or "istd" in k:
+                v = np.abs(v) + 1.0
+            self[k] = v
+            return v
+
+    W = Rand(params.all_shapes(c2))
+    enc, ada = nets.Encoder(W, c2, "user"), nets.Adapter(W, c2, "user")
+    llm = nets.Qwen2(W, c2)
+    feats = rng.standard_normal((19, 80)).astype(np.float32) * 3 + 8
+    kv = nets.KV(sub["llm"])
+    llm.forward(rng.standard_normal((40, c2["llm"]["hidden_size"])).astype(np.float32), kv)
+    est = nets.new_encoder_state(sub["enc"])
+    ac = None
+    t = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        e = enc.infer(feats, est)
+        a, ac = ada(e, ac)
+        llm.forward(a, kv)
+    u1_sub = (time.perf_counter() - t) / reps
+    # split the measured sub-stack time into encoder and LLM parts to extrapolate each
+    t = time.perf_counter()
+    for _ in range(reps):
+        enc.infer(feats, est)
+    u1_enc = (time.perf_counter() - t) / reps
+    u1 = u1_enc * n_enc / sub["enc"] + (u1_sub - u1_enc) * n_llm / sub["llm"]
+    t = time.perf_counter()
+    for _ in range(reps):
+        h = llm.forward(rng.standard_normal((1, c2["llm"]["hidden_size"])).astype(np.float32), kv)
+    u2_layers = (time.perf_counter() - t) / reps
+    t = time.perf_counter()
+    llm.logits(h)
+    u2 = u2_layers * n_llm / sub["llm"] + (time.perf_counter() - t)
+    tts = nets.TTSDecoder(W, c2)
+    idim = c2["decoder_json"][0]
+    kvt, P = tts.prefill(rng.standard_normal((32, idim)).astype(np.float32),
+                         rng.standard_normal((32, idim)).astype(np.float32))
+    t = time.perf_counter()
+    n3 = 5
+    for i in range(n3):
+        tts.step(5 + i, kvt, P)
+    u3 = (time.perf_counter() - t) / n3
+    codec = nets.Codec(W, c2)
+    t = time.perf_counter()
+    codec(rng.integers(0, c2["codec_json"]["n_codes"], 60))
+    u4 = time.perf_counter() - t
+    n_voc = 1 + max(0, (codec_tokens - 50 + 39) // 40)
+    turn = n_chunks * u1 + text_tokens * u2 + codec_tokens * u3 + n_voc * u4
+    speak = text_tokens * u2 + codec_tokens * u3 + n_voc * u4
+    return {"value": round(seconds_audio / turn, 4), "unit": "x real-time (1 user, 1 turn)", "cores": threads,
+            "kind": "port",
+            "sample": (f"numpy fp32 oracle at REAL geometry on {threads} host threads; per-unit times measured on "
+                       f"{sub['llm']}/{n_llm} Qwen2 layers and {sub['enc']}/{n_enc} encoder blocks (extrapolated "
+                       f"linearly), full TTS layers and a full 60-token vocoder call: U1 chunk {u1 * 1e3:.1f} ms, "
+                       f"U2 text token {u2 * 1e3:.1f} ms, U3 codec token {u3 * 1e3:.2f} ms, U4 vocoder "
+                       f"{u4 * 1e3:.1f} ms; turn = {n_chunks} U1 + {text_tokens} U2 + {codec_tokens} U3 + "
+                       f"{n_voc} U4 for {seconds_audio:.0f} s of speech"),
+            "speak_rtf_per_user": round(seconds_audio / speak, 4),
+            "units_ms": {"U1": u1 * 1e3, "U2": u2 * 1e3, "U3": u3 * 1e3, "U4": u4 * 1e3}}
+
+
+def gemm_probe(engine, M, reps=20):
+    """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the
+    k_gemm_wstream<2,...> launch of every layer) with HIP events on the launching stream."""
+    import torch
+    from fo import _lib, ops
+    L = engine.llm.stack.layers[0]
+    x = torch.randn(M, engine.llm.D, device=engine.device)
+    out = torch.empty(M, L.gu.N, device=engine.device)
+    for _ in range(3):
+        L.gu(x, out=out)
+    lib = _lib.load()
+    import ctypes
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    lib.fo_event_create(ctypes.byref(e0))
+    lib.fo_event_create(ctypes.byref(e1))
+    s = ops.stream(engine.device)
+    lib.fo_event_record(e0, s)
+    for _ in range(reps):
+        L.gu(x, out=out)
+    lib.fo_event_record(e1, s)
+    ms = ctypes.c_float()
+    lib.fo_event_elapsed_ms(e0, e1, ctypes.byref(ms))
+    lib.fo_event_destroy(e0)
+    lib.fo_event_destroy(e1)
+    t = ms.value / reps / 1e3
+    weight_bytes = L.gu.nbytes
+    algo = weight_bytes + M * engine.llm.D * 4 + M * L.gu.N * 4
+    return {"bytes": algo, "seconds": t, "gbps": algo / t / 1e9}
+
+
+def main():
+    args = parse()
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from fo.engine import FreezeOmniEngine
+    model_dir = os.path.join(ROOT, "configs", args.config)
+    t0 = time.perf_counter()
+    eng = FreezeOmniEngine(model_dir, device=dev, max_sessions=max(8, args.users))
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    bcast_s = None
+    if dist is not None:
+        # frozen-weight broadcast from rank 0 over RCCL/xGMI (timed separately, excluded from RTF)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tb = time.perf_counter()
+        for L in eng.llm.stack.layers:
+            for lin in (L.qkv, L.o, L.gu, L.down):
+                dist.broadcast(lin.packed, 0)
+        dist.broadcast(eng.llm.lm_head.packed, 0)
+        torch.cuda.synchronize()
+        bcast_s = time.perf_counter() - tb
+
+    def sync():
+        torch.cuda.synchronize()
+
+    base_kv = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    n_samp = int(args.input_sec * 16000)
+    users = [rank * args.users + u for u in range(args.users)]
+    pcms = [synth_pcm(n_samp, 1234 + u) for u in users]
+    for _ in range(args.warmup):
+        run_turn(eng, base_kv, pcms, args, sync)
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t_start = time.perf_counter()
+    stats = [run_turn(eng, base_kv, pcms, args, sync) for _ in range(args.steps)]
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    wall = time.perf_counter() - t_start
+    sr = 24000.0
+    audio = sum(sum(s["samples"]) for s in stats) / sr
+    lat = [(f - s["t_ss"]) * 1e3 for s in stats for f in s["first"] if f is not None]
+    rtf_user = [(n / sr) / (l - s["t_ss"]) for s in stats for n, l in zip(s["samples"], s["last"]) if l is not None]
+    probe = gemm_probe(eng, 2 * args.users)
+    if dist is not None:
+        t = torch.tensor([wall, audio], dtype=torch.float64, device=dev)
+        allw = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allw, t)
+        wall = max(float(x[0]) for x in allw)
+        audio = sum(float(x[1]) for x in allw)
+        lt = torch.tensor(lat + [0.0] * 0, dtype=torch.float64, device=dev)
+        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([lt.numel()], device=dev))
+        mx = max(int(s) for s in sizes)
+        pad = torch.zeros(mx, dtype=torch.float64, device=dev)
+        pad[:lt.numel()] = lt
+        gl = [torch.zeros_like(pad) for _ in range(world)]
+        dist.all_gather(gl, pad)
+        lat = [float(v) for g, n in zip(gl, sizes) for v in g[:int(n)].tolist()]
+    if rank == 0:
+        peak = 8000.0
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args.config, args.cpu_threads, args.codec_tokens / 40.0,
+                                   int(math.ceil(n_samp / 2560)), args.text_tokens, args.codec_tokens)
+            except Exception as e:  # the baseline is reported, never required for the GPU number
+                cpu = {"value": None, "unit": "x real-time", "cores": args.cpu_threads, "kind": "port",
+                       "sample": f"failed: {type(e).__name__}: {e}"}
+        line = {
+            "metric": "real-time factor + p50 first-audio-chunk latency, Qwen2-7B, N users/GPU",
+            "value": round(audio / wall, 3),
+            "unit": "x real-time (aggregate seconds of 24 kHz speech out per wall second)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16w-fp32a",
+            "data": "synthetic (counter-hash weights at Qwen2-7B + paper geometry; synthetic 16 kHz PCM)",
+            "config": {"workload": f"config 3: {args.users} users/GPU, {args.input_sec:.0f} s input (160 ms chunks) "
+                                   f"+ {args.text_tokens} text tokens + {args.codec_tokens} codec tokens per turn",
+                       "model": f"Freeze-Omni ({args.config}): speech encoder + adapter + Qwen2-7B + AR decoder + "
+                                "TiCodec", "users_per_gpu": args.users, "global_users": args.users * world,
+                       "parallelism": f"dp{world} (session-pinned replicas)"},
+            "p50_first_audio_ms": round(float(np.percentile(lat, 50)), 2) if lat else None,
+            "p90_first_audio_ms": round(float(np.percentile(lat, 90)), 2) if lat else None,
+            "rtf_per_user_p50": round(float(np.percentile(rtf_user, 50)), 3) if rtf_user else None,
+            "load_s": round(load_s, 2), "weight_broadcast_s": None if bcast_s is None else round(bcast_s, 3),
+            "roofline": {"bound": "hbm", "achieved": round(probe["gbps"], 1), "peak": peak, "unit": "GB/s",
+                         "frac": round(probe["gbps"] / peak, 4), "traffic": None,
+                         "kernel": "k_gemm_wstream<2,1,true> (Qwen2 gate/up SwiGLU weight stream)",
+                         "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2)},
+            "cpu_baseline": cpu,
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,14 +103,17 @@ __global__ void k_convT1d(const float* x, int Cin, int Tin, const bf16_t* w, con
   out[((size_t)b * Cout + co) * Tout + t] = acc;
 }
 
-__global__ void k_codec_embed(const bf16_t* table, int E, const int* ids, int B, int T, float* out) {
+// ids outside [0, n_codes) (the decoder's BOS/SOS/PAD specials) embed as zeros instead of reading
+// out of bounds; the reference would raise IndexError there (nn.Embedding).
+__global__ void k_codec_embed(const bf16_t* table, int E, int n_codes, const int* ids, int B, int T, float* out) {
   const long long total = (long long)B * E * T;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
     const int t = (int)(e % T);
     const int c = (int)((e / T) % E);
     const int b = (int)(e / ((long long)T * E));
-    out[e] = bf2f(table[(size_t)ids[b * T + t] * E + c]);
+    const int id = ids[b * T + t];
+    out[e] = (id >= 0 && id < n_codes) ? bf2f(table[(size_t)id * E + c]) : 0.f;
   }
 }
 
@@ -245,9 +248,10 @@ int fo_conv_transpose1d(const float* x, int B, int Cin, int Tin, const void* w, 
   return fo::check_launch("fo_conv_transpose1d");
 }
 
-int fo_codec_embed(const void* table, int E, const int* ids, int B, int T, float* out, hipStream_t s) {
+int fo_codec_embed(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s) {
   const long long n = (long long)B * E * T;
-  hipLaunchKernelGGL(k_codec_embed, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)table, E, ids, B, T, out);
+  hipLaunchKernelGGL(k_codec_embed, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)table, E, n_codes, ids, B, T,
+                     out);
   return fo::check_launch("fo_codec_embed");
 }
 

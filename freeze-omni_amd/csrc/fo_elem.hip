@@ -78,15 +78,16 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, int 
 
 // out[m] = table[idx[m]] for f32 or bf16 tables; optional fp16 rounding (the reference's .half()).
 __global__ void k_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D,
-                              float* out, int ldo, int round_fp16) {
+                              float* out, int ldo, const int* out_rows, int round_fp16) {
   const int m = blockIdx.x;
   if (m >= M) return;
   const long long r = idx ? idx[m] : m;
+  const long long orow = out_rows ? out_rows[m] : m;
   for (int i = threadIdx.x; i < D; i += blockDim.x) {
     float v = table_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(table)[r * ld_tab + i])
                          : reinterpret_cast<const float*>(table)[r * ld_tab + i];
     if (round_fp16) v = round_f16(v);
-    out[(size_t)m * ldo + i] = v;
+    out[(size_t)orow * ldo + i] = v;
   }
 }
 
@@ -227,10 +228,10 @@ int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const fl
 }
 
 int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,
-                   int ldo, int round_fp16, hipStream_t s) {
+                   int ldo, const int* out_rows, int round_fp16, hipStream_t s) {
   FO_REQUIRE(M >= 0 && D > 0, "fo_gather_rows: bad shape");
   if (M == 0) return 0;
-  hipLaunchKernelGGL(k_gather_rows, dim3(M), dim3(256), 0, s, table, table_bf16, ld_tab, idx, M, D, out, ldo,
+  hipLaunchKernelGGL(k_gather_rows, dim3(M), dim3(256), 0, s, table, table_bf16, ld_tab, idx, M, D, out, ldo, out_rows,
                      round_fp16);
   return fo::check_launch("fo_gather_rows");
 }

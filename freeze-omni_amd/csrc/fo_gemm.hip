@@ -58,7 +58,7 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
 }
 
 template <int NT, int RB, bool XF32>
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
+__device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
   constexpr int U = (XF32 && RB == 4) ? 2 : 4;
   constexpr int ROWS = RB * 16;
@@ -212,6 +212,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   }
 }
 
+// Same body under two symbols so profiles separate the multi-10-MB weight streams (Qwen2 MLP,
+// lm_head: >= 64 MB of bf16 per launch) from every other linear layer.
+template <int NT, int RB, bool XF32>
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
+  gemm_body<NT, RB, XF32>(a);
+}
+template <int NT, int RB, bool XF32>
+__global__ __launch_bounds__(256) void k_gemm_wstream(GemmArgs a) {
+  gemm_body<NT, RB, XF32>(a);
+}
+
 // Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
 // of the source to destination tile (tile_base + t * tile_stride).
 __global__ void k_pack(const void* W, int src_bf16, int N, int K, int ldw, bf16_t* out, int KSp,
@@ -310,10 +321,16 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
                ws_floats);
   }
   dim3 grid(groups, mt, S);
+  const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
 #define FO_LAUNCH(NT_, RB_)                                                                \
   do {                                                                                     \
-    if (x_f32) hipLaunchKernelGGL((k_gemm<NT_, RB_, true>), grid, dim3(256), 0, stream, a);  \
-    else hipLaunchKernelGGL((k_gemm<NT_, RB_, false>), grid, dim3(256), 0, stream, a);       \
+    if (wstream) {                                                                         \
+      if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, true>), grid, dim3(256), 0, stream, a); \
+      else hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, false>), grid, dim3(256), 0, stream, a);      \
+    } else {                                                                               \
+      if (x_f32) hipLaunchKernelGGL((k_gemm<NT_, RB_, true>), grid, dim3(256), 0, stream, a);  \
+      else hipLaunchKernelGGL((k_gemm<NT_, RB_, false>), grid, dim3(256), 0, stream, a);       \
+    }                                                                                      \
   } while (0)
   if (NT == 1) {
     if (RB == 1) FO_LAUNCH(1, 1);

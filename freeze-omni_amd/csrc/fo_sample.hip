@@ -19,13 +19,13 @@ __device__ __forceinline__ uint64_t smix(uint64_t x) {
 }
 
 // block arg-max over v[0..n) excluding indices already in `taken`; ties -> smallest index
-__device__ void block_argmax(const float* v, int n, const int* taken, int ntaken, float* bv, int* bi, float& mval,
-                             int& midx) {
+__device__ void block_argmax(const float* v, int n, const int* taken, int ntaken, int ban, float* bv, int* bi,
+                             float& mval, int& midx) {
   float best = -INFINITY;
   int besti = 0x7fffffff;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const float x = v[i];
-    bool skip = false;
+    bool skip = (i == ban);
     for (int q = 0; q < ntaken; ++q) skip |= (taken[q] == i);
     if (!skip && (x > best || (x == best && i < besti))) {
       best = x;
@@ -53,8 +53,8 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
 
 __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, int V, const int* top_k_rows,
                                                  const float* temp_rows, const float* top_p_rows,
-                                                 unsigned long long seed, const int* step_rows, int* out_ids,
-                                                 float* out_val) {
+                                                 unsigned long long seed, const int* step_rows, int ban_id,
+                                                 int* out_ids, float* out_val) {
   __shared__ float bv[1024];
   __shared__ int bi[1024];
   __shared__ int taken[KMAXS];
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
   for (int q = 0; q < k; ++q) {
     float m;
     int i;
-    block_argmax(lg, V, taken, q, bv, bi, m, i);
+    block_argmax(lg, V, taken, q, ban_id, bv, bi, m, i);
     if (threadIdx.x == 0) {
       taken[q] = i;
       tv[q] = m;
@@ -121,12 +121,13 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
 extern "C" {
 
 // logits [B][ld] fp32.  top_k/temp/top_p/step are per-row device arrays (nullable: k=1, T=1, p=0, step 0).
+// ban_id >= 0 excludes one token (benchmark policy: EOS masked until a fixed response length).
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
-              const float* top_p, unsigned long long seed, const int* step, int* out_ids, float* out_maxlogit,
-              hipStream_t s) {
+              const float* top_p, unsigned long long seed, const int* step, int ban_id, int* out_ids,
+              float* out_maxlogit, hipStream_t s) {
   FO_REQUIRE(B > 0 && V > 0, "fo_sample: bad shape");
   hipLaunchKernelGGL(k_sample, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
-                     out_ids, out_maxlogit);
+                     ban_id, out_ids, out_maxlogit);
   return fo::check_launch("fo_sample");
 }
 

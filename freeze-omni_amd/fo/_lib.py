@@ -42,7 +42,7 @@ _SIGS = {
     "fo_fill_hash": (c_int, [c_vp, c_int, c_ll, ctypes.c_ulonglong, c_float, c_float, c_vp]),
     "fo_rmsnorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
     "fo_layernorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
-    "fo_gather_rows": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp]),
+    "fo_gather_rows": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "fo_im2col_3x3s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
                                 c_vp]),
     "fo_tcf_permute": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
@@ -65,11 +65,12 @@ _SIGS = {
                           c_int, c_int, c_vp]),
     "fo_conv_transpose1d": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_vp,
                                     c_vp]),
-    "fo_codec_embed": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp]),
+    "fo_codec_embed": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp]),
     "fo_axpy": (c_int, [c_vp, c_vp, c_ll, c_vp]),
     "fo_scale_add_channel": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_silence_cut": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
-    "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_vp, c_vp]),
+    "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_vp,
+                          c_vp]),
 }
 
 _lib = None

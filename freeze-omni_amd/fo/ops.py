@@ -134,14 +134,14 @@ def layernorm(x, w, b, eps=1e-5, out=None, relu=False, M=None):
     return out
 
 
-def gather_rows(table, idx, out=None, round_fp16=False, D=None, M=None):
-    """out[m] = table[idx[m]] (idx None: identity).  table f32 or bf16 2-D."""
+def gather_rows(table, idx, out=None, round_fp16=False, D=None, M=None, out_rows=None):
+    """out[out_rows[m]] = table[idx[m]] (None: identity).  table f32 or bf16 2-D."""
     D = table.shape[1] if D is None else D
     M = (idx.numel() if idx is not None else table.shape[0]) if M is None else M
     if out is None:
         out = torch.empty(M, D, dtype=F32, device=table.device)
     _lib.call("fo_gather_rows", table.data_ptr(), 1 if table.dtype == BF16 else 0, table.stride(0), ptr(idx), M, D,
-              out.data_ptr(), out.stride(0), 1 if round_fp16 else 0, stream(table.device))
+              out.data_ptr(), out.stride(0), ptr(out_rows), 1 if round_fp16 else 0, stream(table.device))
     return out
 
 
@@ -231,8 +231,8 @@ def conv_transpose1d(x, B, Cin, Tin, w, bias, Cout, K, stride_, pad, out, slope=
 
 
 def codec_embed(table, ids, B, T, out):
-    _lib.call("fo_codec_embed", table.data_ptr(), table.shape[1], ids.data_ptr(), B, T, out.data_ptr(),
-              stream(table.device))
+    _lib.call("fo_codec_embed", table.data_ptr(), table.shape[1], table.shape[0], ids.data_ptr(), B, T,
+              out.data_ptr(), stream(table.device))
     return out
 
 
@@ -251,8 +251,10 @@ def silence_cut(x, N, res):
     return res
 
 
-def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None):
+def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None,
+           ban_id=-1):
     B = logits.shape[0] if B is None else B
     _lib.call("fo_sample", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
-              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), out_ids.data_ptr(), ptr(out_max), stream(logits.device))
+              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), int(ban_id), out_ids.data_ptr(), ptr(out_max),
+              stream(logits.device))
     return out_ids

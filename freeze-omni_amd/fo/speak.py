@@ -1,0 +1,123 @@
+"""Batched speech generation: AR codec-token decode + 40/10 codec chunking + silence-cut emission.
+
+Restates llm2TTS.run (models/decoder/llm2tts.py:114-160) for many sessions at once: every decode step
+advances all live sessions with one launch sequence, and sessions that reach a codec chunk in the
+same step share one vocoder launch.  Emission follows find_min_sum_index
+(models/decoder/llm2tts.py:70-112) using the fo_silence_cut kernel for the window search.
+"""
+import torch
+
+from . import ops
+from .ops import F32, I32
+
+
+class SpeakState:
+    def __init__(self, seq, top_k, max_tokens, min_tokens):
+        self.seq = seq
+        self.top_k = top_k
+        self.max_tokens = max_tokens
+        self.min_tokens = min_tokens
+        self.tokens = []          # tokens waiting for the vocoder (incl. left context)
+        self.left = 0
+        self.buffer = None        # held PCM (device 1-D)
+        self.done = False
+        self.n_generated = 0
+        self.emitted = []         # device PCM segments
+        self.all_ids = []
+
+
+def silence_cut(buffer, syn, N, threshold, res):
+    """find_min_sum_index(buffer, syn): returns (new_buffer, emitted or None); device tensors 1-D."""
+    L = syn.numel()
+    ops.silence_cut(syn, N, res)
+    r = res.cpu()
+    min_sum, cut = float(r[0]), int(r[1])
+    if min_sum / N < threshold:
+        out = syn[:cut] if buffer is None or buffer.numel() == 0 else torch.cat([buffer, syn[:cut]])
+        return syn[cut:].clone(), out
+    nb = syn.clone() if buffer is None or buffer.numel() == 0 else torch.cat([buffer, syn])
+    return nb, None
+
+
+def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
+          max_tokens=1000, min_tokens=0, states_out=None, seed=0):
+    """items: list of (hidden [T1, D] device, prefix [T2, D] device or None).
+    min_tokens > 0 masks EOS until that many tokens (benchmark policy).
+    Yields (session index, pcm segment device 1-D) as segments become available; the per-session
+    SpeakState objects are appended to states_out."""
+    tts = engine.tts
+    dev = engine.device
+    seqs = tts.start(items)
+    states = [SpeakState(s, top_k, max_tokens, min_tokens) for s in seqs]
+    if states_out is not None:
+        states_out.extend(states)
+    up = engine.codec.upsample
+    res = torch.empty(2, dtype=F32, device=dev)
+    cur = torch.full((len(states),), tts.sos, dtype=I32, device=dev)
+    topk_d = torch.tensor([top_k] * len(states), dtype=I32).to(dev)
+    out_ids = torch.empty(len(states), dtype=I32, device=dev)
+    live = list(range(len(states)))
+    step = 0
+    while live:
+        lg = tts.step([states[i].seq for i in live], cur[:len(live)])
+        # benchmark policy: while EOS is masked, draw only real codec ids (random weights would otherwise
+        # also emit the BOS/SOS/PAD specials that a trained decoder never produces)
+        forced = bool(min_tokens and step < min_tokens)
+        st = torch.full((len(live),), step, dtype=I32, device=dev)
+        ops.sample(lg, tts.vocab if forced else tts.vocab + 4, out_ids, topk_d, None, None, seed=seed, step=st,
+                   B=len(live))
+        ids = out_ids[:len(live)].cpu().tolist()
+        step += 1
+        finished, chunk_due = [], []
+        for j, i in enumerate(live):
+            s = states[i]
+            t = ids[j]
+            if t == tts.eos or s.n_generated >= s.max_tokens:
+                s.done = True
+                finished.append(i)
+                continue
+            s.tokens.append(t)
+            s.all_ids.append(t)
+            s.n_generated += 1
+            if len(s.tokens) == s.left + codec_chunk_size + codec_padding_size:
+                chunk_due.append(i)
+            if s.n_generated >= s.max_tokens:
+                s.done = True
+                finished.append(i)
+        if chunk_due:
+            yield from _vocode(engine, states, chunk_due, up, codec_padding_size, N, seg_threshold, res,
+                               final=False)
+        if finished:
+            yield from _vocode(engine, states, [i for i in finished if states[i].tokens], up, codec_padding_size, N,
+                               seg_threshold, res, final=True)
+        live = [i for i in live if not states[i].done]
+        if live:
+            cur = torch.tensor([states[i].all_ids[-1] for i in live], dtype=I32).to(dev)
+    tts.free(seqs)
+
+
+def _vocode(engine, states, idx, up, pad, N, thr, res, final):
+    """One batched vocoder call for sessions idx (equal token counts share a launch)."""
+    groups = {}
+    for i in idx:
+        groups.setdefault(len(states[i].tokens), []).append(i)
+    for T, members in groups.items():
+        ids = torch.tensor([states[i].tokens for i in members], dtype=I32).to(engine.device)
+        pcm = engine.codec(ids)
+        for j, i in enumerate(members):
+            s = states[i]
+            syn = pcm[j]
+            if final:
+                syn = syn[s.left * up:]
+                seg = syn if s.buffer is None or s.buffer.numel() == 0 else torch.cat([s.buffer, syn])
+                s.tokens = []
+                s.emitted.append(seg)
+                yield i, seg
+                continue
+            syn = syn[s.left * up: syn.numel() - pad * up]
+            s.left = pad
+            s.tokens = s.tokens[-(s.left + pad):]
+            s.buffer, seg = silence_cut(s.buffer, syn, N, thr, res)
+            if seg is not None:
+                s.emitted.append(seg)
+                yield i, seg

@@ -60,7 +60,7 @@ int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const fl
                  int relu, hipStream_t s);
 /* embedding / row gather (wte at models/audioLLM.py:303,330; decoder embedding decoder.py:318,336) */
 int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,
-                   int ldo, int round_fp16, hipStream_t s);
+                   int ldo, const int* out_rows, int round_fp16, hipStream_t s);
 /* Conv2dSubsampling4 front end as im2col (+ fused GlobalCMVN) (models/encoder/subsampling.py:67-73,
  * models/encoder/cmvn.py:24-35) */
 int fo_im2col_3x3s2(const float* in, int B, int C, int H, int W, long long sb, long long sc, long long sh,
@@ -110,7 +110,7 @@ int fo_conv1d(const float* x, int B, int Cin, int Tin, const void* w, const floa
 int fo_conv_transpose1d(const float* x, int B, int Cin, int Tin, const void* w, const float* bias, int Cout, int K,
                         int stride, int pad, float slope, float* out, hipStream_t s);
 /* Quantizer.embed (models/decoder/ticodec/models.py:661-702) */
-int fo_codec_embed(const void* table, int E, const int* ids, int B, int T, float* out, hipStream_t s);
+int fo_codec_embed(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 int fo_axpy(float* y, const float* x, long long n, hipStream_t s);
 int fo_scale_add_channel(float* y, int B, int C, int T, float sc, const float* g, hipStream_t s);
 /* llm2TTS.find_min_sum_index window search (models/decoder/llm2tts.py:70-112): res = {min_sum, cut} */
@@ -119,8 +119,8 @@ int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s);
 /* ---------------------------------------------------------------- sampling (fo_sample.hip) */
 /* AudioLLM._post_decode (models/audioLLM.py:431-477) / decoder top-k (models/decoder/decoder.py:353-359) */
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
-              const float* top_p, unsigned long long seed, const int* step, int* out_ids, float* out_maxlogit,
-              hipStream_t s);
+              const float* top_p, unsigned long long seed, const int* step, int ban_id, int* out_ids,
+              float* out_maxlogit, hipStream_t s);
 
 #ifdef __cplusplus
 }

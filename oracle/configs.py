@@ -99,3 +99,39 @@ def get(name):
 # Qwen2 special-token ids used when no tokenizer files are present (bench on synthetic weights).
 QWEN2_IDS = {"<|im_start|>": 151644, "<|im_end|>": 151645, "\n": 198, "system": 8948, "user": 872,
              "assistant": 77091}
+
+
+def write_model_dirs(cfg, root):
+    """Write a reference-layout model directory for `cfg` (what freeze-omni_amd loads):
+    <root>/audiollm/train.yaml, decoder/model.json, codec/model.json, synthetic.json, llm/config.json."""
+    import json
+    import os
+
+    import yaml
+    os.makedirs(os.path.join(root, "audiollm"), exist_ok=True)
+    os.makedirs(os.path.join(root, "decoder"), exist_ok=True)
+    os.makedirs(os.path.join(root, "codec"), exist_ok=True)
+    os.makedirs(os.path.join(root, "llm"), exist_ok=True)
+    with open(os.path.join(root, "audiollm", "train.yaml"), "w") as f:
+        yaml.safe_dump(cfg["train_yaml"], f, sort_keys=True)
+    with open(os.path.join(root, "decoder", "model.json"), "w") as f:
+        json.dump(cfg["decoder_json"], f, indent=1)
+    with open(os.path.join(root, "codec", "model.json"), "w") as f:
+        json.dump(cfg["codec_json"], f, indent=1)
+    with open(os.path.join(root, "synthetic.json"), "w") as f:
+        json.dump({"seed": cfg["seed"], "overrides": cfg["overrides"], "name": cfg["name"]}, f, indent=1)
+    llm = dict(cfg["llm"], architectures=["Qwen2ForCausalLM"], model_type="qwen2", torch_dtype="bfloat16")
+    with open(os.path.join(root, "llm", "config.json"), "w") as f:
+        json.dump(llm, f, indent=1)
+
+
+if __name__ == "__main__":
+    import os
+    import shutil
+    import sys
+    out = sys.argv[1] if len(sys.argv) > 1 else "configs"
+    for n in ("tiny", "real"):
+        write_model_dirs(get(n), os.path.join(out, n))
+    tok = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "tiny_tokenizer")
+    for f in os.listdir(tok):
+        shutil.copy(os.path.join(tok, f), os.path.join(out, "tiny", "llm", f))
