@@ -8,12 +8,13 @@
 // user token: 1..~64) while W is 3..150 MB, so the kernel is an HBM weight stream:
 //  * W is packed once at load into MFMA fragment order [N/16][K/32][64 lanes][8 bf16] so every
 //    wave-instruction of the stream is one contiguous 1 KiB read.
-//  * one workgroup = 4 waves = 16 (or 2x16 for the SwiGLU pair) output columns x up to 64 rows;
-//    the 4 waves split the K range and reduce through LDS.
-//  * when there are too few column tiles to fill 256 CUs the K range is also split across
-//    workgroups; partial slabs go to a workspace and the LAST arriving workgroup (agent-scope
-//    ticket, MI355X_MICROARCH "splitk-seam") sums them in fixed order, so results are
-//    deterministic.
+//  * one workgroup = 8 waves (<= 32 rows) or 4 waves (64 rows) = 16 (or 2x16 for the SwiGLU pair)
+//    output columns; the waves split the K range, keep 8 k-steps (8 KiB per column tile) of
+//    weights in flight each, and reduce through LDS.
+//  * only when the grid is tiny (< 48 tiles) is K also split across workgroups; partial slabs go
+//    to a workspace and the LAST arriving workgroup (agent-scope ticket, MI355X_MICROARCH
+//    "splitk-seam") sums them in fixed order, so results are deterministic.  Measured on MI355X
+//    (scripts/gemm_sweep.py) each extra split costs ~8 us, so larger grids never split.
 //  * mfma_f32_16x16x32_bf16 accumulates in fp32; bias/activation/residual/SwiGLU are fused
 //    into the epilogue.
 #include <type_traits>
@@ -57,19 +58,20 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
   }
 }
 
-template <int NT, int RB, bool XF32>
+template <int NT, int RB, bool XF32, int NW>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
-  constexpr int U = (XF32 && RB == 4) ? 2 : 4;
+  // NW waves split K: 8 when the grid has few column tiles (more weight bytes in flight per CU)
+  constexpr int NTH = NW * 64;
+  constexpr int U = RB == 4 ? (XF32 ? 2 : 4) : (RB == 2 ? 4 : (NW == 8 ? 8 : 4));
   constexpr int ROWS = RB * 16;
-  __shared__ float red[4][NT][ROWS][17];
+  __shared__ float red[NW][NT][ROWS][17];
   __shared__ int s_last;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tg = blockIdx.x, mt = blockIdx.y, sp = blockIdx.z;
   const int KS = a.K >> 5;
   const int kb = (int)((long)KS * sp / a.S), ke = (int)((long)KS * (sp + 1) / a.S);
   const int len = ke - kb;
-  const int wb = kb + len * wave / 4, we = kb + len * (wave + 1) / 4;
   const int m0 = mt * ROWS;
   int rbeff = (a.M - m0 + 15) >> 4;
   if (rbeff > RB) rbeff = RB;
@@ -92,8 +94,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
 
-  int ks = wb;
-  for (; ks + U <= we; ks += U) {
+  // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
+  // together); the < U leftover steps go one per wave, so no wave runs a serial tail.
+  const int G = len / U, rem = len - G * U;
+  const int gb = G * wave / NW, ge = G * (wave + 1) / NW;
+  for (int g = gb; g < ge; ++g) {
+    const int ks = kb + g * U;
     bf16x8 bv[U][NT];
     bf16x8 ah[U][RB], al[U][RB];
 #pragma unroll
@@ -117,10 +123,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
               acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[u][r], bv[u][t], acc[t][r], 0, 0, 0);
           }
   }
-  for (; ks < we; ++ks) {
+  for (int ks = kb + G * U + wave; ks < ke; ks += NW) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      bf16x8 b = __builtin_nontemporal_load(bp[t] + (size_t)ks * 64);
+      const bf16x8 b = __builtin_nontemporal_load(bp[t] + (size_t)ks * 64);
 #pragma unroll
       for (int r = 0; r < RB; ++r)
         if (r < rbeff) {
@@ -146,9 +152,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   const int Ncols = a.ntiles * 16;
   if (a.S > 1) {
     float* slab = a.ws + (size_t)sp * Mrows * Ncols;
-    for (int e = threadIdx.x; e < NE; e += 256) {
+    for (int e = threadIdx.x; e < NE; e += NTH) {
       const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
-      const float v = red[0][t][rr][c] + red[1][t][rr][c] + red[2][t][rr][c] + red[3][t][rr][c];
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
       slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = v;
     }
     // publish: every storing wave drains, barrier, one release + ticket (Guideline 16 counter form)
@@ -169,22 +177,25 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     }
     __syncthreads();
     if (!s_last) return;
-    for (int e = threadIdx.x; e < NE; e += 256) {
+    for (int e = threadIdx.x; e < NE; e += NTH) {
       const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
       float v = 0.f;
       for (int q = 0; q < a.S; ++q) v += a.ws[((size_t)q * Mrows + m0 + rr) * Ncols + (tg * NT + t) * 16 + c];
       red[0][t][rr][c] = v;
     }
   } else {
-    for (int e = threadIdx.x; e < NE; e += 256) {
+    for (int e = threadIdx.x; e < NE; e += NTH) {
       const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
-      red[0][t][rr][c] = red[0][t][rr][c] + red[1][t][rr][c] + red[2][t][rr][c] + red[3][t][rr][c];
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
+      red[0][t][rr][c] = v;
     }
   }
   __syncthreads();
 
   // epilogue
-  for (int e = threadIdx.x; e < ROWS * 16; e += 256) {
+  for (int e = threadIdx.x; e < ROWS * 16; e += NTH) {
     const int rr = e >> 4, c = e & 15;
     const int m = m0 + rr;
     const int n = tg * 16 + c;
@@ -214,13 +225,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
 
 // Same body under two symbols so profiles separate the multi-10-MB weight streams (Qwen2 MLP,
 // lm_head: >= 64 MB of bf16 per launch) from every other linear layer.
-template <int NT, int RB, bool XF32>
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
-  gemm_body<NT, RB, XF32>(a);
+template <int NT, int RB, bool XF32, int NW>
+__global__ __launch_bounds__(NW * 64) void k_gemm(GemmArgs a) {
+  gemm_body<NT, RB, XF32, NW>(a);
 }
-template <int NT, int RB, bool XF32>
-__global__ __launch_bounds__(256) void k_gemm_wstream(GemmArgs a) {
-  gemm_body<NT, RB, XF32>(a);
+template <int NT, int RB, bool XF32, int NW>
+__global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
+  gemm_body<NT, RB, XF32, NW>(a);
 }
 
 // Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
@@ -261,8 +272,11 @@ int fo_gemm_pick_split(int M, int N_tiles_groups, int K) {
   const int KS = K >> 5;
   const int mt = (M + 63) / 64;
   const int blocks = N_tiles_groups * mt;
-  int S = (512 + blocks - 1) / blocks;
-  int smax = KS / 8;
+  // Measured on MI355X (scripts/gemm_sweep.py): every cross-workgroup split adds ~8 us of slab
+  // round trip + ordered reduction, more than it buys for any hot-path shape with >= 56 column
+  // tiles; split only when the grid is tiny.
+  int S = blocks >= 48 ? 1 : (64 + blocks - 1) / blocks;
+  int smax = KS / 16;
   if (smax < 1) smax = 1;
   if (S > smax) S = smax;
   if (S > 16) S = 16;
@@ -322,15 +336,21 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
   }
   dim3 grid(groups, mt, S);
   const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
-#define FO_LAUNCH(NT_, RB_)                                                                \
-  do {                                                                                     \
-    if (wstream) {                                                                         \
-      if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, true>), grid, dim3(256), 0, stream, a); \
-      else hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, false>), grid, dim3(256), 0, stream, a);      \
-    } else {                                                                               \
-      if (x_f32) hipLaunchKernelGGL((k_gemm<NT_, RB_, true>), grid, dim3(256), 0, stream, a);  \
-      else hipLaunchKernelGGL((k_gemm<NT_, RB_, false>), grid, dim3(256), 0, stream, a);       \
-    }                                                                                      \
+  const bool nw8 = (long long)groups * mt * S < 1024;  // few tiles: 8 waves keep more bytes in flight
+#define FO_LAUNCH4(NT_, RB_, NW_)                                                                  \
+  do {                                                                                             \
+    if (wstream) {                                                                                 \
+      if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, true, NW_>), grid, dim3(NW_ * 64), 0, stream, a); \
+      else hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, false, NW_>), grid, dim3(NW_ * 64), 0, stream, a);     \
+    } else {                                                                                       \
+      if (x_f32) hipLaunchKernelGGL((k_gemm<NT_, RB_, true, NW_>), grid, dim3(NW_ * 64), 0, stream, a);        \
+      else hipLaunchKernelGGL((k_gemm<NT_, RB_, false, NW_>), grid, dim3(NW_ * 64), 0, stream, a);             \
+    }                                                                                              \
+  } while (0)
+#define FO_LAUNCH(NT_, RB_)                      \
+  do {                                           \
+    if (nw8 && RB_ < 4) FO_LAUNCH4(NT_, RB_, 8); \
+    else FO_LAUNCH4(NT_, RB_, 4);                \
   } while (0)
   if (NT == 1) {
     if (RB == 1) FO_LAUNCH(1, 1);
@@ -341,6 +361,7 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
     else if (RB == 2) FO_LAUNCH(2, 2);
     else FO_LAUNCH(2, 4);
   }
+#undef FO_LAUNCH4
 #undef FO_LAUNCH
   return fo::check_launch("fo_gemm");
 }

@@ -1,0 +1,49 @@
+"""GEMM shape/split sweep on the GPU: event-timed average per launch for the hot-path shapes."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "freeze-omni_amd"))
+from fo import _lib, ops  # noqa: E402
+from fo.ops import PackedLinear  # noqa: E402
+
+
+def timeit(fn, reps=30):
+    lib = _lib.load()
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    lib.fo_event_create(ctypes.byref(e0))
+    lib.fo_event_create(ctypes.byref(e1))
+    for _ in range(3):
+        fn()
+    s = ops.stream()
+    lib.fo_event_record(e0, s)
+    for _ in range(reps):
+        fn()
+    lib.fo_event_record(e1, s)
+    ms = ctypes.c_float()
+    lib.fo_event_elapsed_ms(e0, e1, ctypes.byref(ms))
+    return ms.value / reps * 1e3
+
+
+shapes = [("qwen_qkv", 4608, 3584, 16, False), ("qwen_o", 3584, 3584, 16, False), ("qwen_down", 3584, 18944, 16, False),
+          ("qwen_gu", 18944, 3584, 16, True), ("tts_qkv", 2688, 896, 8, False), ("tts_down", 896, 4864, 8, False),
+          ("enc_ff1", 4096, 1024, 32, False), ("enc_qkv", 3072, 1024, 32, False), ("lm_head", 152064, 3584, 8, False)]
+dev = torch.device("cuda:0")
+for name, N, K, M, sw in shapes:
+    w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    lin = PackedLinear(w, swiglu_up=w if sw else None)
+    x = torch.randn(M, K, device=dev)
+    out = torch.empty(M, N, device=dev)
+    res = []
+    for S in (1, 2, 3, 4, 6, 8):
+        try:
+            t = timeit(lambda: lin(x, out=out, splitk=S))
+        except RuntimeError as e:
+            res.append(f"S{S}:err")
+            continue
+        res.append(f"S{S}:{t:7.1f}us/{lin.nbytes / t / 1e3:5.2f}TB/s")
+    auto = timeit(lambda: lin(x, out=out))
+    print(f"{name:10s} M={M:3d} N={N:6d} K={K:5d} {lin.nbytes / 1e6:7.1f}MB auto {auto:7.1f}us | " + " ".join(res),
+          flush=True)
