@@ -12,7 +12,10 @@ One "step" = one full dialogue turn for every user on every rank (SURVEY.md §8(
            TiCodec vocoder per 40(+10+10) tokens -> silence-cut emission.
 value = seconds of 24 kHz speech emitted by all users on all ranks / max-over-ranks wall seconds
 (aggregate real-time factor, higher is better).  Also reported: per-user RTF (audio / (dialog_ss ->
-last PCM)), p50/p90 first-audio latency (dialog_ss -> first PCM yield).
+last PCM)), p50/p90 first-audio latency (dialog_ss -> PCM of the first vocoder chunk known on the host,
+the reference's "first PCM chunk" of assets/latency.png) and p50_first_emit_gated_ms (dialog_ss -> first
+segment released by the find_min_sum_index silence gate; random-weight codec output has no 100 ms
+quiet window, so the gate holds the audio until the final flush).
 Weights: counter-hash synthetic weights at Qwen2-7B / paper geometry (configs/real), generated on
 device; no checkpoint is on the box.  Launch for N>1 with torch.distributed.run (one rank per GPU).
 """
@@ -119,8 +122,9 @@ def run_turn(engine, base_kv, pcms, args, sync):
     first = [None] * B
     last = [None] * B
     samples = [0] * B
+    states = []
     for i, seg in speak(engine, items, top_k=args.top_k, min_tokens=args.codec_tokens,
-                        max_tokens=args.codec_tokens):
+                        max_tokens=args.codec_tokens, states_out=states):
         now = time.perf_counter()  # the segment's length is known on the host: the cut index was read back
         if first[i] is None:
             first[i] = now
@@ -128,7 +132,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
         samples[i] += seg.numel()
     for t in turns:
         t.kv.free()
-    return dict(t_ss=t_ss, first=first, last=last, samples=samples)
+    return dict(t_ss=t_ss, first=first, last=last, samples=samples, first_pcm=[s.t_first_pcm for s in states])
 
 
 def cpu_baseline(cfg_name, threads, seconds_audio, n_chunks, text_tokens, codec_tokens):
@@ -217,6 +221,34 @@ def cpu_baseline(cfg_name, threads, seconds_audio, n_chunks, text_tokens, codec_
             "units_ms": {"U1": u1 * 1e3, "U2": u2 * 1e3, "U3": u3 * 1e3, "U4": u4 * 1e3}}
 
 
+def gather_list(dist, vals, world, dev):
+    """All ranks' variable-length float lists, concatenated in rank order."""
+    import torch
+    lt = torch.tensor(vals, dtype=torch.float64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([lt.numel()], dtype=torch.int64, device=dev))
+    mx = max(int(x) for x in sizes)
+    pad = torch.zeros(max(mx, 1), dtype=torch.float64, device=dev)
+    pad[:lt.numel()] = lt
+    gl = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(gl, pad)
+    return [float(v) for g, n in zip(gl, sizes) for v in g[:int(n)].tolist()]
+
+
+def recorded_traffic(kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the newest committed FETCH_SIZE pass of this
+    command (profiles/rNN_fetch.json, written by scripts/summarize_profile.py: KiB x 1024 x 2)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch.json")))
+    if not files:
+        return None, None
+    groups = [g for g in json.load(open(files[-1]))["groups"] if kernel_prefix in g["kernel"]]
+    if not groups:
+        return None, os.path.relpath(files[-1], ROOT)
+    g = max(groups, key=lambda g: g["dispatches"])
+    return g["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def gemm_probe(engine, M, reps=20):
     """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the
     k_gemm_wstream<2,...> launch of every layer) with HIP events on the launching stream."""
@@ -265,16 +297,14 @@ def main():
     eng = FreezeOmniEngine(model_dir, device=dev, max_sessions=max(8, args.users))
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
-    bcast_s = None
+    bcast_s = bcast_bytes = None
     if dist is not None:
         # frozen-weight broadcast from rank 0 over RCCL/xGMI (timed separately, excluded from RTF)
         torch.cuda.synchronize()
         dist.barrier()
         tb = time.perf_counter()
-        for L in eng.llm.stack.layers:
-            for lin in (L.qkv, L.o, L.gu, L.down):
-                dist.broadcast(lin.packed, 0)
-        dist.broadcast(eng.llm.lm_head.packed, 0)
+        from fo.replica import broadcast_frozen
+        bcast_n, bcast_bytes = broadcast_frozen(eng, dist)
         torch.cuda.synchronize()
         bcast_s = time.perf_counter() - tb
 
@@ -300,7 +330,8 @@ def main():
     wall = time.perf_counter() - t_start
     sr = 24000.0
     audio = sum(sum(s["samples"]) for s in stats) / sr
-    lat = [(f - s["t_ss"]) * 1e3 for s in stats for f in s["first"] if f is not None]
+    lat = [(f - s["t_ss"]) * 1e3 for s in stats for f in s["first_pcm"] if f is not None]
+    lat_gated = [(f - s["t_ss"]) * 1e3 for s in stats for f in s["first"] if f is not None]
     rtf_user = [(n / sr) / (l - s["t_ss"]) for s in stats for n, l in zip(s["samples"], s["last"]) if l is not None]
     probe = gemm_probe(eng, 2 * args.users)
     if dist is not None:
@@ -309,17 +340,11 @@ def main():
         dist.all_gather(allw, t)
         wall = max(float(x[0]) for x in allw)
         audio = sum(float(x[1]) for x in allw)
-        lt = torch.tensor(lat + [0.0] * 0, dtype=torch.float64, device=dev)
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([lt.numel()], device=dev))
-        mx = max(int(s) for s in sizes)
-        pad = torch.zeros(mx, dtype=torch.float64, device=dev)
-        pad[:lt.numel()] = lt
-        gl = [torch.zeros_like(pad) for _ in range(world)]
-        dist.all_gather(gl, pad)
-        lat = [float(v) for g, n in zip(gl, sizes) for v in g[:int(n)].tolist()]
+        lat = gather_list(dist, lat, world, dev)
+        lat_gated = gather_list(dist, lat_gated, world, dev)
     if rank == 0:
         peak = 8000.0
+        traffic, traffic_src = recorded_traffic("k_gemm_wstream<2, 1, true, 4>")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -343,10 +368,14 @@ def main():
                        "parallelism": f"dp{world} (session-pinned replicas)"},
             "p50_first_audio_ms": round(float(np.percentile(lat, 50)), 2) if lat else None,
             "p90_first_audio_ms": round(float(np.percentile(lat, 90)), 2) if lat else None,
+            "p50_first_emit_gated_ms": round(float(np.percentile(lat_gated, 50)), 2) if lat_gated else None,
             "rtf_per_user_p50": round(float(np.percentile(rtf_user, 50)), 3) if rtf_user else None,
             "load_s": round(load_s, 2), "weight_broadcast_s": None if bcast_s is None else round(bcast_s, 3),
+            "weight_broadcast_bytes": bcast_bytes,
             "roofline": {"bound": "hbm", "achieved": round(probe["gbps"], 1), "peak": peak, "unit": "GB/s",
-                         "frac": round(probe["gbps"] / peak, 4), "traffic": None,
+                         "frac": round(probe["gbps"] / peak, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src,
                          "kernel": "k_gemm_wstream<2,1,true> (Qwen2 gate/up SwiGLU weight stream)",
                          "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2)},
             "cpu_baseline": cpu,

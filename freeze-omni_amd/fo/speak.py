@@ -5,6 +5,8 @@ advances all live sessions with one launch sequence, and sessions that reach a c
 same step share one vocoder launch.  Emission follows find_min_sum_index
 (models/decoder/llm2tts.py:70-112) using the fo_silence_cut kernel for the window search.
 """
+import time
+
 import torch
 
 from . import ops
@@ -24,6 +26,7 @@ class SpeakState:
         self.n_generated = 0
         self.emitted = []         # device PCM segments
         self.all_ids = []
+        self.t_first_pcm = None   # host time the first vocoder chunk's PCM was known (before the silence gate)
 
 
 def silence_cut(buffer, syn, N, threshold, res):
@@ -108,6 +111,9 @@ def _vocode(engine, states, idx, up, pad, N, thr, res, final):
             s = states[i]
             syn = pcm[j]
             if final:
+                if s.t_first_pcm is None:
+                    torch.cuda.synchronize(engine.device)
+                    s.t_first_pcm = time.perf_counter()
                 syn = syn[s.left * up:]
                 seg = syn if s.buffer is None or s.buffer.numel() == 0 else torch.cat([s.buffer, syn])
                 s.tokens = []
@@ -117,7 +123,9 @@ def _vocode(engine, states, idx, up, pad, N, thr, res, final):
             syn = syn[s.left * up: syn.numel() - pad * up]
             s.left = pad
             s.tokens = s.tokens[-(s.left + pad):]
-            s.buffer, seg = silence_cut(s.buffer, syn, N, thr, res)
+            s.buffer, seg = silence_cut(s.buffer, syn, N, thr, res)   # reads the cut back: PCM is final here
+            if s.t_first_pcm is None:
+                s.t_first_pcm = time.perf_counter()
             if seg is not None:
                 s.emitted.append(seg)
                 yield i, seg
