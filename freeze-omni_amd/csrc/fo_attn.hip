@@ -9,16 +9,15 @@
 //    Ragged batch: every token carries (sequence, absolute position); causal mode lets a query
 //    see keys at positions <= its own, full mode (the reference's eager attention with
 //    attention_mask=None / all-ones masks, decoder.py:140,175,302) sees the whole sequence.
-//    Split-KV: grid (token, kv_head, split) computes partial softmax statistics per chunk of CH
-//    keys for the G query heads sharing that kv head; a combine kernel merges them.
+//    Work items group a sequence's batch tokens (x the GQA group of query heads sharing one kv
+//    head) so its keys are read once per kv head; split-KV over key ranges when the grid would
+//    otherwise not cover the chip, merged by a combine kernel.
 // 2. Encoder rel-pos attention over a per-user ring buffer (models/encoder/attention.py:407-459):
 //    scores = ((q+u).K^T + (q+v).P^T)/sqrt(dk), no mask, no rel_shift; P rows come from a
 //    table of linear_pos(sinusoid(position)) precomputed at load for every position.
 #include "fo_common.h"
 
 namespace {
-
-constexpr int CH = 256;  // keys per split
 
 __global__ __launch_bounds__(256) void k_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd,
                                                        const int* pos, const int* slot, const float* cos_t,
@@ -57,135 +56,196 @@ __global__ __launch_bounds__(256) void k_rope_kv_write(const float* qkv, int ldq
 }
 
 struct AttnArgs {
-  const float* q;
-  const int* tok_seq;
-  const int* tok_nvis;  // keys visible to each query token (causal: own cache index + 1; full: all)
-  const int* block_table;
+  const float* q;          // [T][H*hd], rotated
+  const int* items;        // [n_items][3]: sequence, first token, token count (a sequence's tokens are contiguous)
+  const int* tok_nvis;     // keys visible to each query token (causal: own cache index + 1; full: all)
+  const int* block_table;  // [S][maxb]
   const float* kc;
   const float* vc;
-  float* part_ml;  // [T][H][nsplit][2]
-  float* part_o;   // [T][H][nsplit][hd]
+  float* part_ml;  // [T*H][nsplit][2]   (nsplit > 1)
+  float* part_o;   // [T*H][nsplit][hd]  (nsplit > 1)
   float* out;      // [T][H*hd]
-  int H, KVH, hd, PS, maxb, nsplit;
+  int H, KVH, PS, maxb, nsplit;
   float scale;
 };
 
-__device__ __forceinline__ int visible_keys(const AttnArgs& a, int t) { return a.tok_nvis[t]; }
+constexpr int KT = 64;  // keys per LDS tile (one key per lane in the score phase)
 
-template <int HD, int GMAX>
-__global__ __launch_bounds__(256) void k_attn_split(AttnArgs a) {
-  constexpr int LPK = HD / 8;         // lanes per key (8 dims per lane)
-  constexpr int KPW = 64 / LPK;       // keys per wave per iteration
-  constexpr int PARTS = 256 / HD;     // key partitions in the PV phase
-  __shared__ float q_s[GMAX][HD];
-  __shared__ float sc[GMAX][CH];
-  __shared__ float ml_s[GMAX][2];
-  __shared__ float o_s[PARTS][GMAX][HD];
-  const int t = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+// One work item = up to RMAX query rows (tokens x GQA group) of ONE sequence against one kv head,
+// over split `sp` of that sequence's keys.  K/V tiles of 64 keys are loaded with 16-B coalesced
+// loads into registers one tile ahead (the next tile's loads are in flight while the current tile
+// is computed), staged through LDS, and consumed by all rows: a sequence's keys cross HBM once per
+// kv head no matter how many of its tokens are in the batch.  Online softmax per row (a row's
+// 64 scores of a tile are one wave's 64 lanes); fp32 throughout.
+template <int HD, int RMAX>
+__global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
+  constexpr int KP = HD + 4;          // padded K row: lanes j read k_s[j][d..d+3] conflict-free
+  constexpr int D4 = HD / 4;
+  constexpr int LPT = KT * D4 / 256;  // float4 per thread per tile (K and V each)
+  constexpr int RG = 256 / HD;        // row groups in the PV phase (thread owns column tid % HD)
+  constexpr int NACC = RMAX / RG;
+  constexpr int RPW = RMAX / 4;       // rows per wave in the score phase
+  __shared__ float q_s[RMAX][HD];
+  __shared__ float k_s[KT][KP];
+  __shared__ float v_s[KT][HD];
+  __shared__ float p_s[RMAX][KT + 1];
+  __shared__ float alpha_s[RMAX];
+  __shared__ float ml_s[RMAX][2];
+  __shared__ int nvis_s[RMAX];
+
+  const int it = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+  const int seq = a.items[3 * it], t0 = a.items[3 * it + 1], tn = a.items[3 * it + 2];
   const int G = a.H / a.KVH;
-  const int L = visible_keys(a, t);
-  const int c0 = sp * CH;
-  const int n = min(CH, L - c0);
-  const size_t pidx = ((size_t)t * a.H + (size_t)kvh * G) * a.nsplit + sp;
-  if (n <= 0) return;  // combine reads only splits < ceil(L / CH)
-  const int seq = a.tok_seq[t];
+  const int R = tn * G;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int Lmax = 0;
+  for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
+  const int per = ((Lmax + a.nsplit - 1) / a.nsplit + KT - 1) / KT * KT;
+  const int c0 = sp * per, c1 = min(Lmax, c0 + per);
+  if (c0 >= c1) {  // empty split: neutral partial
+    for (int r = tid; r < R; r += 256) {
+      const size_t o = ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * a.nsplit + sp;
+      a.part_ml[o * 2] = -INFINITY;
+      a.part_ml[o * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  for (int e = tid; e < RMAX * D4; e += 256) {
+    const int r = e / D4, d4 = e % D4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < R) {
+      v = *reinterpret_cast<const float4*>(a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + d4 * 4);
+      v.x *= a.scale; v.y *= a.scale; v.z *= a.scale; v.w *= a.scale;
+    }
+    *reinterpret_cast<float4*>(&q_s[r][d4 * 4]) = v;
+  }
+  if (tid < RMAX) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
+
   const int* bt = a.block_table + (size_t)seq * a.maxb;
-  for (int e = threadIdx.x; e < G * HD; e += 256) {
-    const int g = e / HD, d = e % HD;
-    q_s[g][d] = a.q[(size_t)t * a.H * HD + (size_t)(kvh * G + g) * HD + d];
+  const size_t head_off = (size_t)kvh * a.PS * HD;
+  const size_t page_sz = (size_t)a.KVH * a.PS * HD;
+  float4 kreg[LPT], vreg[LPT];
+  // K/V tile [k0, k0 + 64) into registers (a macro, not a lambda: a captured array would live in scratch)
+#define FO_ATTN_LOAD_TILE(K0)                                                                              \
+  _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                        \
+    const int e = tid + 256 * i, j = e / D4, d4 = e % D4, p = (K0) + j;                                    \
+    if (p < c1) {                                                                                          \
+      const size_t off = (size_t)bt[p / a.PS] * page_sz + head_off + (size_t)(p % a.PS) * HD + d4 * 4;     \
+      kreg[i] = *reinterpret_cast<const float4*>(a.kc + off);                                              \
+      vreg[i] = *reinterpret_cast<const float4*>(a.vc + off);                                              \
+    } else {                                                                                               \
+      kreg[i] = make_float4(0.f, 0.f, 0.f, 0.f);                                                           \
+      vreg[i] = kreg[i];                                                                                   \
+    }                                                                                                      \
   }
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kl = lane / LPK, d0 = (lane % LPK) * 8;
-  for (int base = wave * KPW; base < n; base += 4 * KPW) {
-    const int j = base + kl;
-    float part[GMAX];
+  float m_run[RPW], l_run[RPW], acc[NACC];
 #pragma unroll
-    for (int g = 0; g < GMAX; ++g) part[g] = 0.f;
-    if (j < n) {
-      const int p = c0 + j;
-      const float* kr = a.kc + (((size_t)bt[p / a.PS] * a.KVH + kvh) * a.PS + (p % a.PS)) * HD + d0;
-      const float4 k0 = reinterpret_cast<const float4*>(kr)[0];
-      const float4 k1 = reinterpret_cast<const float4*>(kr)[1];
-      const float kv[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  for (int i = 0; i < RPW; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
 #pragma unroll
-      for (int g = 0; g < GMAX; ++g)
-        if (g < G) {
+  for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
+  const int d = tid % HD, rg = tid / HD;
+
+  FO_ATTN_LOAD_TILE(c0)
+  for (int k0 = c0; k0 < c1; k0 += KT) {
+    __syncthreads();  // readers of the previous tile are done (first pass: q_s / nvis_s visible)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) part[g] += q_s[g][d0 + i] * kv[i];
+    for (int i = 0; i < LPT; ++i) {
+      const int e = tid + 256 * i, j = e / D4, d4 = e % D4;
+      *reinterpret_cast<float4*>(&k_s[j][d4 * 4]) = kreg[i];
+      *reinterpret_cast<float4*>(&v_s[j][d4 * 4]) = vreg[i];
+    }
+    if (k0 + KT < c1) {
+      FO_ATTN_LOAD_TILE(k0 + KT)
+    }
+    __syncthreads();
+    const int nk = min(KT, c1 - k0);
+    // scores + online softmax: wave w owns rows w, w+4, ...; lane = key
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wave + 4 * i;
+      if (r < R) {
+        float sc = 0.f;
+#pragma unroll 8
+        for (int d4 = 0; d4 < D4; ++d4) {
+          const float4 kk = *reinterpret_cast<const float4*>(&k_s[lane][d4 * 4]);
+          const float4 qq = *reinterpret_cast<const float4*>(&q_s[r][d4 * 4]);
+          sc += qq.x * kk.x + qq.y * kk.y + qq.z * kk.z + qq.w * kk.w;
         }
+        const bool valid = lane < nk && k0 + lane < nvis_s[r];
+        sc = valid ? sc : -INFINITY;
+        const float mo = m_run[i];
+        const float mn = fmaxf(mo, wave_max(sc));
+        const float p = valid ? expf(sc - mn) : 0.f;
+        const float al = (mo == mn) ? 1.f : expf(mo - mn);
+        l_run[i] = l_run[i] * al + wave_sum(p);
+        m_run[i] = mn;
+        p_s[r][lane] = p;
+        if (lane == 0) alpha_s[r] = al;
+      }
     }
+    __syncthreads();
 #pragma unroll
-    for (int g = 0; g < GMAX; ++g) {
-      float v = part[g];
+    for (int i = 0; i < NACC; ++i) {
+      const int r = rg + RG * i;
+      if (r < R) acc[i] *= alpha_s[r];
+    }
+    for (int j = 0; j < nk; ++j) {
+      const float v = v_s[j][d];
 #pragma unroll
-      for (int o = LPK / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (g < G && j < n && (lane % LPK) == 0) sc[g][j] = v * a.scale;
+      for (int i = 0; i < NACC; ++i) {
+        const int r = rg + RG * i;
+        if (r < R) acc[i] += p_s[r][j] * v;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int r = wave + 4 * i;
+    if (r < R && lane == 0) {
+      ml_s[r][0] = m_run[i];
+      ml_s[r][1] = l_run[i];
     }
   }
   __syncthreads();
-  // per-head max / exp / sum over the chunk
-  for (int g = wave; g < G; g += 4) {
-    float m = -INFINITY;
-    for (int j = lane; j < n; j += 64) m = fmaxf(m, sc[g][j]);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int j = lane; j < n; j += 64) {
-      const float e = expf(sc[g][j] - m);
-      sc[g][j] = e;
-      s += e;
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) {
+    const int r = rg + RG * i;
+    if (r < R) {
+      const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+      if (a.nsplit == 1) {
+        a.out[th * HD + d] = acc[i] / ml_s[r][1];
+      } else {
+        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[i];
+        if (d == 0) {
+          a.part_ml[(th * a.nsplit + sp) * 2] = ml_s[r][0];
+          a.part_ml[(th * a.nsplit + sp) * 2 + 1] = ml_s[r][1];
+        }
+      }
     }
-    s = wave_sum(s);
-    if (lane == 0) {
-      ml_s[g][0] = m;
-      ml_s[g][1] = s;
-    }
-  }
-  __syncthreads();
-  // PV
-  {
-    const int d = threadIdx.x % HD, part = threadIdx.x / HD;
-    float acc[GMAX];
-#pragma unroll
-    for (int g = 0; g < GMAX; ++g) acc[g] = 0.f;
-    for (int j = part; j < n; j += PARTS) {
-      const int p = c0 + j;
-      const float v = a.vc[(((size_t)bt[p / a.PS] * a.KVH + kvh) * a.PS + (p % a.PS)) * HD + d];
-#pragma unroll
-      for (int g = 0; g < GMAX; ++g)
-        if (g < G) acc[g] += sc[g][j] * v;
-    }
-#pragma unroll
-    for (int g = 0; g < GMAX; ++g)
-      if (g < G) o_s[part][g][d] = acc[g];
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < G * HD; e += 256) {
-    const int g = e / HD, d = e % HD;
-    float v = 0.f;
-#pragma unroll
-    for (int p = 0; p < PARTS; ++p) v += o_s[p][g][d];
-    a.part_o[(pidx + (size_t)g * a.nsplit) * HD + d] = v;
-  }
-  if (threadIdx.x < G) {
-    a.part_ml[(pidx + (size_t)threadIdx.x * a.nsplit) * 2 + 0] = ml_s[threadIdx.x][0];
-    a.part_ml[(pidx + (size_t)threadIdx.x * a.nsplit) * 2 + 1] = ml_s[threadIdx.x][1];
   }
 }
 
-__global__ void k_attn_combine(AttnArgs a) {
+#undef FO_ATTN_LOAD_TILE
+
+// merge split partials: grid (T, H)
+__global__ void k_attn_combine(AttnArgs a, int hd) {
   const int t = blockIdx.x, h = blockIdx.y;
-  const int L = visible_keys(a, t);
-  const int ns = (L + CH - 1) / CH;
   const size_t base = ((size_t)t * a.H + h) * a.nsplit;
   float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, a.part_ml[(base + s) * 2]);
+  for (int s = 0; s < a.nsplit; ++s)
+    if (a.part_ml[(base + s) * 2 + 1] > 0.f) M = fmaxf(M, a.part_ml[(base + s) * 2]);
   float l = 0.f;
-  for (int s = 0; s < ns; ++s) l += a.part_ml[(base + s) * 2 + 1] * expf(a.part_ml[(base + s) * 2] - M);
-  for (int d = threadIdx.x; d < a.hd; d += blockDim.x) {
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float ls = a.part_ml[(base + s) * 2 + 1];
+    if (ls > 0.f) l += ls * expf(a.part_ml[(base + s) * 2] - M);
+  }
+  for (int dd = threadIdx.x; dd < hd; dd += blockDim.x) {
     float o = 0.f;
-    for (int s = 0; s < ns; ++s) o += a.part_o[(base + s) * a.hd + d] * expf(a.part_ml[(base + s) * 2] - M);
-    a.out[(size_t)t * a.H * a.hd + (size_t)h * a.hd + d] = o / l;
+    for (int s = 0; s < a.nsplit; ++s) {
+      const float ls = a.part_ml[(base + s) * 2 + 1];
+      if (ls > 0.f) o += a.part_o[(base + s) * hd + dd] * expf(a.part_ml[(base + s) * 2] - M);
+    }
+    a.out[((size_t)t * a.H + h) * hd + dd] = o / l;
   }
 }
 
@@ -277,7 +337,15 @@ inline int grid_for(long long n) {
 
 extern "C" {
 
-int fo_attn_nsplit(int max_keys) { return (max_keys + CH - 1) / CH; }
+int fo_attn_nsplit(int max_keys, int n_items, int KVH) {
+  // enough work groups to cover the chip (~2 per CU) while every split keeps >= one 64-key tile
+  const int by_keys = (max_keys + KT - 1) / KT;
+  const int wgs = n_items * KVH;
+  int ns = (512 + wgs - 1) / wgs;
+  if (ns > by_keys) ns = by_keys;
+  if (ns > 32) ns = 32;
+  return ns < 1 ? 1 : ns;
+}
 
 int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, const int* pos, const int* slot,
                      const float* cos_t, const float* sin_t, float* q_out, float* kc, float* vc, int PS,
@@ -288,21 +356,32 @@ int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, c
   return fo::check_launch("fo_rope_kv_write");
 }
 
-// q [T][H*hd] -> out [T][H*hd]; part_ml >= T*H*nsplit*2 floats, part_o >= T*H*nsplit*hd floats.
-int fo_attention(const float* q, int T, const int* tok_seq, const int* tok_nvis, const int* block_table, int maxb,
-                 int PS, const float* kc, const float* vc, int H, int KVH, int hd, float scale, int nsplit,
-                 float* part_ml, float* part_o, float* out, hipStream_t s) {
-  FO_REQUIRE(T > 0 && H % KVH == 0, "fo_attention: bad heads");
-  FO_REQUIRE(H / KVH <= 8, "fo_attention: GQA group %d > 8 unsupported", H / KVH);
+// q [T][H*hd] -> out [T][H*hd].  items [n_items][3] (sequence, first token, tokens) with
+// tokens * (H/KVH) <= max_rows <= 64; part_ml >= T*H*nsplit*2 and part_o >= T*H*nsplit*hd floats
+// when nsplit > 1.
+int fo_attention(const float* q, int T, const int* items, int n_items, int max_rows, const int* tok_nvis,
+                 const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
+                 float scale, int nsplit, float* part_ml, float* part_o, float* out, hipStream_t s) {
+  FO_REQUIRE(T > 0 && n_items > 0 && KVH > 0 && H % KVH == 0, "fo_attention: bad shape");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
-  AttnArgs a{q, tok_seq, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, hd, PS, maxb, nsplit, scale};
-  dim3 grid(T, KVH, nsplit);
-  if (hd == 128) hipLaunchKernelGGL((k_attn_split<128, 8>), grid, dim3(256), 0, s, a);
-  else if (hd == 64) hipLaunchKernelGGL((k_attn_split<64, 8>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_attn_split<32, 8>), grid, dim3(256), 0, s, a);
-  int rc = fo::check_launch("fo_attention/split");
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_attn_combine, dim3(T, H), dim3(hd < 64 ? 64 : hd), 0, s, a);
+  FO_REQUIRE(max_rows >= 1 && max_rows <= 64, "fo_attention: %d query rows per item (max 64)", max_rows);
+  FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
+  AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale};
+  dim3 grid(n_items, KVH, nsplit);
+  const bool small = max_rows <= 16;
+  if (hd == 128) {
+    if (small) hipLaunchKernelGGL((k_attn_rows<128, 16>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_attn_rows<128, 64>), grid, dim3(256), 0, s, a);
+  } else if (hd == 64) {
+    if (small) hipLaunchKernelGGL((k_attn_rows<64, 16>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_attn_rows<64, 64>), grid, dim3(256), 0, s, a);
+  } else {
+    if (small) hipLaunchKernelGGL((k_attn_rows<32, 16>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_attn_rows<32, 64>), grid, dim3(256), 0, s, a);
+  }
+  int rc = fo::check_launch("fo_attention/rows");
+  if (rc || nsplit == 1) return rc;
+  hipLaunchKernelGGL(k_attn_combine, dim3(T, H), dim3(hd < 64 ? 64 : hd), 0, s, a, hd);
   return fo::check_launch("fo_attention/combine");
 }
 

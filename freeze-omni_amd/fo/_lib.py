@@ -50,11 +50,11 @@ _SIGS = {
     "fo_conv_cache_update": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "fo_state_head": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
     "fo_scale": (c_int, [c_vp, c_ll, c_float, c_vp]),
-    "fo_attn_nsplit": (c_int, [c_int]),
+    "fo_attn_nsplit": (c_int, [c_int, c_int, c_int]),
     "fo_rope_kv_write": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_int, c_vp]),
-    "fo_attention": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_float,
-                             c_int, c_vp, c_vp, c_vp, c_vp]),
+    "fo_attention": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int,
+                             c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp]),
     "fo_enc_kv_write": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "fo_relpos_attention": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                     c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),

@@ -105,10 +105,11 @@ class BatchMeta:
     """Device-side metadata of one ragged forward over several sequences.
 
     entries: list of (KVSeq, n_new, rope_pos_start, causal).  Reserves KV for the new tokens and
-    advances each sequence's length.
+    advances each sequence's length.  gqa = query heads per kv head of the stack that consumes it:
+    attention work items hold up to 64 // gqa tokens of one sequence (fo_attention).
     """
 
-    def __init__(self, entries, device):
+    def __init__(self, entries, device, gqa=1):
         T = sum(n for _, n, _, _ in entries)
         tok_seq = np.empty(T, np.int32)
         tok_pos = np.empty(T, np.int32)
@@ -134,7 +135,17 @@ class BatchMeta:
         bt = np.zeros((len(entries), maxb), np.int32)
         for s, (seq, _, _, _) in enumerate(entries):
             bt[s, :len(seq.pages)] = seq.pages
-        host = np.concatenate([tok_seq, tok_pos, tok_slot, tok_nvis, np.asarray(last_rows, np.int32), bt.ravel()])
+        tpi = max(1, 64 // gqa)
+        items = []
+        t = 0
+        for s, (seq, n, _, _) in enumerate(entries):
+            for b in range(0, n, tpi):
+                items += [s, t + b, min(tpi, n - b)]
+            t += n
+        self.n_items = len(items) // 3
+        self.max_rows = max(items[2::3]) * gqa
+        host = np.concatenate([tok_seq, tok_pos, tok_slot, tok_nvis, np.asarray(last_rows, np.int32), bt.ravel(),
+                               np.asarray(items, np.int32)])
         dev = torch.from_numpy(host).to(device, non_blocking=True)
         S = len(entries)
         self.T, self.S, self.maxb, self.max_keys = T, S, maxb, max_keys
@@ -143,6 +154,7 @@ class BatchMeta:
         self.tok_slot = dev[2 * T:3 * T]
         self.tok_nvis = dev[3 * T:4 * T]
         self.last_rows = dev[4 * T:4 * T + S]
-        self.block_table = dev[4 * T + S:].view(S, maxb)
+        self.block_table = dev[4 * T + S:4 * T + S + S * maxb].view(S, maxb)
+        self.items = dev[4 * T + S + S * maxb:]
         self.last_rows_host = last_rows
         self._host = host  # keep the staging buffer alive until the copy is consumed

@@ -48,7 +48,7 @@ class LLMEngine:
     def forward(self, x, entries):
         """x: fp32 [T, D] input embeds (already rounded to fp16 values, models/audioLLM.py:338,410);
         entries: list of (KVSeq, n_tokens).  Returns (final-normed hidden [T, D], BatchMeta)."""
-        meta = BatchMeta([(s, n, s.length, True) for s, n in entries], self.device)
+        meta = BatchMeta([(s, n, s.length, True) for s, n in entries], self.device, gqa=self.H // self.KVH)
         self.stack.forward(x, meta)
         ops.rmsnorm(x, self.norm, self.eps, out=x)
         return x, meta

@@ -177,8 +177,8 @@ def scale_(x, s):
     return x
 
 
-def attn_nsplit(max_keys):
-    return _lib.load().fo_attn_nsplit(int(max_keys))
+def attn_nsplit(max_keys, n_items, KVH):
+    return _lib.load().fo_attn_nsplit(int(max_keys), int(n_items), int(KVH))
 
 
 def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS):
@@ -187,10 +187,11 @@ def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS
               stream(qkv.device))
 
 
-def attention(q, T, tok_seq, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit, part_ml, part_o, out):
-    _lib.call("fo_attention", q.data_ptr(), T, tok_seq.data_ptr(), tok_nvis.data_ptr(), block_table.data_ptr(),
-              block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd, float(scale), nsplit,
-              part_ml.data_ptr(), part_o.data_ptr(), out.data_ptr(), stream(q.device))
+def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,
+              part_ml, part_o, out):
+    _lib.call("fo_attention", q.data_ptr(), T, items.data_ptr(), n_items, max_rows, tok_nvis.data_ptr(),
+              block_table.data_ptr(), block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd, float(scale),
+              nsplit, ptr(part_ml), ptr(part_o), out.data_ptr(), stream(q.device))
     return out
 
 

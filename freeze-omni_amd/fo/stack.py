@@ -58,9 +58,11 @@ class DecoderStack:
         qkv = torch.empty(T, (H + 2 * KVH) * hd, dtype=F32, device=dev)
         q = torch.empty(T, H * hd, dtype=F32, device=dev)
         att = torch.empty(T, H * hd, dtype=F32, device=dev)
-        nsplit = ops.attn_nsplit(meta.max_keys)
-        part_ml = torch.empty(T * H * nsplit * 2, dtype=F32, device=dev)
-        part_o = torch.empty(T * H * nsplit * hd, dtype=F32, device=dev)
+        nsplit = ops.attn_nsplit(meta.max_keys, meta.n_items, KVH)
+        part_ml = part_o = None
+        if nsplit > 1:
+            part_ml = torch.empty(T * H * nsplit * 2, dtype=F32, device=dev)
+            part_o = torch.empty(T * H * nsplit * hd, dtype=F32, device=dev)
         m = None
         scale = hd ** -0.5
         for i, L in enumerate(self.layers):
@@ -69,8 +71,9 @@ class DecoderStack:
             L.qkv(h, out=qkv)
             ops.rope_kv_write(qkv, T, H, KVH, hd, meta.tok_pos, meta.tok_slot, self.cos, self.sin, q,
                               self.pool.k[li], self.pool.v[li], self.pool.PS)
-            ops.attention(q, T, meta.tok_seq, meta.tok_nvis, meta.block_table, self.pool.PS, self.pool.k[li],
-                          self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o, att)
+            ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
+                          self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
+                          att)
             L.o(att, out=x, residual=True)
             ops.rmsnorm(x, L.ln2, self.eps, out=h)
             if m is None:

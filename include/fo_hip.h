@@ -76,17 +76,21 @@ int fo_state_head(const float* h, int ldh, const int* rows, int S, const float* 
 int fo_scale(float* x, long long n, float sc, hipStream_t s);
 
 /* ---------------------------------------------------------------- attention (fo_attn.hip) */
-int fo_attn_nsplit(int max_keys);
+/* number of key splits for fo_attention: ~2 work groups per CU, >= 64 keys per split, <= 32 */
+int fo_attn_nsplit(int max_keys, int n_items, int KVH);
 /* RoPE (rotate_half, host cos/sin tables) + paged KV append: transformers apply_rotary_pos_emb +
  * DynamicCache.update (models/audioLLM.py:416-419, models/decoder/decoder.py:146,305) */
 int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, const int* pos, const int* slot,
                      const float* cos_t, const float* sin_t, float* q_out, float* kc, float* vc, int PS,
                      hipStream_t s);
-/* GQA attention over paged KV for a ragged batch; token t sees the first tok_nvis[t] keys of its
- * sequence (causal: own cache index + 1, full/unmasked: all).  Split-KV + combine. */
-int fo_attention(const float* q, int T, const int* tok_seq, const int* tok_nvis, const int* block_table, int maxb,
-                 int PS, const float* kc, const float* vc, int H, int KVH, int hd, float scale, int nsplit,
-                 float* part_ml, float* part_o, float* out, hipStream_t s);
+/* GQA attention over paged KV for a ragged batch (transformers sdpa/eager attention reached from
+ * models/audioLLM.py:482 and models/decoder/decoder.py:142-153,299-311); token t sees the first
+ * tok_nvis[t] keys of its sequence (causal: own cache index + 1, full/unmasked: all).  items
+ * [n_items][3] = (sequence, first token, token count), token count * H/KVH <= max_rows <= 64.
+ * Split-KV (nsplit from fo_attn_nsplit) + combine. */
+int fo_attention(const float* q, int T, const int* items, int n_items, int max_rows, const int* tok_nvis,
+                 const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
+                 float scale, int nsplit, float* part_ml, float* part_o, float* out, hipStream_t s);
 /* encoder MultiHeadedAttention.infer left-chunk buffer as a ring + rel-pos scores
  * (models/encoder/attention.py:407-459) */
 int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,

@@ -39,6 +39,6 @@ def test_library_exports_every_declared_symbol():
     from fo import _lib
     lib = _lib.load()
     assert lib.fo_version() >= 1
-    assert lib.fo_attn_nsplit(257) == 2
+    assert lib.fo_attn_nsplit(257, 8, 4) == 5 and lib.fo_attn_nsplit(100, 64, 14) == 1 and lib.fo_attn_nsplit(1, 1, 1) == 1
     assert _lib.load().fo_gemm_pick_split(1, 224, 18944) == 1   # measured: split-K never pays at >= 48 tiles
     assert _lib.load().fo_gemm_pick_split(1, 4, 4096) > 1
