@@ -69,7 +69,8 @@ struct AttnArgs {
   float scale;
 };
 
-constexpr int KT = 64;  // keys per LDS tile (one key per lane in the score phase)
+constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
+constexpr int MAXPG = 256;  // pages of one split staged in LDS (fo_attn_nsplit keeps splits <= 4096 keys)
 
 // One work item = up to RMAX query rows (tokens x GQA group) of ONE sequence against one kv head,
 // over split `sp` of that sequence's keys.  K/V tiles of 64 keys are loaded with 16-B coalesced
@@ -88,10 +89,11 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
   __shared__ float q_s[RMAX][HD];
   __shared__ float k_s[KT][KP];
   __shared__ float v_s[KT][HD];
-  __shared__ float p_s[RMAX][KT + 1];
+  __shared__ float p_s[RMAX][KT + 4];
   __shared__ float alpha_s[RMAX];
   __shared__ float ml_s[RMAX][2];
   __shared__ int nvis_s[RMAX];
+  __shared__ int pg_s[MAXPG];
 
   const int it = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
   const int seq = a.items[3 * it], t0 = a.items[3 * it + 1], tn = a.items[3 * it + 2];
@@ -110,32 +112,48 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
     }
     return;
   }
-  for (int e = tid; e < RMAX * D4; e += 256) {
-    const int r = e / D4, d4 = e % D4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < R) {
-      v = *reinterpret_cast<const float4*>(a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + d4 * 4);
-      v.x *= a.scale; v.y *= a.scale; v.z *= a.scale; v.w *= a.scale;
-    }
+  for (int e = tid; e < RMAX * D4; e += 256) {  // rows >= R duplicate row R-1 (never output)
+    const int r = e / D4, d4 = e % D4, rr = min(r, R - 1);
+    float4 v = *reinterpret_cast<const float4*>(a.q + ((size_t)(t0 + rr / G) * a.H + kvh * G + rr % G) * HD + d4 * 4);
+    v.x *= a.scale; v.y *= a.scale; v.z *= a.scale; v.w *= a.scale;
     *reinterpret_cast<float4*>(&q_s[r][d4 * 4]) = v;
   }
   if (tid < RMAX) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
 
+  // the split's block-table slice goes to LDS once, so tile loads never wait on a dependent global load
   const int* bt = a.block_table + (size_t)seq * a.maxb;
+  const int pb = c0 / a.PS, npg = (c1 - 1) / a.PS - pb + 1;
+  if (npg > MAXPG) {  // host contract broken (split wider than 4096 keys): poison rather than read wrong keys
+    for (int r = tid; r < R; r += 256) a.out[((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD] = NAN;
+    return;
+  }
+  for (int i = tid; i < npg; i += 256) pg_s[i] = bt[pb + i];
+  __syncthreads();
   const size_t head_off = (size_t)kvh * a.PS * HD;
   const size_t page_sz = (size_t)a.KVH * a.PS * HD;
   float4 kreg[LPT], vreg[LPT];
-  // K/V tile [k0, k0 + 64) into registers (a macro, not a lambda: a captured array would live in scratch)
+  // K/V tile [k0, k0 + 64) into registers.  A macro, not a lambda (a captured array would live in
+  // scratch).  Full tiles load branch-free (a per-element "load or zero" makes hipcc wait vmcnt(0)
+  // per load); only the split's last, partial tile takes the guarded path.
 #define FO_ATTN_LOAD_TILE(K0)                                                                              \
-  _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                        \
-    const int e = tid + 256 * i, j = e / D4, d4 = e % D4, p = (K0) + j;                                    \
-    if (p < c1) {                                                                                          \
-      const size_t off = (size_t)bt[p / a.PS] * page_sz + head_off + (size_t)(p % a.PS) * HD + d4 * 4;     \
+  if ((K0) + KT <= c1) {                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                      \
+      const int e = tid + 256 * i, j = e / D4, d4 = e % D4, p = (K0) + j;                                  \
+      const size_t off = (size_t)pg_s[p / a.PS - pb] * page_sz + head_off + (size_t)(p % a.PS) * HD + d4 * 4; \
       kreg[i] = *reinterpret_cast<const float4*>(a.kc + off);                                              \
       vreg[i] = *reinterpret_cast<const float4*>(a.vc + off);                                              \
-    } else {                                                                                               \
-      kreg[i] = make_float4(0.f, 0.f, 0.f, 0.f);                                                           \
-      vreg[i] = kreg[i];                                                                                   \
+    }                                                                                                      \
+  } else {                                                                                                 \
+    _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                      \
+      const int e = tid + 256 * i, j = e / D4, d4 = e % D4, p = (K0) + j;                                  \
+      if (p < c1) {                                                                                        \
+        const size_t off = (size_t)pg_s[p / a.PS - pb] * page_sz + head_off + (size_t)(p % a.PS) * HD + d4 * 4; \
+        kreg[i] = *reinterpret_cast<const float4*>(a.kc + off);                                            \
+        vreg[i] = *reinterpret_cast<const float4*>(a.vc + off);                                            \
+      } else {                                                                                             \
+        kreg[i] = make_float4(0.f, 0.f, 0.f, 0.f);                                                         \
+        vreg[i] = kreg[i];                                                                                 \
+      }                                                                                                    \
     }                                                                                                      \
   }
   float m_run[RPW], l_run[RPW], acc[NACC];
@@ -159,51 +177,70 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
     }
     __syncthreads();
     const int nk = min(KT, c1 - k0);
-    // scores + online softmax: wave w owns rows w, w+4, ...; lane = key
+    // scores: wave w owns rows w, w+4, ...; lane = key.  Rows go in blocks of 4 with a wave-uniform
+    // guard, and the inner loops are branch-free so LDS reads batch instead of serialising.
+    float sc[RPW];
+#pragma unroll
+    for (int ib = 0; ib < RPW; ib += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sc[ib + u] = 0.f;
+      if (wave + 4 * ib < R) {
+#pragma unroll 4
+        for (int d4 = 0; d4 < D4; ++d4) {
+          const float4 kk = *reinterpret_cast<const float4*>(&k_s[lane][d4 * 4]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float4 qq = *reinterpret_cast<const float4*>(&q_s[wave + 4 * (ib + u)][d4 * 4]);
+            sc[ib + u] += qq.x * kk.x + qq.y * kk.y + qq.z * kk.z + qq.w * kk.w;
+          }
+        }
+      }
+    }
+    // online softmax per row (a row's 64 scores are this wave's 64 lanes)
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int r = wave + 4 * i;
       if (r < R) {
-        float sc = 0.f;
-#pragma unroll 8
-        for (int d4 = 0; d4 < D4; ++d4) {
-          const float4 kk = *reinterpret_cast<const float4*>(&k_s[lane][d4 * 4]);
-          const float4 qq = *reinterpret_cast<const float4*>(&q_s[r][d4 * 4]);
-          sc += qq.x * kk.x + qq.y * kk.y + qq.z * kk.z + qq.w * kk.w;
-        }
         const bool valid = lane < nk && k0 + lane < nvis_s[r];
-        sc = valid ? sc : -INFINITY;
+        const float x = valid ? sc[i] : -INFINITY;
         const float mo = m_run[i];
-        const float mn = fmaxf(mo, wave_max(sc));
-        const float p = valid ? expf(sc - mn) : 0.f;
+        const float mn = fmaxf(mo, wave_max(x));
+        const float p = valid ? expf(x - mn) : 0.f;
         const float al = (mo == mn) ? 1.f : expf(mo - mn);
-        l_run[i] = l_run[i] * al + wave_sum(p);
+        l_run[i] = l_run[i] * al + p;  // per-lane partial; reduced once after the last tile
         m_run[i] = mn;
         p_s[r][lane] = p;
         if (lane == 0) alpha_s[r] = al;
       }
     }
     __syncthreads();
+    // PV: thread owns column d for rows rg, rg+RG, ...; keys in steps of 4 (p_s rows are 16-B aligned;
+    // keys past nk have p = 0 and zero V)
 #pragma unroll
-    for (int i = 0; i < NACC; ++i) {
-      const int r = rg + RG * i;
-      if (r < R) acc[i] *= alpha_s[r];
-    }
-    for (int j = 0; j < nk; ++j) {
-      const float v = v_s[j][d];
+    for (int i = 0; i < NACC; ++i) acc[i] *= alpha_s[min(rg + RG * i, RMAX - 1)];
+    for (int j = 0; j < nk; j += 4) {
+      const float v0 = v_s[j][d], v1 = v_s[j + 1][d], v2 = v_s[j + 2][d], v3 = v_s[j + 3][d];
 #pragma unroll
-      for (int i = 0; i < NACC; ++i) {
-        const int r = rg + RG * i;
-        if (r < R) acc[i] += p_s[r][j] * v;
+      for (int ib = 0; ib < NACC; ib += 4) {
+        if (rg + RG * ib < R) {
+#pragma unroll
+          for (int u = 0; u < 4 && ib + u < NACC; ++u) {
+            const float4 pp = *reinterpret_cast<const float4*>(&p_s[rg + RG * (ib + u)][j]);
+            acc[ib + u] += pp.x * v0 + pp.y * v1 + pp.z * v2 + pp.w * v3;
+          }
+        }
       }
     }
   }
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int r = wave + 4 * i;
-    if (r < R && lane == 0) {
-      ml_s[r][0] = m_run[i];
-      ml_s[r][1] = l_run[i];
+    if (r < R) {
+      const float l = wave_sum(l_run[i]);
+      if (lane == 0) {
+        ml_s[r][0] = m_run[i];
+        ml_s[r][1] = l;
+      }
     }
   }
   __syncthreads();
@@ -344,6 +381,8 @@ int fo_attn_nsplit(int max_keys, int n_items, int KVH) {
   int ns = (512 + wgs - 1) / wgs;
   if (ns > by_keys) ns = by_keys;
   if (ns > 32) ns = 32;
+  const int need = (max_keys + MAXPG * 16 - 1) / (MAXPG * 16);  // every split within the LDS page table
+  if (ns < need) ns = need;
   return ns < 1 ? 1 : ns;
 }
 
