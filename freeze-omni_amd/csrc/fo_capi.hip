@@ -81,6 +81,50 @@ int fo_event_create(void** ev) {
   *ev = (void*)e;
   return 0;
 }
+// Blocking stream (synchronises with the legacy default stream like torch's default work does), for
+// the engines' own launch sequences and graph capture (capture needs a non-null stream).
+int fo_stream_create(void** s_out) {
+  hipStream_t s;
+  FO_HIP(hipStreamCreate(&s));
+  *s_out = (void*)s;
+  return 0;
+}
+int fo_stream_destroy(void* s) {
+  FO_HIP(hipStreamDestroy((hipStream_t)s));
+  return 0;
+}
+// Pinned, device-mapped host memory: kernels write it through *dev_ptr, the host reads *host_ptr
+// after an event (the decode graph's token history).
+int fo_host_alloc(long long bytes, void** host_ptr, void** dev_ptr) {
+  void* h = nullptr;
+  FO_HIP(hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped));
+  void* d = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    fo::set_error("hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    return -1;
+  }
+  *host_ptr = h;
+  *dev_ptr = d;
+  return 0;
+}
+int fo_host_free(void* host_ptr) {
+  FO_HIP(hipHostFree(host_ptr));
+  return 0;
+}
+int fo_event_sync(void* ev) {
+  FO_HIP(hipEventSynchronize((hipEvent_t)ev));
+  return 0;
+}
+// 1 when the event has completed, 0 while pending, <0 on error.
+int fo_event_query(void* ev) {
+  hipError_t e = hipEventQuery((hipEvent_t)ev);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  fo::set_error("hipEventQuery: %s", hipGetErrorString(e));
+  return -1;
+}
 int fo_event_record(void* ev, hipStream_t s) {
   FO_HIP(hipEventRecord((hipEvent_t)ev, s));
   return 0;

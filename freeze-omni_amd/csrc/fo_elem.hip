@@ -203,6 +203,11 @@ inline int grid_for(long long n, int bs = 256) {
 
 }  // namespace
 
+__global__ void k_record_ids(const int* ids, int B, int* dst, int ld, const int* row) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) dst[(size_t)row[0] * ld + b] = ids[b];
+}
+
 extern "C" {
 
 int fo_fill_hash(void* out, int out_bf16, long long n, unsigned long long key, float center, float scale,
@@ -279,6 +284,14 @@ int fo_scale(float* x, long long n, float sc, hipStream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_scale_rows, dim3(grid_for(n)), dim3(256), 0, s, x, n, sc);
   return fo::check_launch("fo_scale");
+}
+
+// dst[row[0]][b] = ids[b]: per-step token history written by the decode graph (row index read on the
+// device so one captured graph serves every step; dst may be host-mapped pinned memory).
+int fo_record_ids(const int* ids, int B, int* dst, int ld, const int* row, hipStream_t s) {
+  FO_REQUIRE(B > 0 && ld >= B, "fo_record_ids: bad shape");
+  hipLaunchKernelGGL(k_record_ids, dim3((B + 63) / 64), dim3(64), 0, s, ids, B, dst, ld, row);
+  return fo::check_launch("fo_record_ids");
 }
 
 }  // extern "C"

@@ -8,13 +8,12 @@
 // user token: 1..~64) while W is 3..150 MB, so the kernel is an HBM weight stream:
 //  * W is packed once at load into MFMA fragment order [N/16][K/32][64 lanes][8 bf16] so every
 //    wave-instruction of the stream is one contiguous 1 KiB read.
-//  * one workgroup = 8 waves (<= 32 rows) or 4 waves (64 rows) = 16 (or 2x16 for the SwiGLU pair)
-//    output columns; the waves split the K range, keep 8 k-steps (8 KiB per column tile) of
-//    weights in flight each, and reduce through LDS.
-//  * only when the grid is tiny (< 48 tiles) is K also split across workgroups; partial slabs go
-//    to a workspace and the LAST arriving workgroup (agent-scope ticket, MI355X_MICROARCH
-//    "splitk-seam") sums them in fixed order, so results are deterministic.  Measured on MI355X
-//    (scripts/gemm_sweep.py) each extra split costs ~8 us, so larger grids never split.
+//  * one workgroup = 16 output columns (2x16 for the SwiGLU pair) x up to 64 rows; its 4/8/16 waves
+//    split the K range (16 when the grid is about one workgroup per CU, fewer as it grows), keep 4
+//    k-steps of weights in flight each, and reduce through LDS.
+//  * only when the grid is tiny (< 48 tiles) is K also split across workgroups: each split writes a
+//    partial slab and a second launch (k_gemm_reduce) sums the slabs in split order and applies the
+//    epilogue, so results are deterministic and no cross-workgroup fence sits inside the GEMM.
 //  * mfma_f32_16x16x32_bf16 accumulates in fp32; bias/activation/residual/SwiGLU are fused
 //    into the epilogue.
 #include <type_traits>
@@ -58,15 +57,34 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
   }
 }
 
-template <int NT, int RB, bool XF32, int NW>
+// Output element (m, n): bias, folded-BN affine, activation or SwiGLU, residual, store.
+__device__ __forceinline__ void epilogue_store(const GemmArgs& a, int NT, int m, int n, float v, float u) {
+  if (NT == 2) {
+    v = v / (1.f + expf(-v)) * u;
+  } else {
+    if (a.bias) v += a.bias[n];
+    if (a.scale) v = v * a.scale[n] + a.shift[n];
+    v = apply_act(v, a.act);
+  }
+  const size_t o = (size_t)m * a.ldy + n;
+  if (a.out_bf16) {
+    bf16_t* y = reinterpret_cast<bf16_t*>(a.Y);
+    if (a.residual) v += bf2f(y[o]);
+    y[o] = f2bf(v);
+  } else {
+    float* y = reinterpret_cast<float*>(a.Y);
+    if (a.residual) v += y[o];
+    y[o] = v;
+  }
+}
+
+template <int NT, int RB, bool XF32, int NW, int U>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
-  // NW waves split K: 8 when the grid has few column tiles (more weight bytes in flight per CU)
+  // NW waves split K inside the workgroup; each keeps U k-steps of weights in flight
   constexpr int NTH = NW * 64;
-  constexpr int U = RB == 4 ? (XF32 ? 2 : 4) : (RB == 2 ? 4 : (NW == 8 ? 8 : 4));
   constexpr int ROWS = RB * 16;
   __shared__ float red[NW][NT][ROWS][17];
-  __shared__ int s_last;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tg = blockIdx.x, mt = blockIdx.y, sp = blockIdx.z;
   const int KS = a.K >> 5;
@@ -148,90 +166,93 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   __syncthreads();
 
   constexpr int NE = NT * ROWS * 16;
-  const int Mrows = gridDim.y * ROWS;
-  const int Ncols = a.ntiles * 16;
+  for (int e = threadIdx.x; e < NE; e += NTH) {
+    const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
+    red[0][t][rr][c] = v;
+  }
+  __syncthreads();
   if (a.S > 1) {
+    // K split across workgroups: write this split's partial slab; k_gemm_reduce (the next launch
+    // on the stream) sums the slabs in split order and applies the epilogue -- deterministic, and no
+    // cross-workgroup fence or ticket inside the GEMM.
+    const int Mrows = gridDim.y * ROWS;
+    const int Ncols = a.ntiles * 16;
     float* slab = a.ws + (size_t)sp * Mrows * Ncols;
     for (int e = threadIdx.x; e < NE; e += NTH) {
       const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
-      slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = v;
+      slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = red[0][t][rr][c];
     }
-    // publish: every storing wave drains, barrier, one release + ticket (Guideline 16 counter form)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int* cnt = a.counters + (size_t)mt * gridDim.x + tg;
-      const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (ticket == a.S - 1);
-      if (last) {
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    for (int e = threadIdx.x; e < NE; e += NTH) {
-      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
-      float v = 0.f;
-      for (int q = 0; q < a.S; ++q) v += a.ws[((size_t)q * Mrows + m0 + rr) * Ncols + (tg * NT + t) * 16 + c];
-      red[0][t][rr][c] = v;
-    }
-  } else {
-    for (int e = threadIdx.x; e < NE; e += NTH) {
-      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
-      red[0][t][rr][c] = v;
-    }
+    return;
   }
-  __syncthreads();
-
-  // epilogue
   for (int e = threadIdx.x; e < ROWS * 16; e += NTH) {
     const int rr = e >> 4, c = e & 15;
     const int m = m0 + rr;
     const int n = tg * 16 + c;
     if (m >= a.M || n >= a.N) continue;
-    float v;
-    if (NT == 2) {
-      const float g = red[0][0][rr][c], u = red[0][1][rr][c];
-      v = g / (1.f + expf(-g)) * u;
-    } else {
-      v = red[0][0][rr][c];
-      if (a.bias) v += a.bias[n];
-      if (a.scale) v = v * a.scale[n] + a.shift[n];
-      v = apply_act(v, a.act);
+    epilogue_store(a, NT, m, n, red[0][0][rr][c], NT == 2 ? red[0][1][rr][c] : 0.f);
+  }
+}
+
+// Sum of the S partial slabs + epilogue for the split-K path (grid-stride over M x N outputs).
+__global__ void k_gemm_reduce(GemmArgs a, int NT, int Mrows) {
+  const int Ncols = a.ntiles * 16;
+  const size_t slab = (size_t)Mrows * Ncols;
+  const long long total = (long long)a.M * a.N;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(e / a.N), n = (int)(e % a.N);
+    const int col = NT == 2 ? (n >> 4) * 32 + (n & 15) : n;
+    float v = 0.f, u = 0.f;
+    for (int q = 0; q < a.S; ++q) {
+      const float* p = a.ws + q * slab + (size_t)m * Ncols + col;
+      v += p[0];
+      if (NT == 2) u += p[16];
     }
-    const size_t o = (size_t)m * a.ldy + n;
-    if (a.out_bf16) {
-      bf16_t* y = reinterpret_cast<bf16_t*>(a.Y);
-      if (a.residual) v += bf2f(y[o]);
-      y[o] = f2bf(v);
-    } else {
-      float* y = reinterpret_cast<float*>(a.Y);
-      if (a.residual) v += y[o];
-      y[o] = v;
-    }
+    epilogue_store(a, NT, m, n, v, u);
   }
 }
 
 // Same body under two symbols so profiles separate the multi-10-MB weight streams (Qwen2 MLP,
 // lm_head: >= 64 MB of bf16 per launch) from every other linear layer.
-template <int NT, int RB, bool XF32, int NW>
+template <int NT, int RB, bool XF32, int NW, int U>
 __global__ __launch_bounds__(NW * 64) void k_gemm(GemmArgs a) {
-  gemm_body<NT, RB, XF32, NW>(a);
+  gemm_body<NT, RB, XF32, NW, U>(a);
 }
-template <int NT, int RB, bool XF32, int NW>
+template <int NT, int RB, bool XF32, int NW, int U>
 __global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
-  gemm_body<NT, RB, XF32, NW>(a);
+  gemm_body<NT, RB, XF32, NW, U>(a);
+}
+
+template <int NT, int RB, int NW, int U>
+void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
+  if (wstream) {
+    if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, U>), grid, dim3(NW * 64), 0, s, a);
+    else hipLaunchKernelGGL((k_gemm_wstream<NT, RB, false, NW, U>), grid, dim3(NW * 64), 0, s, a);
+  } else {
+    if (x_f32) hipLaunchKernelGGL((k_gemm<NT, RB, true, NW, U>), grid, dim3(NW * 64), 0, s, a);
+    else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U>), grid, dim3(NW * 64), 0, s, a);
+  }
+}
+
+// (waves, k-steps in flight per wave) for the M <= 16 kernels; 0 = automatic
+thread_local int g_force_nw = 0, g_force_u = 0;
+
+template <int NT>
+void launch_rb1(int nw, int u, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
+  if (nw == 16) {
+    if (u >= 8) launch_gemm<NT, 1, 16, 8>(wstream, x_f32, grid, a, s);
+    else launch_gemm<NT, 1, 16, 4>(wstream, x_f32, grid, a, s);
+  } else if (nw == 8) {
+    if (u >= 16) launch_gemm<NT, 1, 8, 16>(wstream, x_f32, grid, a, s);
+    else if (u >= 8) launch_gemm<NT, 1, 8, 8>(wstream, x_f32, grid, a, s);
+    else launch_gemm<NT, 1, 8, 4>(wstream, x_f32, grid, a, s);
+  } else {
+    if (u >= 8) launch_gemm<NT, 1, 4, 8>(wstream, x_f32, grid, a, s);
+    else launch_gemm<NT, 1, 4, 4>(wstream, x_f32, grid, a, s);
+  }
 }
 
 // Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
@@ -336,34 +357,45 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
   }
   dim3 grid(groups, mt, S);
   const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
-  const bool nw8 = (long long)groups * mt * S < 1024;  // few tiles: 8 waves keep more bytes in flight
-#define FO_LAUNCH4(NT_, RB_, NW_)                                                                  \
-  do {                                                                                             \
-    if (wstream) {                                                                                 \
-      if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, true, NW_>), grid, dim3(NW_ * 64), 0, stream, a); \
-      else hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, false, NW_>), grid, dim3(NW_ * 64), 0, stream, a);     \
-    } else {                                                                                       \
-      if (x_f32) hipLaunchKernelGGL((k_gemm<NT_, RB_, true, NW_>), grid, dim3(NW_ * 64), 0, stream, a);        \
-      else hipLaunchKernelGGL((k_gemm<NT_, RB_, false, NW_>), grid, dim3(NW_ * 64), 0, stream, a);             \
-    }                                                                                              \
-  } while (0)
-#define FO_LAUNCH(NT_, RB_)                      \
-  do {                                           \
-    if (nw8 && RB_ < 4) FO_LAUNCH4(NT_, RB_, 8); \
-    else FO_LAUNCH4(NT_, RB_, 4);                \
-  } while (0)
-  if (NT == 1) {
-    if (RB == 1) FO_LAUNCH(1, 1);
-    else if (RB == 2) FO_LAUNCH(1, 2);
-    else FO_LAUNCH(1, 4);
+  const long long wgs = (long long)groups * mt * S;
+  if (RB == 1) {
+    // measured (scripts/gemm_sweep.py, MI355X): one workgroup per CU wants 16 waves, a couple per
+    // CU 8, many 4; 4 k-steps in flight per wave is the sweet spot everywhere on the hot path
+    int nw = wgs <= 256 ? 16 : (wgs < 1024 ? 8 : 4), u = 4;
+    if (g_force_nw) nw = g_force_nw;
+    if (g_force_u) u = g_force_u;
+    if (NT == 1) launch_rb1<1>(nw, u, wstream, x_f32, grid, a, stream);
+    else launch_rb1<2>(nw, u, wstream, x_f32, grid, a, stream);
+  } else if (RB == 2) {
+    if (NT == 1) launch_gemm<1, 2, 8, 4>(wstream, x_f32, grid, a, stream);
+    else launch_gemm<2, 2, 8, 4>(wstream, x_f32, grid, a, stream);
   } else {
-    if (RB == 1) FO_LAUNCH(2, 1);
-    else if (RB == 2) FO_LAUNCH(2, 2);
-    else FO_LAUNCH(2, 4);
+    if (x_f32) {
+      if (NT == 1) launch_gemm<1, 4, 4, 2>(wstream, x_f32, grid, a, stream);
+      else launch_gemm<2, 4, 4, 2>(wstream, x_f32, grid, a, stream);
+    } else {
+      if (NT == 1) launch_gemm<1, 4, 4, 4>(wstream, x_f32, grid, a, stream);
+      else launch_gemm<2, 4, 4, 4>(wstream, x_f32, grid, a, stream);
+    }
   }
-#undef FO_LAUNCH4
-#undef FO_LAUNCH
+  if (S > 1) {
+    int rc = fo::check_launch("fo_gemm/split");
+    if (rc) return rc;
+    const long long total = (long long)M * N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(blocks), dim3(256), 0, stream, a, NT, mt * RB * 16);
+  }
   return fo::check_launch("fo_gemm");
+}
+
+// Force (waves, k-steps per wave) of the M <= 16 kernels on this thread (0 = automatic); for sweeps.
+int fo_gemm_tune(int nw, int u) {
+  FO_REQUIRE(nw == 0 || nw == 4 || nw == 8 || nw == 16, "fo_gemm_tune: nw must be 0/4/8/16");
+  FO_REQUIRE(u == 0 || u == 4 || u == 8 || u == 16, "fo_gemm_tune: u must be 0/4/8/16");
+  g_force_nw = nw;
+  g_force_u = u;
+  return 0;
 }
 
 long long fo_pack_weight_elems(int N, int K) { return (long long)((N + 15) / 16) * 16 * ((K + 31) / 32) * 32; }

@@ -53,7 +53,7 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
 
 __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, int V, const int* top_k_rows,
                                                  const float* temp_rows, const float* top_p_rows,
-                                                 unsigned long long seed, const int* step_rows, int ban_id,
+                                                 unsigned long long seed, const int* step_rows, const int* key_rows, int ban_id,
                                                  int* out_ids, float* out_val) {
   __shared__ float bv[1024];
   __shared__ int bi[1024];
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
         for (int q = 0; q < keep; ++q) z += p[q];
       }
       const uint64_t st = step_rows ? (uint64_t)step_rows[row] : 0ull;
-      const float u = (float)(uint32_t)(smix(seed ^ (0x9E37ull * (uint64_t)(row + 1)) + st) >> 40) *
+      const uint64_t key = key_rows ? (uint64_t)key_rows[row] : (uint64_t)row;  // stream id: session, not batch row
+      const float u = (float)(uint32_t)(smix(seed ^ (0x9E37ull * (key + 1)) + st) >> 40) *
                       (1.0f / 16777216.0f) * z;
       float c = 0.f;
       pick = taken[keep - 1];
@@ -123,10 +124,10 @@ extern "C" {
 // logits [B][ld] fp32.  top_k/temp/top_p/step are per-row device arrays (nullable: k=1, T=1, p=0, step 0).
 // ban_id >= 0 excludes one token (benchmark policy: EOS masked until a fixed response length).
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
-              const float* top_p, unsigned long long seed, const int* step, int ban_id, int* out_ids,
+              const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id, int* out_ids,
               float* out_maxlogit, hipStream_t s) {
   FO_REQUIRE(B > 0 && V > 0, "fo_sample: bad shape");
-  hipLaunchKernelGGL(k_sample, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
+  hipLaunchKernelGGL(k_sample, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step, key,
                      ban_id, out_ids, out_maxlogit);
   return fo::check_launch("fo_sample");
 }

@@ -29,10 +29,17 @@ _SIGS = {
     "fo_graph_end": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "fo_graph_launch": (c_int, [c_vp, c_vp]),
     "fo_graph_destroy": (c_int, [c_vp]),
+    "fo_stream_create": (c_int, [ctypes.POINTER(c_vp)]),
+    "fo_stream_destroy": (c_int, [c_vp]),
+    "fo_host_alloc": (c_int, [c_ll, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
+    "fo_host_free": (c_int, [c_vp]),
+    "fo_event_sync": (c_int, [c_vp]),
+    "fo_event_query": (c_int, [c_vp]),
     "fo_event_create": (c_int, [ctypes.POINTER(c_vp)]),
     "fo_event_record": (c_int, [c_vp, c_vp]),
     "fo_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
     "fo_event_destroy": (c_int, [c_vp]),
+    "fo_gemm_tune": (c_int, [c_int, c_int]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),
@@ -49,6 +56,7 @@ _SIGS = {
     "fo_im2col_conv1d": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp]),
     "fo_conv_cache_update": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "fo_state_head": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "fo_record_ids": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
     "fo_scale": (c_int, [c_vp, c_ll, c_float, c_vp]),
     "fo_attn_nsplit": (c_int, [c_int, c_int, c_int]),
     "fo_rope_kv_write": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -68,9 +76,16 @@ _SIGS = {
     "fo_codec_embed": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp]),
     "fo_axpy": (c_int, [c_vp, c_vp, c_ll, c_vp]),
     "fo_scale_add_channel": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
+    "fo_conv_pack_elems": (c_ll, [c_int, c_int, c_int]),
+    "fo_pack_conv": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "fo_conv_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_int, c_int, c_float, c_vp, c_int, c_vp]),
+    "fo_codec_embed_cl": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp]),
+    "fo_scale_add_cl": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
+    "fo_conv_post_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_silence_cut": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
-    "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_vp,
-                          c_vp]),
+    "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int, c_vp,
+                          c_vp, c_vp]),
 }
 
 _lib = None

@@ -44,6 +44,20 @@ class CodecEngine:
         self.upsample = 1
         for u in h["upsample_rates"]:
             self.upsample *= u
+        # MFMA path: every conv packed once into A-fragment order (fo_vocoder.hip)
+        self.p_pre = ops.PackedConv(*self.conv_pre)
+        self.p_ups = []
+        for w, b, u, k in self.ups:
+            pad = (k - u) // 2
+            phases = []
+            for r in range(u):
+                j0 = (r + pad) % u
+                pc = ops.PackedConv(w, b, transposed=(j0, u))
+                off = (r + pad - j0) // u
+                phases.append((r, pc, pc.K - 1 - off))  # (phase, weights, pad of the equivalent conv)
+            self.p_ups.append(phases)
+        self.p_res = [[(k, [(ops.PackedConv(c1[0], c1[1]), c1[2], None if c2 is None else ops.PackedConv(c2[0], c2[1]))
+                            for c1, c2 in convs]) for k, convs in stage] for stage in self.res]
 
     def flops(self, T):
         """Algorithmic FLOPs of one generator call on T tokens (2*Cin*Cout*K*Tout per conv)."""
@@ -60,7 +74,50 @@ class CodecEngine:
         return f
 
     def __call__(self, ids):
-        """ids: device int32 [B, T] codec token ids -> pcm [B, T*upsample] fp32 (tanh output)."""
+        """ids: device int32 [B, T] codec token ids -> pcm [B, T*upsample] fp32 (tanh output).
+        Channel-last activations [B][T][C]; every conv on the matrix cores (fo_conv_cl)."""
+        B, T = ids.shape
+        dev = self.device
+        E = self.codebook.shape[1]
+        x = torch.empty(B, T, E, dtype=F32, device=dev)
+        ops.codec_embed_cl(self.codebook, E, self.codebook.shape[0], ids.contiguous(), B, T, x)
+        y = torch.empty(B, T, self.U, dtype=F32, device=dev)
+        ops.conv_cl(x, B, E, T, self.p_pre, 1, 3, y)
+        x, C, L = y, self.U, T
+        g = self.gfeat.view(1, -1).expand(B, -1).contiguous()
+        nk = len(self.res[0])
+        for i, (w, b, u, k) in enumerate(self.ups):
+            Co = C // 2
+            Lo = (L - 1) * u - 2 * ((k - u) // 2) + k
+            up = torch.empty(B, Lo, Co, dtype=F32, device=dev)
+            for r, pc, pad_r in self.p_ups[i]:  # leaky -> ConvTranspose1d as u polyphase convs
+                Tq = (Lo - r + u - 1) // u
+                ops.conv_cl(x, B, C, L, pc, 1, pad_r, up, Tq=Tq, ostride=u, ooff=r, Tout_total=Lo, pre_leaky=0.1)
+            C, L = Co, Lo
+            xs = None
+            t1 = torch.empty(B, L, C, dtype=F32, device=dev)
+            for kk, convs in self.p_res[i]:
+                yb = up.clone() if xs is not None or nk > 1 else up
+                for p1, d1, p2 in convs:
+                    if p2 is None:  # ResBlock2: y = conv(leaky(y)) + y
+                        ops.conv_cl(yb, B, C, L, p1, d1, (kk * d1 - d1) // 2, yb, pre_leaky=0.1, residual=True)
+                        continue
+                    ops.conv_cl(yb, B, C, L, p1, d1, (kk * d1 - d1) // 2, t1, pre_leaky=0.1)
+                    ops.conv_cl(t1, B, C, L, p2, 1, (kk - 1) // 2, yb, pre_leaky=0.1, residual=True)
+                if xs is None:
+                    xs = yb
+                else:
+                    ops.axpy_(xs, yb)
+            ops.scale_add_cl(xs, B, L, C, 1.0 / nk, g if C == g.shape[1] else None)
+            x = xs
+        w, b = self.conv_post
+        out = torch.empty(B, L, dtype=F32, device=dev)
+        ops.conv_post_cl(x, B, L, C, w, b, w.shape[-1], (w.shape[-1] - 1) // 2, 0.1, out)
+        return out
+
+    def forward_ncl(self, ids):
+        """Channel-major direct-convolution path (VALU kernels of fo_codec.hip); kept as a
+        cross-check of the MFMA path."""
         B, T = ids.shape
         dev = self.device
         x = torch.empty(B, 512, T, dtype=F32, device=dev)

@@ -21,6 +21,23 @@ def stream(device=None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_ENGINE_STREAMS = {}
+
+
+def engine_stream(device):
+    """A blocking HIP stream per device (fo_stream_create) wrapped for torch: it orders against the
+    legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it."""
+    import ctypes
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    if idx not in _ENGINE_STREAMS:
+        h = ctypes.c_void_p()
+        with torch.cuda.device(idx):
+            _lib.call("fo_stream_create", ctypes.byref(h))
+        _ENGINE_STREAMS[idx] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    return _ENGINE_STREAMS[idx]
+
+
 class Runtime:
     """Per-device scratch shared by all kernels of one replica (single stream discipline)."""
 
@@ -172,6 +189,32 @@ def state_head(h, rows, W, b, out):
     return out
 
 
+def record_ids(ids, B, dst_ptr, ld, row):
+    """dst[row[0] * ld + b] = ids[b] for b < B (dst: device pointer, e.g. HostBuffer.dev)."""
+    _lib.call("fo_record_ids", ids.data_ptr(), B, dst_ptr, ld, row.data_ptr(), stream(ids.device))
+
+
+class HostBuffer:
+    """int32 [rows, cols] in pinned, device-mapped host memory (fo_host_alloc): kernels write through
+    .dev, the host reads .np after the writing work has completed."""
+
+    def __init__(self, rows, cols):
+        import ctypes
+        import numpy as np
+        self.rows, self.cols = rows, cols
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("fo_host_alloc", rows * cols * 4, ctypes.byref(h), ctypes.byref(d))
+        self.host, self.dev = h.value, d.value
+        buf = (ctypes.c_int32 * (rows * cols)).from_address(self.host)
+        self.np = np.frombuffer(buf, dtype=np.int32).reshape(rows, cols)
+
+    def free(self):
+        if self.host:
+            self.np = None
+            _lib.call("fo_host_free", self.host)
+            self.host = self.dev = None
+
+
 def scale_(x, s):
     _lib.call("fo_scale", x.data_ptr(), x.numel(), float(s), stream(x.device))
     return x
@@ -225,6 +268,59 @@ def conv1d(x, B, Cin, Tin, w, bias, Cout, K, dil, pad, out, pre_leaky=None, resi
     return out
 
 
+class PackedConv:
+    """Conv1d weight packed into MFMA A-fragment order for fo_conv_cl (channel-last activations).
+    w: conv [Cout][Cin][K]; or, for one polyphase component of a ConvTranspose1d with stride u,
+    w: [Cin][Cout][Ktot] with transposed=(j0, u) -> taps j0, j0+u, ... reversed."""
+
+    def __init__(self, w, bias, transposed=None):
+        _check_dev(w)
+        w = w.contiguous()
+        src_bf16 = 1 if w.dtype == BF16 else 0
+        if w.dtype not in (BF16, F32):
+            w = w.float()
+        if transposed is None:
+            self.Cout, self.Cin, self.K = w.shape
+            Ktot, j0, u = self.K, 0, 1
+        else:
+            j0, u = transposed
+            self.Cin, self.Cout, Ktot = w.shape
+            self.K = (Ktot - j0 + u - 1) // u
+        n = _lib.load().fo_conv_pack_elems(self.Cout, self.Cin, self.K)
+        self.packed = torch.empty(n, dtype=BF16, device=w.device)
+        _lib.call("fo_pack_conv", w.data_ptr(), src_bf16, self.Cout, self.Cin, self.K, 0 if transposed is None else 1,
+                  Ktot, j0, u, self.packed.data_ptr(), stream(w.device))
+        self.bias = None if bias is None else bias.detach().to(device=w.device, dtype=F32).contiguous()
+
+
+def conv_cl(x, B, Cin, Tin, pc, dil, pad, out, Tq=None, ostride=1, ooff=0, Tout_total=None, pre_leaky=None,
+            residual=False):
+    """out[b][q*ostride+ooff][:] (+)= conv(x)[b][q] for q < Tq; x [B][Tin][Cin], out [B][Tout_total][Cout]."""
+    Tq = Tin + 2 * pad - dil * (pc.K - 1) if Tq is None else Tq
+    Tout_total = Tq if Tout_total is None else Tout_total
+    _lib.call("fo_conv_cl", x.data_ptr(), B, Cin, Tin, pc.packed.data_ptr(), ptr(pc.bias), pc.Cout, pc.K, dil, pad,
+              Tq, ostride, ooff, Tout_total, 0 if pre_leaky is None else 1,
+              0.0 if pre_leaky is None else float(pre_leaky), out.data_ptr(), 1 if residual else 0, stream(x.device))
+    return out
+
+
+def codec_embed_cl(table, E, n_codes, ids, B, T, out):
+    _lib.call("fo_codec_embed_cl", table.data_ptr(), E, n_codes, ids.data_ptr(), B, T, out.data_ptr(),
+              stream(out.device))
+    return out
+
+
+def scale_add_cl(y, B, T, C, sc, g=None):
+    _lib.call("fo_scale_add_cl", y.data_ptr(), B, T, C, float(sc), ptr(g), stream(y.device))
+    return y
+
+
+def conv_post_cl(x, B, T, C, w, bias, K, pad, slope, out):
+    _lib.call("fo_conv_post_cl", x.data_ptr(), B, T, C, w.data_ptr(), ptr(bias), K, pad, float(slope), out.data_ptr(),
+              stream(x.device))
+    return out
+
+
 def conv_transpose1d(x, B, Cin, Tin, w, bias, Cout, K, stride_, pad, out, slope=1.0):
     _lib.call("fo_conv_transpose1d", x.data_ptr(), B, Cin, Tin, w.data_ptr(), ptr(bias), Cout, K, stride_, pad,
               float(slope), out.data_ptr(), stream(x.device))
@@ -253,9 +349,10 @@ def silence_cut(x, N, res):
 
 
 def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None,
-           ban_id=-1):
+           ban_id=-1, key=None):
+    """key: optional per-row int32 stream ids (defaults to the row index)."""
     B = logits.shape[0] if B is None else B
     _lib.call("fo_sample", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
-              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), int(ban_id), out_ids.data_ptr(), ptr(out_max),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), ptr(out_max),
               stream(logits.device))
     return out_ids

@@ -5,11 +5,12 @@ advances all live sessions with one launch sequence, and sessions that reach a c
 same step share one vocoder launch.  Emission follows find_min_sum_index
 (models/decoder/llm2tts.py:70-112) using the fo_silence_cut kernel for the window search.
 """
+import collections
 import time
 
 import torch
 
-from . import ops
+from . import _lib, ops
 from .ops import F32, I32
 
 
@@ -43,17 +44,65 @@ def silence_cut(buffer, syn, N, threshold, res):
 
 
 def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
-          max_tokens=1000, min_tokens=0, states_out=None, seed=0):
+          max_tokens=1000, min_tokens=0, states_out=None, seed=0, graph=True, window=16):
     """items: list of (hidden [T1, D] device, prefix [T2, D] device or None).
     min_tokens > 0 masks EOS until that many tokens (benchmark policy).
     Yields (session index, pcm segment device 1-D) as segments become available; the per-session
-    SpeakState objects are appended to states_out."""
-    tts = engine.tts
-    dev = engine.device
-    seqs = tts.start(items)
-    states = [SpeakState(s, top_k, max_tokens, min_tokens) for s in seqs]
+    SpeakState objects are appended to states_out.
+    graph=True replays a captured decode step (fo.tts.DecodeGraph) and reads sampled ids back lazily,
+    up to `window` steps behind the GPU; graph=False is the step-by-step eager loop.  Both produce the
+    same ids (same kernels, same RNG stream)."""
+    es = ops.engine_stream(engine.device)
+    with torch.cuda.stream(es):
+        seqs = engine.tts.start(items)
+    states = [SpeakState(sq, top_k, max_tokens, min_tokens) for sq in seqs]
     if states_out is not None:
         states_out.extend(states)
+    run = _speak_graph if graph else _speak_eager
+    gen = run(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens, min_tokens,
+              seed, window)
+    try:
+        while True:
+            with torch.cuda.stream(es):  # the engine stream is current only while engine code runs
+                out = next(gen, None)
+            if out is None:
+                break
+            yield from out
+    finally:
+        engine.tts.free(seqs)
+
+
+def _after_token(states, i, t, eos, chunk_due, finished, codec_chunk_size, codec_padding_size):
+    """llm2tts.py:122-129 bookkeeping for one sampled id of session i."""
+    s = states[i]
+    if t == eos or s.n_generated >= s.max_tokens:
+        s.done = True
+        finished.append(i)
+        return
+    s.tokens.append(t)
+    s.all_ids.append(t)
+    s.n_generated += 1
+    if len(s.tokens) == s.left + codec_chunk_size + codec_padding_size:
+        chunk_due.append(i)
+    if s.n_generated >= s.max_tokens:
+        s.done = True
+        finished.append(i)
+
+
+def _emit(engine, states, chunk_due, finished, up, pad, N, thr, res):
+    segs = []
+    if chunk_due:
+        segs += list(_vocode(engine, states, chunk_due, up, pad, N, thr, res, final=False))
+    if finished:
+        segs += list(_vocode(engine, states, [i for i in finished if states[i].tokens], up, pad, N, thr, res,
+                             final=True))
+    return segs
+
+
+def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
+                 min_tokens, seed, window):
+    tts = engine.tts
+    dev = engine.device
     up = engine.codec.upsample
     res = torch.empty(2, dtype=F32, device=dev)
     cur = torch.full((len(states),), tts.sos, dtype=I32, device=dev)
@@ -66,37 +115,83 @@ def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=
         # benchmark policy: while EOS is masked, draw only real codec ids (random weights would otherwise
         # also emit the BOS/SOS/PAD specials that a trained decoder never produces)
         forced = bool(min_tokens and step < min_tokens)
-        st = torch.full((len(live),), step, dtype=I32, device=dev)
-        ops.sample(lg, tts.vocab if forced else tts.vocab + 4, out_ids, topk_d, None, None, seed=seed, step=st,
-                   B=len(live))
+        st = torch.tensor([step] * len(live) + live, dtype=I32).to(dev)  # RNG (step, session) per row
+        ops.sample(lg, tts.vocab if forced else tts.vocab + 4, out_ids, topk_d, None, None, seed=seed,
+                   step=st[:len(live)], B=len(live), key=st[len(live):])
         ids = out_ids[:len(live)].cpu().tolist()
         step += 1
         finished, chunk_due = [], []
         for j, i in enumerate(live):
-            s = states[i]
-            t = ids[j]
-            if t == tts.eos or s.n_generated >= s.max_tokens:
-                s.done = True
-                finished.append(i)
-                continue
-            s.tokens.append(t)
-            s.all_ids.append(t)
-            s.n_generated += 1
-            if len(s.tokens) == s.left + codec_chunk_size + codec_padding_size:
-                chunk_due.append(i)
-            if s.n_generated >= s.max_tokens:
-                s.done = True
-                finished.append(i)
-        if chunk_due:
-            yield from _vocode(engine, states, chunk_due, up, codec_padding_size, N, seg_threshold, res,
-                               final=False)
-        if finished:
-            yield from _vocode(engine, states, [i for i in finished if states[i].tokens], up, codec_padding_size, N,
-                               seg_threshold, res, final=True)
+            _after_token(states, i, ids[j], tts.eos, chunk_due, finished, codec_chunk_size, codec_padding_size)
+        segs = _emit(engine, states, chunk_due, finished, up, codec_padding_size, N, seg_threshold, res)
         live = [i for i in live if not states[i].done]
         if live:
             cur = torch.tensor([states[i].all_ids[-1] for i in live], dtype=I32).to(dev)
-    tts.free(seqs)
+        if segs:
+            yield segs
+
+
+def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
+                 min_tokens, seed, window):
+    tts = engine.tts
+    dev = engine.device
+    up = engine.codec.upsample
+    res = torch.empty(2, dtype=F32, device=dev)
+    live = list(range(len(states)))
+    max_keys = max(s.seq.kv.length for s in states) + max_tokens + 1
+    pending = collections.deque()   # (step, live list, graph, event) launched but not yet read
+    step = 0                        # decode steps launched (RNG step and history row)
+    g = None
+    while live or pending:
+        # launch ahead while the window has room
+        while live and len(pending) < window and step < max_tokens:
+            forced = bool(min_tokens and step < min_tokens)
+            ng = tts.decode_graph(len(live), tts.vocab if forced else tts.vocab + 4, top_k, seed, max_keys,
+                                  max_tokens + 1)
+            if ng is not g:
+                if g is None or ng.B != g.B:
+                    ng.ids.fill_(tts.sos) if step == 0 else ng.ids.copy_(torch.tensor(
+                        [states[i].all_ids[-1] for i in live], dtype=I32).to(dev))
+                else:
+                    ng.ids.copy_(g.ids)  # same batch, other sampler bound: ids stay on the device
+                g = ng
+            ev = g.launch([states[i].seq for i in live], live, step, step)
+            pending.append((step, list(live), g, ev))
+            step += 1
+        if not pending:
+            break
+        st, batch, pg, ev = pending.popleft()
+        _lib.call("fo_event_sync", ev)
+        row = pg.hist.np[st].tolist()
+        finished, chunk_due = [], []
+        for j, i in enumerate(batch):
+            if not states[i].done:
+                _after_token(states, i, row[j], tts.eos, chunk_due, finished, codec_chunk_size, codec_padding_size)
+        segs = _emit(engine, states, chunk_due, finished, up, codec_padding_size, N, seg_threshold, res)
+        if finished:
+            # the batch shrinks: drain what was launched with the old batch (finished rows are ignored),
+            # then continue with a graph for the survivors, seeded with their last ids
+            while pending:
+                st, batch, pg, ev = pending.popleft()
+                _lib.call("fo_event_sync", ev)
+                row = pg.hist.np[st].tolist()
+                fin2, due2 = [], []
+                for j, i in enumerate(batch):
+                    if not states[i].done:
+                        _after_token(states, i, row[j], tts.eos, due2, fin2, codec_chunk_size, codec_padding_size)
+                segs += _emit(engine, states, due2, fin2, up, codec_padding_size, N, seg_threshold, res)
+            live = [i for i in live if not states[i].done]
+            g = None
+        if step >= max_tokens and not pending:
+            # every launched token is read; sessions still open ran into max_tokens
+            rest = [i for i in live if not states[i].done]
+            for i in rest:
+                states[i].done = True
+            segs += _emit(engine, states, [], [i for i in rest if states[i].tokens], up, codec_padding_size, N,
+                          seg_threshold, res)
+            live = []
+        if segs:
+            yield segs
 
 
 def _vocode(engine, states, idx, up, pad, N, thr, res, final):

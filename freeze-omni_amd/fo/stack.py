@@ -49,35 +49,41 @@ class DecoderStack:
     def weight_bytes(self):
         return sum(L.qkv.nbytes + L.o.nbytes + L.gu.nbytes + L.down.nbytes for L in self.layers)
 
-    def forward(self, x, meta: BatchMeta):
-        """x: fp32 [T, D] residual stream, updated in place; KV for meta's tokens is appended."""
+    def workspace(self, T, nsplit, device):
+        """Preallocated per-forward buffers for T tokens (graph capture must not allocate)."""
+        H, KVH, hd = self.H, self.KVH, self.hd
+        ws = {"h": torch.empty(T, self.D, dtype=F32, device=device),
+              "qkv": torch.empty(T, (H + 2 * KVH) * hd, dtype=F32, device=device),
+              "q": torch.empty(T, H * hd, dtype=F32, device=device),
+              "att": torch.empty(T, H * hd, dtype=F32, device=device),
+              "m": torch.empty(T, self.layers[0].gu.N, dtype=F32, device=device),
+              "nsplit": nsplit, "part_ml": None, "part_o": None}
+        if nsplit > 1:
+            ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
+            ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
+        return ws
+
+    def forward(self, x, meta: BatchMeta, ws=None):
+        """x: fp32 [T, D] residual stream, updated in place; KV for meta's tokens is appended.
+        ws: optional workspace() of at least meta.T tokens (then nothing is allocated here)."""
         T = meta.T
         H, KVH, hd = self.H, self.KVH, self.hd
-        dev = x.device
-        h = torch.empty(T, self.D, dtype=F32, device=dev)
-        qkv = torch.empty(T, (H + 2 * KVH) * hd, dtype=F32, device=dev)
-        q = torch.empty(T, H * hd, dtype=F32, device=dev)
-        att = torch.empty(T, H * hd, dtype=F32, device=dev)
-        nsplit = ops.attn_nsplit(meta.max_keys, meta.n_items, KVH)
-        part_ml = part_o = None
-        if nsplit > 1:
-            part_ml = torch.empty(T * H * nsplit * 2, dtype=F32, device=dev)
-            part_o = torch.empty(T * H * nsplit * hd, dtype=F32, device=dev)
-        m = None
+        if ws is None:
+            ws = self.workspace(T, ops.attn_nsplit(meta.max_keys, meta.n_items, KVH), x.device)
+        h, qkv, q, att, m = ws["h"][:T], ws["qkv"][:T], ws["q"][:T], ws["att"][:T], ws["m"][:T]
+        nsplit, part_ml, part_o = ws["nsplit"], ws["part_ml"], ws["part_o"]
         scale = hd ** -0.5
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
-            ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=(self.first_fp16 and i == 0))
-            L.qkv(h, out=qkv)
+            ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=(self.first_fp16 and i == 0), M=T)
+            L.qkv(h, out=qkv, M=T)
             ops.rope_kv_write(qkv, T, H, KVH, hd, meta.tok_pos, meta.tok_slot, self.cos, self.sin, q,
                               self.pool.k[li], self.pool.v[li], self.pool.PS)
             ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
                           self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
                           att)
-            L.o(att, out=x, residual=True)
-            ops.rmsnorm(x, L.ln2, self.eps, out=h)
-            if m is None:
-                m = torch.empty(T, L.gu.N, dtype=F32, device=dev)
-            L.gu(h, out=m)
-            L.down(m, out=x, residual=True)
+            L.o(att, out=x, residual=True, M=T)
+            ops.rmsnorm(x, L.ln2, self.eps, out=h, M=T)
+            L.gu(h, out=m, M=T)
+            L.down(m, out=x, residual=True, M=T)
         return x

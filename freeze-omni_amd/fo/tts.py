@@ -6,9 +6,13 @@ Positions: the prefix KV occupies cache rows 0..P-1 with its own RoPE positions 
 bidirectional prefill then uses RoPE positions 0..T while writing rows P..P+T; decode tokens use
 position cache_len - P (decoder.py:337-340).  Many sessions decode in one batched step.
 """
+import ctypes
+from types import SimpleNamespace
+
+import numpy as np
 import torch
 
-from . import ops, tables
+from . import _lib, ops, tables
 from .kv import BatchMeta, KVPool, KVSeq
 from .ops import F32, I32, PackedLinear
 from .stack import DecoderStack
@@ -97,6 +101,126 @@ class TTSEngine:
             s.generated += 1
         return self.out_fnn(x)
 
+    def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows):
+        """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows)."""
+        key = (B, V_sample, top_k, seed)
+        g = self._graphs.get(key) if hasattr(self, "_graphs") else None
+        if g is None or g.max_keys < max_keys or g.hist_rows < hist_rows:
+            if not hasattr(self, "_graphs"):
+                self._graphs = {}
+            if g is not None:
+                g.destroy()
+            g = DecodeGraph(self, B, V_sample, top_k, seed, max(max_keys, 1024), max(hist_rows, 1024))
+            self._graphs[key] = g
+        return g
+
     def free(self, seqs):
         for s in seqs:
             s.kv.free()
+
+
+class DecodeGraph:
+    """One AR decode step (decoder.py:341-367: embed -> layers -> norm -> out_fnn -> sample) for a fixed
+    batch of B sessions, captured once as a hipGraph and replayed per token.
+
+    Everything the step reads is in static device buffers: the current ids (written by the previous
+    replay's sampler, so ids never round-trip through the host), and a per-step metadata block
+    (positions, cache slots, visible keys, RNG step, history row, block tables) uploaded with one
+    async copy from a ring of pinned host buffers.  The sampled ids are also recorded into a pinned,
+    host-mapped history [hist_rows, B] at the step's row, so the host reads them lazily, behind the
+    GPU, after an event instead of synchronising every token.
+    """
+
+    RING = 64
+
+    def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows):
+        dev = tts.device
+        PS = tts.pool.PS
+        self.tts, self.B, self.V_sample, self.seed = tts, B, V_sample, seed
+        self.max_keys, self.hist_rows = max_keys, hist_rows
+        self.maxb = (max_keys + PS - 1) // PS
+        self.n_meta = 5 * B + 1 + B * self.maxb
+        self.host = [torch.empty(self.n_meta, dtype=I32).pin_memory() for _ in range(self.RING)]
+        self.host_np = [h.numpy() for h in self.host]
+        self.meta_d = torch.zeros(self.n_meta, dtype=I32, device=dev)
+        m = self.meta_d
+        items = torch.tensor([[b, b, 1] for b in range(B)], dtype=I32).reshape(-1).to(dev)
+        self.meta = SimpleNamespace(T=B, S=B, tok_pos=m[0:B], tok_slot=m[B:2 * B], tok_nvis=m[2 * B:3 * B],
+                                    step=m[3 * B:4 * B], key=m[4 * B:5 * B], hist_row=m[5 * B:5 * B + 1],
+                                    block_table=m[5 * B + 1:].view(B, self.maxb), items=items, n_items=B,
+                                    max_rows=1, max_keys=max_keys)
+        self.ids = torch.full((B,), tts.sos, dtype=I32, device=dev)
+        self.hist = ops.HostBuffer(hist_rows, B)
+        self.x = torch.empty(B, tts.D, dtype=F32, device=dev)
+        self.logits = torch.empty(B, tts.vocab + 4, dtype=F32, device=dev)
+        self.topk = torch.tensor([top_k] * B, dtype=I32).to(dev)
+        self.ws = tts.main.workspace(B, ops.attn_nsplit(max_keys, B, tts.H), dev)
+        self.events = []
+        for _ in range(self.RING):
+            e = ctypes.c_void_p()
+            _lib.call("fo_event_create", ctypes.byref(e))
+            self.events.append(e)
+        self.exec = None
+        self._capture()
+
+    def _body(self):
+        t = self.tts
+        ops.gather_rows(t.embedding, self.ids, out=self.x)
+        t.main.forward(self.x, self.meta, self.ws)
+        ops.rmsnorm(self.x, t.norm, t.eps, out=self.x)
+        t.out_fnn(self.x, out=self.logits)
+        ops.sample(self.logits, self.V_sample, self.ids, self.topk, None, None, seed=self.seed, step=self.meta.step,
+                   B=self.B, key=self.meta.key)
+        ops.record_ids(self.ids, self.B, self.hist.dev, self.B, self.meta.hist_row)
+
+    def _capture(self):
+        s = ops.stream(self.tts.device)
+        if s == 0 or s is None:
+            raise RuntimeError("DecodeGraph must be captured on a non-default stream (ops.engine_stream)")
+        _lib.call("fo_graph_begin", s)
+        try:
+            self._body()
+        finally:
+            ex = ctypes.c_void_p()
+            _lib.call("fo_graph_end", s, ctypes.byref(ex))
+        self.exec = ex
+
+    def set_ids(self, ids_dev):
+        self.ids.copy_(ids_dev[:self.B])
+
+    def launch(self, seqs, keys, step, slot):
+        """Replay one step for seqs (len B, batch order) with RNG stream ids `keys` at step `step`,
+        history row `slot`; appends one KV position to every sequence.  Returns the step's event."""
+        B, maxb = self.B, self.maxb
+        h = self.host_np[slot % self.RING]
+        h[4 * B:5 * B] = keys
+        h[5 * B] = slot
+        bt = h[5 * B + 1:].reshape(B, maxb)
+        for b, s in enumerate(seqs):
+            kv = s.kv
+            L = kv.length
+            kv.reserve(L + 1)
+            if len(kv.pages) > maxb:
+                raise RuntimeError("decode graph block table too small")
+            h[b] = L - s.P
+            h[B + b] = kv.slot(L)
+            h[2 * B + b] = L + 1
+            h[3 * B + b] = step
+            bt[b, :len(kv.pages)] = kv.pages
+            kv.length = L + 1
+            s.generated += 1
+        self.meta_d.copy_(self.host[slot % self.RING], non_blocking=True)
+        st = ops.stream(self.tts.device)
+        _lib.call("fo_graph_launch", self.exec, st)
+        ev = self.events[slot % self.RING]
+        _lib.call("fo_event_record", ev, st)
+        return ev
+
+    def destroy(self):
+        if self.exec is not None:
+            _lib.call("fo_graph_destroy", self.exec)
+            self.exec = None
+        for e in self.events:
+            _lib.call("fo_event_destroy", e)
+        self.events = []
+        self.hist.free()

@@ -24,6 +24,12 @@ int fo_graph_begin(hipStream_t s);
 int fo_graph_end(hipStream_t s, void** exec_out);
 int fo_graph_launch(void* exec, hipStream_t s);
 int fo_graph_destroy(void* exec);
+int fo_stream_create(void** s_out);
+int fo_stream_destroy(void* s);
+int fo_host_alloc(long long bytes, void** host_ptr, void** dev_ptr);
+int fo_host_free(void* host_ptr);
+int fo_event_sync(void* ev);
+int fo_event_query(void* ev);
 int fo_event_create(void** ev);
 int fo_event_record(void* ev, hipStream_t s);
 int fo_event_elapsed_ms(void* a, void* b, float* ms);
@@ -36,6 +42,8 @@ int fo_event_destroy(void* ev);
  *   adapter conv/project (models/adapter.py:670,679), TTS Llama layers + out_fnn
  *   (models/decoder/decoder.py:299-311,346).
  * W is packed once by fo_pack_weight into MFMA fragment order. */
+/* sweep hook: force (waves, k-steps in flight per wave) of the M <= 16 GEMM kernels; 0 = automatic */
+int fo_gemm_tune(int nw, int u);
 long long fo_pack_weight_elems(int N, int K);
 int fo_pack_weight(const void* W, int src_bf16, int N, int K, int ldw, void* out, int tile_base, int tile_stride,
                    hipStream_t stream);
@@ -74,6 +82,8 @@ int fo_conv_cache_update(float* cache, const int* slots, const float* x, int B, 
 int fo_state_head(const float* h, int ldh, const int* rows, int S, const float* W, const float* bias, int D,
                   float* probs, hipStream_t s);
 int fo_scale(float* x, long long n, float sc, hipStream_t s);
+/* dst[row[0]][b] = ids[b]: the AR decode graph's token history (llm2tts.py:122-129 accumulate ids) */
+int fo_record_ids(const int* ids, int B, int* dst, int ld, const int* row, hipStream_t s);
 
 /* ---------------------------------------------------------------- attention (fo_attn.hip) */
 /* number of key splits for fo_attention: ~2 work groups per CU, >= 64 keys per split, <= 32 */
@@ -117,14 +127,32 @@ int fo_conv_transpose1d(const float* x, int B, int Cin, int Tin, const void* w, 
 int fo_codec_embed(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 int fo_axpy(float* y, const float* x, long long n, hipStream_t s);
 int fo_scale_add_channel(float* y, int B, int C, int T, float sc, const float* g, hipStream_t s);
+/* ---------------------------------------------------------------- vocoder on MFMA (fo_vocoder.hip)
+ * Generator.forward convs (models/decoder/ticodec/models.py:59-110,211-242) as implicit GEMMs on
+ * channel-last activations [B][T][C]; ConvTranspose1d as stride-u polyphase convs. */
+long long fo_conv_pack_elems(int Cout, int Cin, int K);
+int fo_pack_conv(const void* W, int src_bf16, int Cout, int Cin, int K, int transposed, int Ktot, int j0, int u,
+                 void* out, hipStream_t s);
+int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const float* bias, int Cout, int K, int dil,
+               int pad, int Tq, int ostride, int ooff, int Tout_total, int pre_leaky, float slope, float* out,
+               int residual, hipStream_t s);
+/* Quantizer.embed (models/decoder/ticodec/models.py:661-700), channel-last output */
+int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
+/* xs / num_kernels (+ global feature, models.py:233-238), channel-last */
+int fo_scale_add_cl(float* y, int B, int T, int C, float sc, const float* g, hipStream_t s);
+/* leaky -> conv_post (Cout 1) -> tanh (models.py:239-241), channel-last input */
+int fo_conv_post_cl(const float* x, int B, int T, int C, const void* w, const float* bias, int K, int pad, float slope,
+                    float* out, hipStream_t s);
+
 /* llm2TTS.find_min_sum_index window search (models/decoder/llm2tts.py:70-112): res = {min_sum, cut} */
 int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s);
 
 /* ---------------------------------------------------------------- sampling (fo_sample.hip) */
-/* AudioLLM._post_decode (models/audioLLM.py:431-477) / decoder top-k (models/decoder/decoder.py:353-359) */
+/* AudioLLM._post_decode (models/audioLLM.py:431-477) / decoder top-k (models/decoder/decoder.py:353-359).
+ * Draws come from a counter stream keyed by (seed, key[row] or row, step[row]). */
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
-              const float* top_p, unsigned long long seed, const int* step, int ban_id, int* out_ids,
-              float* out_maxlogit, hipStream_t s);
+              const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
+              int* out_ids, float* out_maxlogit, hipStream_t s);
 
 #ifdef __cplusplus
 }

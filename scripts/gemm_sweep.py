@@ -28,22 +28,25 @@ def timeit(fn, reps=30):
 
 
 shapes = [("qwen_qkv", 4608, 3584, 16, False), ("qwen_o", 3584, 3584, 16, False), ("qwen_down", 3584, 18944, 16, False),
-          ("qwen_gu", 18944, 3584, 16, True), ("tts_qkv", 2688, 896, 8, False), ("tts_down", 896, 4864, 8, False),
-          ("enc_ff1", 4096, 1024, 32, False), ("enc_qkv", 3072, 1024, 32, False), ("lm_head", 152064, 3584, 8, False)]
+          ("qwen_gu", 18944, 3584, 16, True), ("tts_qkv", 2688, 896, 8, False), ("tts_o", 896, 896, 8, False),
+          ("tts_gu", 4864, 896, 8, True), ("tts_down", 896, 4864, 8, False), ("lm_head", 152064, 3584, 8, False)]
 dev = torch.device("cuda:0")
+lib = _lib.load()
 for name, N, K, M, sw in shapes:
     w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     lin = PackedLinear(w, swiglu_up=w if sw else None)
     x = torch.randn(M, K, device=dev)
     out = torch.empty(M, N, device=dev)
-    res = []
-    for S in (1, 2, 3, 4, 6, 8):
-        try:
-            t = timeit(lambda: lin(x, out=out, splitk=S))
-        except RuntimeError as e:
-            res.append(f"S{S}:err")
-            continue
-        res.append(f"S{S}:{t:7.1f}us/{lin.nbytes / t / 1e3:5.2f}TB/s")
+    ref = lin(x, out=torch.empty(M, N, device=dev)).clone()
     auto = timeit(lambda: lin(x, out=out))
-    print(f"{name:10s} M={M:3d} N={N:6d} K={K:5d} {lin.nbytes / 1e6:7.1f}MB auto {auto:7.1f}us | " + " ".join(res),
-          flush=True)
+    res = []
+    for nw, u in ((4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 4), (16, 8)):
+        for S in (1, 2, 4):
+            lib.fo_gemm_tune(nw, u)
+            t = timeit(lambda: lin(x, out=out, splitk=S))
+            err = (out - ref).abs().max().item()
+            res.append((t, f"nw{nw}u{u}S{S}:{t:6.1f}" + ("" if err < 1e-3 else f"(ERR {err:.2g})")))
+    lib.fo_gemm_tune(0, 0)
+    res.sort()
+    print(f"{name:9s} M={M:2d} N={N:6d} K={K:5d} {lin.nbytes / 1e6:7.1f}MB auto {auto:6.1f}us "
+          f"({lin.nbytes / auto / 1e3:4.2f}TB/s) best: " + " ".join(r for _, r in res[:6]), flush=True)

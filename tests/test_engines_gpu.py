@@ -196,3 +196,80 @@ def test_sampler_topk_topp(dev):
             topk = lg[r].topk(int(k[r])).indices.cpu()
             assert int(ids[r]) in topk.tolist()
         assert int(ids[2]) == int(lg[2].argmax())
+
+
+@pytest.fixture(scope="module")
+def speech_engine(dev, src):
+    from types import SimpleNamespace
+    from fo.codec import CodecEngine
+    from fo.tts import TTSEngine
+    return SimpleNamespace(device=dev, tts=TTSEngine(src, CFG["decoder_json"], dev, kv_tokens=16384),
+                           codec=CodecEngine(src, CFG["codec_json"], dev))
+
+
+def _speak_all(eng, items, graph, **kw):
+    from fo.speak import speak
+    states = []
+    segs = [(i, s.cpu().numpy()) for i, s in speak(eng, items, states_out=states, graph=graph, **kw)]
+    return [s.all_ids for s in states], segs
+
+
+def _items(dev, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    t = np.load(os.path.join(G, "tts_tiny.npz"))
+    out = []
+    for u in range(n):
+        h = torch.from_numpy(t["hidden"]) + 0.05 * u * torch.randn(t["hidden"].shape, generator=g)
+        p = torch.from_numpy(t["prefix"])[: 24 - 4 * (u % 3)]
+        out.append((h.to(dev).contiguous(), p.to(dev).contiguous()))
+    return out
+
+
+@pytest.mark.parametrize("top_k,min_tokens", [(1, 0), (4, 0), (1, 60)])
+def test_speak_graph_matches_eager(dev, speech_engine, top_k, min_tokens):
+    """The captured decode graph with lazy id readback gives the eager loop's ids and PCM exactly."""
+    items = _items(dev, 3, 5)
+    kw = dict(top_k=top_k, max_tokens=130, min_tokens=min_tokens, seed=3)
+    ids_e, segs_e = _speak_all(speech_engine, items, False, **kw)
+    ids_g, segs_g = _speak_all(speech_engine, items, True, **kw)
+    assert ids_g == ids_e
+    assert [i for i, _ in segs_g] == [i for i, _ in segs_e]
+    for (_, a), (_, b) in zip(segs_g, segs_e):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_speak_graph_eos_shrinks_batch(dev, speech_engine):
+    """Sessions hitting EOS at different steps: the graph path drains, shrinks the batch and still
+    matches the eager loop token for token."""
+    tts = speech_engine.tts
+    saved = tts.out_fnn.bias.clone()
+    try:
+        tts.out_fnn.bias[tts.eos] += 3.0  # make EOS likely among the top-8 candidates
+        items = _items(dev, 4, 9)
+        kw = dict(top_k=8, max_tokens=200, seed=11)
+        ids_e, segs_e = _speak_all(speech_engine, items, False, **kw)
+        ids_g, segs_g = _speak_all(speech_engine, items, True, **kw)
+    finally:
+        tts.out_fnn.bias.copy_(saved)
+    lens = [len(x) for x in ids_e]
+    assert len(set(lens)) > 1 and min(lens) < 200   # sessions really ended at different steps
+    assert ids_g == ids_e
+    for (_, a), (_, b) in zip(segs_g, segs_e):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_codec_mfma_matches_direct_at_real_geometry(dev):
+    """Channel-last MFMA vocoder (polyphase ConvTranspose, implicit-GEMM convs) vs the channel-major
+    direct-convolution kernels, at the real TiCodec geometry (512 -> 16 channels, x600 upsampling)."""
+    from fo.codec import CodecEngine
+    from fo.weights import SynthSource
+    cfg = configs.get("real")
+    shapes = {k: v for k, v in all_shapes(cfg).items() if k.startswith("codec.")}
+    src = SynthSource(cfg["seed"], shapes, dev, cfg["overrides"])
+    eng = CodecEngine(src, cfg["codec_json"], dev)
+    rng = np.random.default_rng(5)
+    ids = torch.from_numpy(rng.integers(0, 1024, size=(3, 50))).to(dev, torch.int32)
+    a = eng(ids)
+    b = eng.forward_ncl(ids).view(3, -1)
+    assert a.shape == b.shape and a.shape[1] >= 50 * 600  # odd (k - u) stages add a few samples, as upstream
+    close(a, b.cpu().numpy(), rtol=1e-4, atol=2e-5)
