@@ -170,29 +170,25 @@ class SpeechEncoderEngine:
     def new_cache(self):
         return EncoderCache(self)
 
-    def infer(self, feats, caches, pe_indices):
-        """feats: device [B, R, 80]; caches: list[EncoderCache]; pe_indices: list[int].
-        Returns (out [B*T, d] device fp32, T, new pe_indices)."""
-        B, R, _ = feats.shape
-        dev = self.device
+    def dims(self, R):
         H1, W1 = (R - 3) // 2 + 1, (80 - 3) // 2 + 1
         H2, W2 = (H1 - 3) // 2 + 1, (W1 - 3) // 2 + 1
-        T = H2
-        assert W2 == self.F and T <= 8
-        C = self.C
-        x1 = torch.empty(B * H1 * W1, 32, dtype=F32, device=dev)
-        ops.im2col_3x3s2(feats, B, 1, R, 80, (R * 80, 0, 80, 1), x1, self.mean, self.istd)
-        y1 = self.conv1(x1, act="relu")
-        x2 = torch.empty(B * H2 * W2, self.conv2.Kp, dtype=F32, device=dev)
-        ops.im2col_3x3s2(y1, B, C, H1, W1, (H1 * W1 * C, 1, W1 * C, C), x2)
-        y2 = self.conv2(x2, act="relu")
-        z = torch.empty(B * T, C * self.F, dtype=F32, device=dev)
-        ops.tcf_permute(y2, B, T, self.F, C, z)
-        x = self.out(z)
-        x = self.embed(x)
-        ops.layernorm(x, *self.embed_ln, out=x, relu=True)
-        ops.scale_(x, math.sqrt(self.d))
-        # per-user ring / position metadata (host ints -> one small upload)
+        assert W2 == self.F and H2 <= 8
+        return H1, W1, H2, W2
+
+    def buffers(self, B, R):
+        """Every intermediate of one infer() for B users x R frames (graph capture allocates nothing)."""
+        H1, W1, H2, W2 = self.dims(R)
+        T, C, dev = H2, self.C, self.device
+        e = lambda *shape: torch.empty(*shape, dtype=F32, device=dev)  # noqa: E731
+        return {"x1": e(B * H1 * W1, 32), "y1": e(B * H1 * W1, C), "x2": e(B * H2 * W2, self.conv2.Kp),
+                "y2": e(B * H2 * W2, C), "z": e(B * T, C * self.F), "o": e(B * T, self.out.N),
+                "x": e(B * T, self.d), "h": e(B * T, self.d), "qkv": e(B * T, 3 * self.d),
+                "att": e(B * T, self.d), "f": e(B * T, self.layers[0]["ff1"].N),
+                "meta": torch.empty(4 * B, dtype=I32, device=dev)}
+
+    def host_meta(self, caches, pe_indices):
+        """Per-user ring / position metadata [starts | lens | rings | pos starts] and the next pe_index."""
         starts, lens, rings, pstarts, new_pe = [], [], [], [], []
         for c, pe in zip(caches, pe_indices):
             pe = pe % self.max_len
@@ -201,12 +197,32 @@ class SpeechEncoderEngine:
             rings.append(c.slot)
             pstarts.append(max(0, pe - self.full_chunk))
             new_pe.append(pe + self.chunk)
-        meta = torch.from_numpy(np.asarray(starts + lens + rings + pstarts, np.int32)).to(dev)
+        return np.asarray(starts + lens + rings + pstarts, np.int32), new_pe
+
+    def advance(self, caches, T):
+        """Ring bookkeeping after a chunk: keep the last buffersize frames (attention.py:415-428)."""
+        for c in caches:
+            total = c.len + T
+            keep = min(total, self.buffersize)
+            c.start = (c.start + total - keep) % self.cap
+            c.len = keep
+
+    def run(self, feats, B, R, bufs):
+        """The device part of infer(): bufs from buffers(B, R) with bufs['meta'] already uploaded."""
+        H1, W1, H2, W2 = self.dims(R)
+        T, C = H2, self.C
+        ops.im2col_3x3s2(feats, B, 1, R, 80, (R * 80, 0, 80, 1), bufs["x1"], self.mean, self.istd)
+        self.conv1(bufs["x1"], out=bufs["y1"], act="relu")
+        ops.im2col_3x3s2(bufs["y1"], B, C, H1, W1, (H1 * W1 * C, 1, W1 * C, C), bufs["x2"])
+        self.conv2(bufs["x2"], out=bufs["y2"], act="relu")
+        ops.tcf_permute(bufs["y2"], B, T, self.F, C, bufs["z"])
+        self.out(bufs["z"], out=bufs["o"])
+        x = self.embed(bufs["o"], out=bufs["x"])
+        ops.layernorm(x, *self.embed_ln, out=x, relu=True)
+        ops.scale_(x, math.sqrt(self.d))
+        meta = bufs["meta"]
         st, ln, rg, ps = meta[:B], meta[B:2 * B], meta[2 * B:3 * B], meta[3 * B:]
-        h = torch.empty_like(x)
-        qkv = torch.empty(B * T, 3 * self.d, dtype=F32, device=dev)
-        att = torch.empty(B * T, self.d, dtype=F32, device=dev)
-        f = None
+        h, qkv, att, f = bufs["h"], bufs["qkv"], bufs["att"], bufs["f"]
         scale = 1.0 / math.sqrt(self.dk)
         for i, L in enumerate(self.layers):
             ops.layernorm(x, *L["ln1"], out=h)
@@ -217,14 +233,20 @@ class SpeechEncoderEngine:
                                  L["bv"], B, T, self.h, self.dk, scale, att)
             L["out"](att, out=x, residual=True)
             ops.layernorm(x, *L["ln2"], out=h)
-            f = L["ff1"](h, out=f, act="relu")
+            L["ff1"](h, out=f, act="relu")
             L["ff2"](f, out=x, residual=True)
         ops.layernorm(x, *self.after, out=x)
-        for c in caches:
-            total = c.len + T
-            keep = min(total, self.buffersize)
-            c.start = (c.start + total - keep) % self.cap
-            c.len = keep
+        return x, T
+
+    def infer(self, feats, caches, pe_indices):
+        """feats: device [B, R, 80]; caches: list[EncoderCache]; pe_indices: list[int].
+        Returns (out [B*T, d] device fp32, T, new pe_indices)."""
+        B, R, _ = feats.shape
+        bufs = self.buffers(B, R)
+        meta, new_pe = self.host_meta(caches, pe_indices)
+        bufs["meta"].copy_(torch.from_numpy(meta))
+        x, T = self.run(feats, B, R, bufs)
+        self.advance(caches, T)
         return x, T, new_pe
 
 
@@ -265,14 +287,28 @@ class AdapterEngine:
     def new_cache(self):
         return AdapterCache(self)
 
+    def out_len(self, T):
+        return (self.k - 1 + T - self.k) // 2 + 1
+
+    def buffers(self, B, T):
+        To, dev = self.out_len(T), self.device
+        return {"cols": torch.empty(B * To, self.conv.Kp, dtype=F32, device=dev),
+                "y": torch.empty(B * To, self.conv.N, dtype=F32, device=dev),
+                "out": torch.empty(B * To, self.project.N, dtype=F32, device=dev),
+                "slots": torch.empty(B, dtype=I32, device=dev)}
+
+    def run(self, x, B, T, bufs):
+        """Device part of __call__ with bufs['slots'] uploaded."""
+        KC = self.k - 1
+        slots = bufs["slots"]
+        ops.im2col_conv1d(self.cache, slots, x, B, KC, T, self.d, self.k, 2, bufs["cols"])
+        ops.conv_cache_update(self.cache, slots, x, B, KC, T, self.d)
+        self.conv(bufs["cols"], out=bufs["y"], act="relu")
+        return self.project(bufs["y"], out=bufs["out"]), self.out_len(T)
+
     def __call__(self, x, T, caches):
         """x: device [B*T, d]; returns (out [B*To, L], To)."""
         B = len(caches)
-        KC = self.k - 1
-        To = (KC + T - self.k) // 2 + 1
-        slots = torch.tensor([c.slot for c in caches], dtype=I32).to(self.device)
-        cols = torch.empty(B * To, self.conv.Kp, dtype=F32, device=self.device)
-        ops.im2col_conv1d(self.cache, slots, x, B, KC, T, self.d, self.k, 2, cols)
-        ops.conv_cache_update(self.cache, slots, x, B, KC, T, self.d)
-        y = self.conv(cols, act="relu")
-        return self.project(y), To
+        bufs = self.buffers(B, T)
+        bufs["slots"].copy_(torch.tensor([c.slot for c in caches], dtype=I32))
+        return self.run(x, B, T, bufs)

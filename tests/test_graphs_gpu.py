@@ -1,0 +1,52 @@
+"""Captured listen step (fo.engine.ListenGraph) against the eager launch sequence."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def eng(dev):
+    from fo.engine import FreezeOmniEngine
+    return FreezeOmniEngine(os.path.join(ROOT, "configs", "tiny"), device=dev, max_sessions=16)
+
+
+def _session_run(eng, feats_seq, graph, n_users):
+    base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    kvs = [base.fork() for _ in range(n_users)]
+    state = [dict(enc_cache=None, ada_cache=None, pe_index=0) for _ in range(n_users)]
+    out = []
+    for c, f in enumerate(feats_seq):
+        items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=f[u], kv=kvs[u], **state[u])
+                 for u in range(n_users)]
+        res = eng.listen(items, graph=graph)
+        for u, r in enumerate(res):
+            state[u] = dict(enc_cache=r["enc_cache"], ada_cache=r["ada_cache"], pe_index=r["pe_index"])
+        h, row = res[0]["hidden_row"]
+        out.append(([(r["probs"]["state_1"], r["probs"]["state_2"]) for r in res],
+                    [h[rr].cpu().numpy().copy() for rr in [r["hidden_row"][1] for r in res]],
+                    [kv.length for kv in kvs], [r["pe_index"] for r in res]))
+    for kv in kvs:
+        kv.free()
+    base.free()
+    return out
+
+
+def test_listen_graph_matches_eager(eng, dev):
+    g = np.load(os.path.join(G, "fbank.npz"))
+    n_users = 3
+    feats = torch.from_numpy(g["A_feats"]).to(dev)          # [13, 19, 80]
+    seq = [torch.stack([feats[(c + 4 * u) % 13] for u in range(n_users)]) for c in range(7)]
+    eager = _session_run(eng, seq, False, n_users)
+    graph = _session_run(eng, seq, True, n_users)
+    assert len(eng._lgraphs) >= 1                             # the graph path really ran
+    for (pe, he, le, qe), (pg, hg, lg, qg) in zip(eager, graph):
+        assert le == lg and qe == qg
+        np.testing.assert_allclose(np.array(pg), np.array(pe), atol=1e-5)
+        for a, b in zip(hg, he):
+            np.testing.assert_allclose(a, b, atol=2e-5, rtol=1e-5)
