@@ -58,8 +58,8 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
 }
 
 // Output element (m, n): bias, folded-BN affine, activation or SwiGLU, residual, store.
-__device__ __forceinline__ void epilogue_store(const GemmArgs& a, int NT, int m, int n, float v, float u) {
-  if (NT == 2) {
+__device__ __forceinline__ void epilogue_store(const GemmArgs& a, bool sw, int m, int n, float v, float u) {
+  if (sw) {
     v = v / (1.f + expf(-v)) * u;
   } else {
     if (a.bias) v += a.bias[n];
@@ -78,7 +78,8 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int NT, int m,
   }
 }
 
-template <int NT, int RB, bool XF32, int NW, int U>
+// NT packed 16-column tiles per workgroup (SW: NT/2 interleaved gate/up pairs -> NT/2 output tiles)
+template <int NT, int RB, bool XF32, int NW, int U, bool SW>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
   // NW waves split K inside the workgroup; each keeps U k-steps of weights in flight
@@ -187,72 +188,66 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     }
     return;
   }
-  for (int e = threadIdx.x; e < ROWS * 16; e += NTH) {
-    const int rr = e >> 4, c = e & 15;
+  constexpr int LT = SW ? NT / 2 : NT;  // logical output tiles
+  for (int e = threadIdx.x; e < LT * ROWS * 16; e += NTH) {
+    const int lt = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
     const int m = m0 + rr;
-    const int n = tg * 16 + c;
+    const int n = (tg * LT + lt) * 16 + c;
     if (m >= a.M || n >= a.N) continue;
-    epilogue_store(a, NT, m, n, red[0][0][rr][c], NT == 2 ? red[0][1][rr][c] : 0.f);
+    if (SW) epilogue_store(a, true, m, n, red[0][2 * lt][rr][c], red[0][2 * lt + 1][rr][c]);
+    else epilogue_store(a, false, m, n, red[0][lt][rr][c], 0.f);
   }
 }
 
 // Sum of the S partial slabs + epilogue for the split-K path (grid-stride over M x N outputs).
-__global__ void k_gemm_reduce(GemmArgs a, int NT, int Mrows) {
+__global__ void k_gemm_reduce(GemmArgs a, int sw, int Mrows) {
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
   const long long total = (long long)a.M * a.N;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
     const int m = (int)(e / a.N), n = (int)(e % a.N);
-    const int col = NT == 2 ? (n >> 4) * 32 + (n & 15) : n;
+    const int col = sw ? (n >> 4) * 32 + (n & 15) : n;
     float v = 0.f, u = 0.f;
     for (int q = 0; q < a.S; ++q) {
       const float* p = a.ws + q * slab + (size_t)m * Ncols + col;
       v += p[0];
-      if (NT == 2) u += p[16];
+      if (sw) u += p[16];
     }
-    epilogue_store(a, NT, m, n, v, u);
+    epilogue_store(a, sw != 0, m, n, v, u);
   }
 }
 
 // Same body under two symbols so profiles separate the multi-10-MB weight streams (Qwen2 MLP,
 // lm_head: >= 64 MB of bf16 per launch) from every other linear layer.
-template <int NT, int RB, bool XF32, int NW, int U>
+template <int NT, int RB, bool XF32, int NW, int U, bool SW>
 __global__ __launch_bounds__(NW * 64) void k_gemm(GemmArgs a) {
-  gemm_body<NT, RB, XF32, NW, U>(a);
+  gemm_body<NT, RB, XF32, NW, U, SW>(a);
 }
-template <int NT, int RB, bool XF32, int NW, int U>
+template <int NT, int RB, bool XF32, int NW, int U, bool SW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
-  gemm_body<NT, RB, XF32, NW, U>(a);
+  gemm_body<NT, RB, XF32, NW, U, SW>(a);
 }
 
-template <int NT, int RB, int NW, int U>
+template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
   if (wstream) {
-    if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, U>), grid, dim3(NW * 64), 0, s, a);
-    else hipLaunchKernelGGL((k_gemm_wstream<NT, RB, false, NW, U>), grid, dim3(NW * 64), 0, s, a);
+    if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
+    else hipLaunchKernelGGL((k_gemm_wstream<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
   } else {
-    if (x_f32) hipLaunchKernelGGL((k_gemm<NT, RB, true, NW, U>), grid, dim3(NW * 64), 0, s, a);
-    else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U>), grid, dim3(NW * 64), 0, s, a);
+    if (x_f32) hipLaunchKernelGGL((k_gemm<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
+    else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
   }
 }
 
-// (waves, k-steps in flight per wave) for the M <= 16 kernels; 0 = automatic
-thread_local int g_force_nw = 0, g_force_u = 0;
+// forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
+thread_local int g_force_nw = 0, g_force_nt = 0;
 
-template <int NT>
-void launch_rb1(int nw, int u, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
-  if (nw == 16) {
-    if (u >= 8) launch_gemm<NT, 1, 16, 8>(wstream, x_f32, grid, a, s);
-    else launch_gemm<NT, 1, 16, 4>(wstream, x_f32, grid, a, s);
-  } else if (nw == 8) {
-    if (u >= 16) launch_gemm<NT, 1, 8, 16>(wstream, x_f32, grid, a, s);
-    else if (u >= 8) launch_gemm<NT, 1, 8, 8>(wstream, x_f32, grid, a, s);
-    else launch_gemm<NT, 1, 8, 4>(wstream, x_f32, grid, a, s);
-  } else {
-    if (u >= 8) launch_gemm<NT, 1, 4, 8>(wstream, x_f32, grid, a, s);
-    else launch_gemm<NT, 1, 4, 4>(wstream, x_f32, grid, a, s);
-  }
+template <int NT, bool SW>
+void launch_rb1_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
+  if (nw == 16) launch_gemm<NT, 1, 16, 4, SW>(wstream, x_f32, grid, a, s);
+  else if (nw == 8) launch_gemm<NT, 1, 8, 4, SW>(wstream, x_f32, grid, a, s);
+  else launch_gemm<NT, 1, 4, 4, SW>(wstream, x_f32, grid, a, s);
 }
 
 // Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
@@ -342,18 +337,33 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
   a.act = act;
   a.out_bf16 = out_bf16;
   a.residual = residual;
-  const int NT = swiglu ? 2 : 1;
-  a.ntiles = NT * ((N + 15) / 16);
-  const int groups = a.ntiles / NT;
-  int S = splitk > 0 ? splitk : fo_gemm_pick_split(M, groups, K);
-  if (S > (K >> 5)) S = K >> 5;
-  a.S = S;
+  a.ntiles = (swiglu ? 2 : 1) * ((N + 15) / 16);
   const int RB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   const int mt = (M + RB * 16 - 1) / (RB * 16);
+  // tiles per workgroup: the activation rows are re-read by every workgroup, so workgroups that
+  // cover more output columns read X fewer times per weight byte (measured, gemm_sweep.py)
+  int NT = swiglu ? 2 : 1;
+  int S_auto = 0;
+  const int KS = K >> 5;
+  if (RB == 1) {
+    // measured policy (gemm_sweep.py): wide layers (>= 1024 tiles: Qwen2 gate/up, lm_head) take 4
+    // tiles per workgroup; long-K layers (Qwen2 down) 4 tiles and a 4-way K split; mid-size grids
+    // (> 256 tiles: Qwen2 qkv) 2 tiles; small ones 1
+    if (a.ntiles >= 1024) NT = 4;
+    else if (KS >= 256 && a.ntiles >= 128) { NT = 4; S_auto = 4; }
+    else if (a.ntiles > 256) NT = 2;
+    if (g_force_nt) NT = g_force_nt;
+    FO_REQUIRE(NT == 1 || NT == 2 || NT == 4, "fo_gemm: tiles per workgroup %d", NT);
+    FO_REQUIRE(!swiglu || NT >= 2, "fo_gemm: swiglu needs tile pairs");
+    if (a.ntiles % NT) NT = swiglu ? 2 : 1;
+  }
+  const int groups = a.ntiles / NT;
+  int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : fo_gemm_pick_split(M, groups, K));
+  if (S > (K >> 5)) S = K >> 5;
+  a.S = S;
   if (S > 1) {
     const long long need = (long long)S * mt * RB * 16 * a.ntiles * 16;
-    FO_REQUIRE(ws && counters && need <= ws_floats, "fo_gemm: split-K workspace too small (%lld > %lld)", need,
-               ws_floats);
+    FO_REQUIRE(ws && need <= ws_floats, "fo_gemm: split-K workspace too small (%lld > %lld)", need, ws_floats);
   }
   dim3 grid(groups, mt, S);
   const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
@@ -361,21 +371,26 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
   if (RB == 1) {
     // measured (scripts/gemm_sweep.py, MI355X): one workgroup per CU wants 16 waves, a couple per
     // CU 8, many 4; 4 k-steps in flight per wave is the sweet spot everywhere on the hot path
-    int nw = wgs <= 256 ? 16 : (wgs < 1024 ? 8 : 4), u = 4;
+    int nw = wgs <= 160 ? 16 : (wgs <= 256 ? (NT == 1 ? 16 : 8) : ((NT == 4 || wgs >= 1024) ? 4 : 8));
     if (g_force_nw) nw = g_force_nw;
-    if (g_force_u) u = g_force_u;
-    if (NT == 1) launch_rb1<1>(nw, u, wstream, x_f32, grid, a, stream);
-    else launch_rb1<2>(nw, u, wstream, x_f32, grid, a, stream);
+    if (swiglu) {
+      if (NT == 4) launch_rb1_nw<4, true>(nw, wstream, x_f32, grid, a, stream);
+      else launch_rb1_nw<2, true>(nw, wstream, x_f32, grid, a, stream);
+    } else {
+      if (NT == 4) launch_rb1_nw<4, false>(nw, wstream, x_f32, grid, a, stream);
+      else if (NT == 2) launch_rb1_nw<2, false>(nw, wstream, x_f32, grid, a, stream);
+      else launch_rb1_nw<1, false>(nw, wstream, x_f32, grid, a, stream);
+    }
   } else if (RB == 2) {
-    if (NT == 1) launch_gemm<1, 2, 8, 4>(wstream, x_f32, grid, a, stream);
-    else launch_gemm<2, 2, 8, 4>(wstream, x_f32, grid, a, stream);
+    if (swiglu) launch_gemm<2, 2, 8, 4, true>(wstream, x_f32, grid, a, stream);
+    else launch_gemm<1, 2, 8, 4, false>(wstream, x_f32, grid, a, stream);
   } else {
     if (x_f32) {
-      if (NT == 1) launch_gemm<1, 4, 4, 2>(wstream, x_f32, grid, a, stream);
-      else launch_gemm<2, 4, 4, 2>(wstream, x_f32, grid, a, stream);
+      if (swiglu) launch_gemm<2, 4, 4, 2, true>(wstream, x_f32, grid, a, stream);
+      else launch_gemm<1, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
     } else {
-      if (NT == 1) launch_gemm<1, 4, 4, 4>(wstream, x_f32, grid, a, stream);
-      else launch_gemm<2, 4, 4, 4>(wstream, x_f32, grid, a, stream);
+      if (swiglu) launch_gemm<2, 4, 4, 4, true>(wstream, x_f32, grid, a, stream);
+      else launch_gemm<1, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
     }
   }
   if (S > 1) {
@@ -384,17 +399,17 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
     const long long total = (long long)M * N;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_gemm_reduce, dim3(blocks), dim3(256), 0, stream, a, NT, mt * RB * 16);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(blocks), dim3(256), 0, stream, a, swiglu, mt * RB * 16);
   }
   return fo::check_launch("fo_gemm");
 }
 
-// Force (waves, k-steps per wave) of the M <= 16 kernels on this thread (0 = automatic); for sweeps.
-int fo_gemm_tune(int nw, int u) {
+// Force (waves, tiles per workgroup) of the M <= 16 kernels on this thread (0 = automatic); sweeps.
+int fo_gemm_tune(int nw, int nt) {
   FO_REQUIRE(nw == 0 || nw == 4 || nw == 8 || nw == 16, "fo_gemm_tune: nw must be 0/4/8/16");
-  FO_REQUIRE(u == 0 || u == 4 || u == 8 || u == 16, "fo_gemm_tune: u must be 0/4/8/16");
+  FO_REQUIRE(nt == 0 || nt == 1 || nt == 2 || nt == 4, "fo_gemm_tune: nt must be 0/1/2/4");
   g_force_nw = nw;
-  g_force_u = u;
+  g_force_nt = nt;
   return 0;
 }
 

@@ -42,8 +42,8 @@ int fo_event_destroy(void* ev);
  *   adapter conv/project (models/adapter.py:670,679), TTS Llama layers + out_fnn
  *   (models/decoder/decoder.py:299-311,346).
  * W is packed once by fo_pack_weight into MFMA fragment order. */
-/* sweep hook: force (waves, k-steps in flight per wave) of the M <= 16 GEMM kernels; 0 = automatic */
-int fo_gemm_tune(int nw, int u);
+/* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
+int fo_gemm_tune(int nw, int nt);
 long long fo_pack_weight_elems(int N, int K);
 int fo_pack_weight(const void* W, int src_bf16, int N, int K, int ldw, void* out, int tile_base, int tile_stride,
                    hipStream_t stream);

@@ -27,7 +27,7 @@ def timeit(fn, reps=30):
     return ms.value / reps * 1e3
 
 
-shapes = [("qwen_qkv", 4608, 3584, 16, False), ("qwen_o", 3584, 3584, 16, False), ("qwen_down", 3584, 18944, 16, False),
+shapes = [("qwen_down_m8", 3584, 18944, 8, False), ("qwen_gu_m8", 18944, 3584, 8, True), ("qwen_qkv", 4608, 3584, 16, False), ("qwen_o", 3584, 3584, 16, False), ("qwen_down", 3584, 18944, 16, False),
           ("qwen_gu", 18944, 3584, 16, True), ("tts_qkv", 2688, 896, 8, False), ("tts_o", 896, 896, 8, False),
           ("tts_gu", 4864, 896, 8, True), ("tts_down", 896, 4864, 8, False), ("lm_head", 152064, 3584, 8, False)]
 dev = torch.device("cuda:0")
@@ -40,12 +40,13 @@ for name, N, K, M, sw in shapes:
     ref = lin(x, out=torch.empty(M, N, device=dev)).clone()
     auto = timeit(lambda: lin(x, out=out))
     res = []
-    for nw, u in ((4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 4), (16, 8)):
-        for S in (1, 2, 4):
-            lib.fo_gemm_tune(nw, u)
-            t = timeit(lambda: lin(x, out=out, splitk=S))
-            err = (out - ref).abs().max().item()
-            res.append((t, f"nw{nw}u{u}S{S}:{t:6.1f}" + ("" if err < 1e-3 else f"(ERR {err:.2g})")))
+    for nw in (4, 8, 16):
+        for nt in ((2, 4) if sw else (1, 2, 4)):
+            for S in (1, 2, 4):
+                lib.fo_gemm_tune(nw, nt)
+                t = timeit(lambda: lin(x, out=out, splitk=S))
+                err = (out - ref).abs().max().item()
+                res.append((t, f"nw{nw}nt{nt}S{S}:{t:6.1f}" + ("" if err < 1e-3 else f"(ERR {err:.2g})")))
     lib.fo_gemm_tune(0, 0)
     res.sort()
     print(f"{name:9s} M={M:2d} N={N:6d} K={K:5d} {lin.nbytes / 1e6:7.1f}MB auto {auto:6.1f}us "
