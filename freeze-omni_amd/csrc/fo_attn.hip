@@ -72,34 +72,56 @@ struct AttnArgs {
 constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
 constexpr int MAXPG = 256;  // pages of one split staged in LDS (fo_attn_nsplit keeps splits <= 4096 keys)
 
-// One work item = up to RMAX query rows (tokens x GQA group) of ONE sequence against one kv head,
-// over split `sp` of that sequence's keys.  K/V tiles of 64 keys are loaded with 16-B coalesced
-// loads into registers one tile ahead (the next tile's loads are in flight while the current tile
-// is computed), staged through LDS, and consumed by all rows: a sequence's keys cross HBM once per
-// kv head no matter how many of its tokens are in the batch.  Online softmax per row (a row's
-// 64 scores of a tile are one wave's 64 lanes); fp32 throughout.
-template <int HD, int RMAX>
-__global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
-  constexpr int KP = HD + 4;          // padded K row: lanes j read k_s[j][d..d+3] conflict-free
-  constexpr int D4 = HD / 4;
-  constexpr int LPT = KT * D4 / 256;  // float4 per thread per tile (K and V each)
-  constexpr int RG = 256 / HD;        // row groups in the PV phase (thread owns column tid % HD)
-  constexpr int NACC = RMAX / RG;
-  constexpr int RPW = RMAX / 4;       // rows per wave in the score phase
-  __shared__ float q_s[RMAX][HD];
-  __shared__ float k_s[KT][KP];
-  __shared__ float v_s[KT][HD];
-  __shared__ float p_s[RMAX][KT + 4];
-  __shared__ float alpha_s[RMAX];
-  __shared__ float ml_s[RMAX][2];
-  __shared__ int nvis_s[RMAX];
+// fp32 -> bf16 hi + lo: two bf16 operands whose sum carries ~16 mantissa bits
+__device__ __forceinline__ void split8(const float* f, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const __bf16 h = (__bf16)f[i];
+    hi[i] = h;
+    lo[i] = (__bf16)(f[i] - (float)h);
+  }
+}
+
+// sum / max over the 16 lanes of a row group (lanes l, l^1, l^2, l^4, l^8)
+__device__ __forceinline__ float row16_max(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One work item = up to 16 query rows (a sequence's batch tokens x the GQA group sharing one kv head)
+// against that kv head, over split `sp` of the sequence's keys, on the matrix cores:
+//   S = Q K^T   (A = Q rows, B = K rows read straight from the paged cache in B-fragment order)
+//   O = P V     (A = P through LDS, B = V staged in LDS as [key][d])
+// 64-key tiles, one 16-key column block per wave; K and V of the next tile are loaded into registers
+// while the current tile computes.  Every fp32 operand is split into bf16 hi + lo and each product
+// uses three MFMAs (hi*hi + hi*lo + lo*hi), so scores and outputs keep ~fp32 accuracy.  Online
+// softmax per row with the running max exchanged across the 4 waves through LDS.
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
+  constexpr int DC = HD / 32;            // 32-wide d chunks (score k-steps)
+  constexpr int NTILE = HD / 16;         // 16-wide d tiles of the output
+  constexpr int NTW = (NTILE + 3) / 4;   // output tiles per wave
+  constexpr int VP = HD + 2;             // V row pitch: the 4 key groups of a B fragment hit distinct banks
+  constexpr int VL = KT * HD / 4 / 256;  // float4 of V per thread per tile
+  __shared__ float v_s[KT][VP];
+  __shared__ float p_s[16][KT + 4];
+  __shared__ float mx_s[4][16];
+  __shared__ float l_s[4][16];
+  __shared__ int nvis_s[16];
   __shared__ int pg_s[MAXPG];
 
   const int it = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
   const int seq = a.items[3 * it], t0 = a.items[3 * it + 1], tn = a.items[3 * it + 2];
   const int G = a.H / a.KVH;
-  const int R = tn * G;
+  const int R = tn * G;  // <= 16
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int grp = lane >> 4, col = lane & 15;
   int Lmax = 0;
   for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
   const int per = ((Lmax + a.nsplit - 1) / a.nsplit + KT - 1) / KT * KT;
@@ -112,15 +134,6 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
     }
     return;
   }
-  for (int e = tid; e < RMAX * D4; e += 256) {  // rows >= R duplicate row R-1 (never output)
-    const int r = e / D4, d4 = e % D4, rr = min(r, R - 1);
-    float4 v = *reinterpret_cast<const float4*>(a.q + ((size_t)(t0 + rr / G) * a.H + kvh * G + rr % G) * HD + d4 * 4);
-    v.x *= a.scale; v.y *= a.scale; v.z *= a.scale; v.w *= a.scale;
-    *reinterpret_cast<float4*>(&q_s[r][d4 * 4]) = v;
-  }
-  if (tid < RMAX) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
-
-  // the split's block-table slice goes to LDS once, so tile loads never wait on a dependent global load
   const int* bt = a.block_table + (size_t)seq * a.maxb;
   const int pb = c0 / a.PS, npg = (c1 - 1) / a.PS - pb + 1;
   if (npg > MAXPG) {  // host contract broken (split wider than 4096 keys): poison rather than read wrong keys
@@ -128,141 +141,169 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a) {
     return;
   }
   for (int i = tid; i < npg; i += 256) pg_s[i] = bt[pb + i];
-  __syncthreads();
+  if (tid < 16) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
+
+  // Q as A fragments: row = col (lane & 15), d = 32 c + 8 grp; rows >= R are zero
+  bf16x8 qh[DC], ql[DC];
+  {
+    const int r = col < R ? col : R - 1;
+    const float* qr = a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + 8 * grp;
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+      float f[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(qr + 32 * c);
+      const float4 x1 = *reinterpret_cast<const float4*>(qr + 32 * c + 4);
+      const float sc = col < R ? a.scale : 0.f;
+      f[0] = x0.x * sc; f[1] = x0.y * sc; f[2] = x0.z * sc; f[3] = x0.w * sc;
+      f[4] = x1.x * sc; f[5] = x1.y * sc; f[6] = x1.z * sc; f[7] = x1.w * sc;
+      split8(f, qh[c], ql[c]);
+    }
+  }
+  __syncthreads();  // pg_s, nvis_s
+
   const size_t head_off = (size_t)kvh * a.PS * HD;
   const size_t page_sz = (size_t)a.KVH * a.PS * HD;
-  float4 kreg[LPT], vreg[LPT];
-  // K/V tile [k0, k0 + 64) into registers.  A macro, not a lambda (a captured array would live in
-  // scratch).  Full tiles load branch-free (a per-element "load or zero" makes hipcc wait vmcnt(0)
-  // per load); only the split's last, partial tile takes the guarded path.
-#define FO_ATTN_LOAD_TILE(K0)                                                                              \
-  if ((K0) + KT <= c1) {                                                                                   \
-    _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                      \
-      const int e = tid + 256 * i, j = e / D4, d4 = e % D4, p = (K0) + j;                                  \
-      const size_t off = (size_t)pg_s[p / a.PS - pb] * page_sz + head_off + (size_t)(p % a.PS) * HD + d4 * 4; \
-      kreg[i] = *reinterpret_cast<const float4*>(a.kc + off);                                              \
-      vreg[i] = *reinterpret_cast<const float4*>(a.vc + off);                                              \
-    }                                                                                                      \
-  } else {                                                                                                 \
-    _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                      \
-      const int e = tid + 256 * i, j = e / D4, d4 = e % D4, p = (K0) + j;                                  \
-      if (p < c1) {                                                                                        \
-        const size_t off = (size_t)pg_s[p / a.PS - pb] * page_sz + head_off + (size_t)(p % a.PS) * HD + d4 * 4; \
-        kreg[i] = *reinterpret_cast<const float4*>(a.kc + off);                                            \
-        vreg[i] = *reinterpret_cast<const float4*>(a.vc + off);                                            \
-      } else {                                                                                             \
-        kreg[i] = make_float4(0.f, 0.f, 0.f, 0.f);                                                         \
-        vreg[i] = kreg[i];                                                                                 \
-      }                                                                                                    \
-    }                                                                                                      \
+  float4 kreg[2 * DC], vreg[VL];
+  // K: this lane's key (16 per wave) x its 8-wide d slices; V: cooperative 16-B rows for LDS
+#define FO_ATTN_LOAD(K0)                                                                                  \
+  {                                                                                                       \
+    const int pk = min((K0) + 16 * wave + col, c1 - 1);                                                   \
+    const float* kr = a.kc + (size_t)pg_s[pk / a.PS - pb] * page_sz + head_off + (size_t)(pk % a.PS) * HD \
+                      + 8 * grp;                                                                          \
+    _Pragma("unroll") for (int c = 0; c < DC; ++c) {                                                      \
+      kreg[2 * c] = *reinterpret_cast<const float4*>(kr + 32 * c);                                        \
+      kreg[2 * c + 1] = *reinterpret_cast<const float4*>(kr + 32 * c + 4);                                \
+    }                                                                                                     \
+    _Pragma("unroll") for (int i = 0; i < VL; ++i) {                                                      \
+      const int e = tid + 256 * i, j = e / (HD / 4), d4 = e % (HD / 4);                                   \
+      const int pv = min((K0) + j, c1 - 1);                                                               \
+      vreg[i] = *reinterpret_cast<const float4*>(a.vc + (size_t)pg_s[pv / a.PS - pb] * page_sz + head_off \
+                                                 + (size_t)(pv % a.PS) * HD + d4 * 4);                    \
+    }                                                                                                     \
   }
-  float m_run[RPW], l_run[RPW], acc[NACC];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
-#pragma unroll
-  for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
-  const int d = tid % HD, rg = tid / HD;
 
-  FO_ATTN_LOAD_TILE(c0)
+  float m_run[4], l_lane[4];
+  f32x4 acc[NTW];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m_run[i] = -INFINITY; l_lane[i] = 0.f; }
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  FO_ATTN_LOAD(c0)
   for (int k0 = c0; k0 < c1; k0 += KT) {
-    __syncthreads();  // readers of the previous tile are done (first pass: q_s / nvis_s visible)
+    __syncthreads();  // the previous tile's p_s / v_s readers are done
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int e = tid + 256 * i, j = e / D4, d4 = e % D4;
-      *reinterpret_cast<float4*>(&k_s[j][d4 * 4]) = kreg[i];
-      *reinterpret_cast<float4*>(&v_s[j][d4 * 4]) = vreg[i];
+    for (int i = 0; i < VL; ++i) {
+      const int e = tid + 256 * i, j = e / (HD / 4), d4 = e % (HD / 4);
+      *reinterpret_cast<float2*>(&v_s[j][d4 * 4]) = make_float2(vreg[i].x, vreg[i].y);
+      *reinterpret_cast<float2*>(&v_s[j][d4 * 4 + 2]) = make_float2(vreg[i].z, vreg[i].w);
     }
-    if (k0 + KT < c1) {
-      FO_ATTN_LOAD_TILE(k0 + KT)
+    bf16x8 kh[DC], kl[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+      const float f[8] = {kreg[2 * c].x, kreg[2 * c].y, kreg[2 * c].z, kreg[2 * c].w,
+                          kreg[2 * c + 1].x, kreg[2 * c + 1].y, kreg[2 * c + 1].z, kreg[2 * c + 1].w};
+      split8(f, kh[c], kl[c]);
     }
-    __syncthreads();
-    const int nk = min(KT, c1 - k0);
-    // scores: wave w owns rows w, w+4, ...; lane = key.  Rows go in blocks of 4 with a wave-uniform
-    // guard, and the inner loops are branch-free so LDS reads batch instead of serialising.
-    float sc[RPW];
+    if (k0 + KT < c1) FO_ATTN_LOAD(k0 + KT)
+    // S[r = 4 grp + i][key = k0 + 16 wave + col]
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ib = 0; ib < RPW; ib += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sc[ib + u] = 0.f;
-      if (wave + 4 * ib < R) {
-#pragma unroll 4
-        for (int d4 = 0; d4 < D4; ++d4) {
-          const float4 kk = *reinterpret_cast<const float4*>(&k_s[lane][d4 * 4]);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float4 qq = *reinterpret_cast<const float4*>(&q_s[wave + 4 * (ib + u)][d4 * 4]);
-            sc[ib + u] += qq.x * kk.x + qq.y * kk.y + qq.z * kk.z + qq.w * kk.w;
-          }
-        }
-      }
+    for (int c = 0; c < DC; ++c) {
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[c], kh[c], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[c], kl[c], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ql[c], kh[c], s, 0, 0, 0);
     }
-    // online softmax per row (a row's 64 scores are this wave's 64 lanes)
+    const int key = k0 + 16 * wave + col;
+    bool valid[4];
+    float mw[4];
 #pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      const int r = wave + 4 * i;
-      if (r < R) {
-        const bool valid = lane < nk && k0 + lane < nvis_s[r];
-        const float x = valid ? sc[i] : -INFINITY;
-        const float mo = m_run[i];
-        const float mn = fmaxf(mo, wave_max(x));
-        const float p = valid ? expf(x - mn) : 0.f;
-        const float al = (mo == mn) ? 1.f : expf(mo - mn);
-        l_run[i] = l_run[i] * al + p;  // per-lane partial; reduced once after the last tile
-        m_run[i] = mn;
-        p_s[r][lane] = p;
-        if (lane == 0) alpha_s[r] = al;
-      }
+    for (int i = 0; i < 4; ++i) {
+      valid[i] = key < c1 && key < nvis_s[4 * grp + i];
+      mw[i] = row16_max(valid[i] ? s[i] : -INFINITY);
+    }
+    if (col == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx_s[wave][4 * grp + i] = mw[i];
     }
     __syncthreads();
-    // PV: thread owns column d for rows rg, rg+RG, ...; keys in steps of 4 (p_s rows are 16-B aligned;
-    // keys past nk have p = 0 and zero V)
+    float alpha[4];
 #pragma unroll
-    for (int i = 0; i < NACC; ++i) acc[i] *= alpha_s[min(rg + RG * i, RMAX - 1)];
-    for (int j = 0; j < nk; j += 4) {
-      const float v0 = v_s[j][d], v1 = v_s[j + 1][d], v2 = v_s[j + 2][d], v3 = v_s[j + 3][d];
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * grp + i;
+      const float tm = fmaxf(fmaxf(mx_s[0][r], mx_s[1][r]), fmaxf(mx_s[2][r], mx_s[3][r]));
+      const float mn = fmaxf(m_run[i], tm);
+      alpha[i] = (m_run[i] == mn) ? 1.f : expf(m_run[i] - mn);
+      m_run[i] = mn;
+      const float p = valid[i] ? expf(s[i] - mn) : 0.f;
+      l_lane[i] = l_lane[i] * alpha[i] + p;
+      p_s[r][16 * wave + col] = p;
+    }
+    __syncthreads();  // p_s and v_s complete
+    // O[r][d] += P[r][:] V[:][d] for this wave's d tiles
 #pragma unroll
-      for (int ib = 0; ib < NACC; ib += 4) {
-        if (rg + RG * ib < R) {
+    for (int n = 0; n < NTW; ++n) {
 #pragma unroll
-          for (int u = 0; u < 4 && ib + u < NACC; ++u) {
-            const float4 pp = *reinterpret_cast<const float4*>(&p_s[rg + RG * (ib + u)][j]);
-            acc[ib + u] += pp.x * v0 + pp.y * v1 + pp.z * v2 + pp.w * v3;
-          }
+      for (int i = 0; i < 4; ++i) acc[n][i] *= alpha[i];
+    }
+#pragma unroll
+    for (int kc = 0; kc < KT / 32; ++kc) {
+      bf16x8 ph, pl;
+      {
+        const float4 x0 = *reinterpret_cast<const float4*>(&p_s[col][32 * kc + 8 * grp]);
+        const float4 x1 = *reinterpret_cast<const float4*>(&p_s[col][32 * kc + 8 * grp + 4]);
+        const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        split8(f, ph, pl);
+      }
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) {
+        const int dt = wave + 4 * n;
+        if (dt < NTILE) {
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = v_s[32 * kc + 8 * grp + e][16 * dt + col];
+          bf16x8 vh, vl;
+          split8(f, vh, vl);
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vh, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vl, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vh, acc[n], 0, 0, 0);
         }
       }
     }
   }
+#undef FO_ATTN_LOAD
+  // row sums: 16 lanes of the row group, then the 4 waves
+  float lw[4];
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int r = wave + 4 * i;
-    if (r < R) {
-      const float l = wave_sum(l_run[i]);
-      if (lane == 0) {
-        ml_s[r][0] = m_run[i];
-        ml_s[r][1] = l;
-      }
-    }
+  for (int i = 0; i < 4; ++i) lw[i] = row16_sum(l_lane[i]);
+  if (col == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) l_s[wave][4 * grp + i] = lw[i];
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < NACC; ++i) {
-    const int r = rg + RG * i;
-    if (r < R) {
-      const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * grp + i;
+    if (r >= R) continue;
+    const float l = l_s[0][r] + l_s[1][r] + l_s[2][r] + l_s[3][r];
+    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) {
+      const int dt = wave + 4 * n;
+      if (dt >= NTILE) continue;
+      const int d = 16 * dt + col;
       if (a.nsplit == 1) {
-        a.out[th * HD + d] = acc[i] / ml_s[r][1];
+        a.out[th * HD + d] = acc[n][i] / l;
       } else {
-        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[i];
-        if (d == 0) {
-          a.part_ml[(th * a.nsplit + sp) * 2] = ml_s[r][0];
-          a.part_ml[(th * a.nsplit + sp) * 2 + 1] = ml_s[r][1];
-        }
+        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[n][i];
       }
+    }
+    if (a.nsplit > 1 && wave == 0 && col == 0) {
+      a.part_ml[(th * a.nsplit + sp) * 2] = m_run[i];
+      a.part_ml[(th * a.nsplit + sp) * 2 + 1] = l;
     }
   }
 }
-
-#undef FO_ATTN_LOAD_TILE
 
 // merge split partials: grid (T, H)
 __global__ void k_attn_combine(AttnArgs a, int hd) {
@@ -403,21 +444,13 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
                  float scale, int nsplit, float* part_ml, float* part_o, float* out, hipStream_t s) {
   FO_REQUIRE(T > 0 && n_items > 0 && KVH > 0 && H % KVH == 0, "fo_attention: bad shape");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
-  FO_REQUIRE(max_rows >= 1 && max_rows <= 64, "fo_attention: %d query rows per item (max 64)", max_rows);
+  FO_REQUIRE(max_rows >= 1 && max_rows <= 16, "fo_attention: %d query rows per item (max 16)", max_rows);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale};
   dim3 grid(n_items, KVH, nsplit);
-  const bool small = max_rows <= 16;
-  if (hd == 128) {
-    if (small) hipLaunchKernelGGL((k_attn_rows<128, 16>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_attn_rows<128, 64>), grid, dim3(256), 0, s, a);
-  } else if (hd == 64) {
-    if (small) hipLaunchKernelGGL((k_attn_rows<64, 16>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_attn_rows<64, 64>), grid, dim3(256), 0, s, a);
-  } else {
-    if (small) hipLaunchKernelGGL((k_attn_rows<32, 16>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_attn_rows<32, 64>), grid, dim3(256), 0, s, a);
-  }
+  if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
+  else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_attn_mfma<32>), grid, dim3(256), 0, s, a);
   int rc = fo::check_launch("fo_attention/rows");
   if (rc || nsplit == 1) return rc;
   hipLaunchKernelGGL(k_attn_combine, dim3(T, H), dim3(hd < 64 ? 64 : hd), 0, s, a, hd);

@@ -258,7 +258,7 @@ class ListenGraph:
         self.To = To = ada.out_len(self.T)
         n = B * To
         G = llm.H // llm.KVH
-        assert To * G <= 64
+        assert To * G <= 16, "listen graph: one attention work item per session"
         PS = llm.pool.PS
         self.maxb = (max_keys + PS - 1) // PS
         # metadata block: [enc 4B | ada slots B | tok_pos n | tok_slot n | tok_nvis n | block table B*maxb]

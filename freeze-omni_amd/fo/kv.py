@@ -106,7 +106,7 @@ class BatchMeta:
 
     entries: list of (KVSeq, n_new, rope_pos_start, causal).  Reserves KV for the new tokens and
     advances each sequence's length.  gqa = query heads per kv head of the stack that consumes it:
-    attention work items hold up to 64 // gqa tokens of one sequence (fo_attention).
+    attention work items hold up to 16 // gqa tokens of one sequence (fo_attention: 16 query rows).
     """
 
     def __init__(self, entries, device, gqa=1):
@@ -135,7 +135,7 @@ class BatchMeta:
         bt = np.zeros((len(entries), maxb), np.int32)
         for s, (seq, _, _, _) in enumerate(entries):
             bt[s, :len(seq.pages)] = seq.pages
-        tpi = max(1, 64 // gqa)
+        tpi = max(1, 16 // gqa)
         items = []
         t = 0
         for s, (seq, n, _, _) in enumerate(entries):

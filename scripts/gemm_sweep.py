@@ -30,6 +30,10 @@ def timeit(fn, reps=30):
 shapes = [("qwen_down_m8", 3584, 18944, 8, False), ("qwen_gu_m8", 18944, 3584, 8, True), ("qwen_qkv", 4608, 3584, 16, False), ("qwen_o", 3584, 3584, 16, False), ("qwen_down", 3584, 18944, 16, False),
           ("qwen_gu", 18944, 3584, 16, True), ("tts_qkv", 2688, 896, 8, False), ("tts_o", 896, 896, 8, False),
           ("tts_gu", 4864, 896, 8, True), ("tts_down", 896, 4864, 8, False), ("lm_head", 152064, 3584, 8, False)]
+if len(sys.argv) > 1 and sys.argv[1] == "enc":   # speech encoder / adapter: 8 users x 4 frames (2 for the adapter)
+    shapes = [("enc_qkv", 3072, 1024, 32, False), ("enc_o", 1024, 1024, 32, False), ("enc_ff1", 4096, 1024, 32, False),
+              ("enc_ff2", 1024, 4096, 32, False), ("ada_conv", 2048, 5120, 16, False), ("ada_proj", 3584, 2048, 16, False),
+              ("sub_out", 1024, 4864, 32, False)]
 dev = torch.device("cuda:0")
 lib = _lib.load()
 for name, N, K, M, sw in shapes:
