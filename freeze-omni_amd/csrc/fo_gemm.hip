@@ -36,6 +36,17 @@ struct GemmArgs {
   int ntiles;      // packed 16-column tiles in Wp
   int S;           // K split across workgroups
   int act, out_bf16, residual;
+  // fused RMSNorm, split across two GEMMs (Qwen2RMSNorm / LlamaRMSNorm between residual updates):
+  //  producer: besides Y (the residual stream) writes yg = Y * gamma_next and per-row partial sums
+  //            of Y^2 per workgroup column group (sout);
+  //  consumer: takes yg as X and scales its accumulators by rstd(row) = rsqrt(sum / K + eps) before
+  //            bias / activation -- W (x*g*rstd) = rstd * (W (x*g)), so no separate norm kernel.
+  float* sout;        // producer: [M][groups] partial sums of squares
+  const float* gnext; // producer: gamma of the next norm [N]
+  float* yg;          // producer: Y * gamma_next, row stride ldy
+  const float* rstats;  // consumer: producer's partials
+  int rgroups;          // consumer: partials per row
+  float reps;           // consumer: eps
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -58,7 +69,7 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
 }
 
 // Output element (m, n): bias, folded-BN affine, activation or SwiGLU, residual, store.
-__device__ __forceinline__ void epilogue_store(const GemmArgs& a, bool sw, int m, int n, float v, float u) {
+__device__ __forceinline__ float epilogue_store(const GemmArgs& a, bool sw, int m, int n, float v, float u) {
   if (sw) {
     v = v / (1.f + expf(-v)) * u;
   } else {
@@ -76,6 +87,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, bool sw, int m
     if (a.residual) v += y[o];
     y[o] = v;
   }
+  return v;
 }
 
 // NT packed 16-column tiles per workgroup (SW: NT/2 interleaved gate/up pairs -> NT/2 output tiles)
@@ -94,6 +106,25 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   const int m0 = mt * ROWS;
   int rbeff = (a.M - m0 + 15) >> 4;
   if (rbeff > RB) rbeff = RB;
+
+  // post-scaled RMSNorm: prefetch the producer's partial sums of this workgroup's rows now, reduce
+  // them after the main loop (their latency hides behind the weight stream)
+  constexpr int RPWV = (ROWS + NW - 1) / NW;  // rows per wave
+  // wide variants are at the VGPR edge of their occupancy step: they load the partials after the loop
+  constexpr bool RPRE = NT * U <= 8;
+  float rpart[RPWV];
+  auto load_rpart = [&]() {
+#pragma unroll
+    for (int i = 0; i < RPWV; ++i) {
+      const int rr = wave + i * NW;
+      const int m = min(m0 + rr, a.M - 1);
+      float v = 0.f;
+      if (rr < ROWS)
+        for (int j = lane; j < a.rgroups; j += 64) v += a.rstats[(size_t)m * a.rgroups + j];
+      rpart[i] = v;
+    }
+  };
+  if (RPRE && a.rstats) load_rpart();
 
   f32x4 acc[NT][RB];
 #pragma unroll
@@ -174,6 +205,21 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
     red[0][t][rr][c] = v;
   }
+  if (a.rstats) {
+    if (!RPRE) load_rpart();
+    __shared__ float rstd_s[ROWS];
+#pragma unroll
+    for (int i = 0; i < RPWV; ++i) {
+      const int rr = wave + i * NW;
+      const float ss = wave_sum(rpart[i]);
+      if (rr < ROWS && lane == 0) rstd_s[rr] = rsqrtf(ss / (float)a.K + a.reps);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NE; e += NTH) {
+      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+      red[0][t][rr][c] *= rstd_s[rr];
+    }
+  }
   __syncthreads();
   if (a.S > 1) {
     // K split across workgroups: write this split's partial slab; k_gemm_reduce (the next launch
@@ -194,19 +240,36 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     const int m = m0 + rr;
     const int n = (tg * LT + lt) * 16 + c;
     if (m >= a.M || n >= a.N) continue;
-    if (SW) epilogue_store(a, true, m, n, red[0][2 * lt][rr][c], red[0][2 * lt + 1][rr][c]);
-    else epilogue_store(a, false, m, n, red[0][lt][rr][c], 0.f);
+    float y;
+    if (SW) y = epilogue_store(a, true, m, n, red[0][2 * lt][rr][c], red[0][2 * lt + 1][rr][c]);
+    else y = epilogue_store(a, false, m, n, red[0][lt][rr][c], 0.f);
+    if (!SW) red[0][lt][rr][c] = y;
+  }
+  if (!SW && a.sout) {
+    // row partial sums of squares of this workgroup's LT*16 output columns, for the next norm
+    __syncthreads();
+    const int n0 = tg * LT * 16;
+    const int cnt = min(LT * 16, a.N - n0);
+    for (int rr = wave; rr < ROWS; rr += NW) {
+      const int m = m0 + rr;
+      if (m >= a.M) break;
+      const float v = lane < cnt ? red[0][lane >> 4][rr][lane & 15] : 0.f;
+      const float ss = wave_sum(v * v);
+      if (lane == 0) a.sout[(size_t)m * gridDim.x + tg] = ss;
+      if (a.yg && lane < cnt) a.yg[(size_t)m * a.ldy + n0 + lane] = v * a.gnext[n0 + lane];
+    }
   }
 }
 
-// Sum of the S partial slabs + epilogue for the split-K path (grid-stride over M x N outputs).
-__global__ void k_gemm_reduce(GemmArgs a, int sw, int Mrows) {
+// Sum of the S partial slabs + epilogue for the split-K path.  Grid (ceil(N/256), M): one row
+// chunk of 256 columns per block, which is also the statistics group for a fused normalisation.
+__global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mrows) {
+  __shared__ float red_s[4];
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
-  const long long total = (long long)a.M * a.N;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int m = (int)(e / a.N), n = (int)(e % a.N);
+  const int m = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  float y = 0.f;
+  if (n < a.N) {
     const int col = sw ? (n >> 4) * 32 + (n & 15) : n;
     float v = 0.f, u = 0.f;
     for (int q = 0; q < a.S; ++q) {
@@ -214,12 +277,15 @@ __global__ void k_gemm_reduce(GemmArgs a, int sw, int Mrows) {
       v += p[0];
       if (sw) u += p[16];
     }
-    epilogue_store(a, sw != 0, m, n, v, u);
+    y = epilogue_store(a, sw != 0, m, n, v, u);
+  }
+  if (a.sout && !sw) {
+    const float ss = block_sum<4>(n < a.N ? y * y : 0.f, red_s);
+    if (threadIdx.x == 0) a.sout[(size_t)m * gridDim.x + blockIdx.x] = ss;
+    if (a.yg && n < a.N) a.yg[(size_t)m * a.ldy + n] = y * a.gnext[n];
   }
 }
 
-// Same body under two symbols so profiles separate the multi-10-MB weight streams (Qwen2 MLP,
-// lm_head: >= 64 MB of bf16 per launch) from every other linear layer.
 template <int NT, int RB, bool XF32, int NW, int U, bool SW>
 __global__ __launch_bounds__(NW * 64) void k_gemm(GemmArgs a) {
   gemm_body<NT, RB, XF32, NW, U, SW>(a);
@@ -231,23 +297,24 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
 
 template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
+  const size_t shm = 0;
   if (wstream) {
-    if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
-    else hipLaunchKernelGGL((k_gemm_wstream<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
+    if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
+    else hipLaunchKernelGGL((k_gemm_wstream<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
   } else {
-    if (x_f32) hipLaunchKernelGGL((k_gemm<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
-    else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), 0, s, a);
+    if (x_f32) hipLaunchKernelGGL((k_gemm<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
+    else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
   }
 }
 
 // forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
 thread_local int g_force_nw = 0, g_force_nt = 0;
 
-template <int NT, bool SW>
-void launch_rb1_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
-  if (nw == 16) launch_gemm<NT, 1, 16, 4, SW>(wstream, x_f32, grid, a, s);
-  else if (nw == 8) launch_gemm<NT, 1, 8, 4, SW>(wstream, x_f32, grid, a, s);
-  else launch_gemm<NT, 1, 4, 4, SW>(wstream, x_f32, grid, a, s);
+template <int NT, int RB, bool SW>
+void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
+  if (nw == 16) launch_gemm<NT, RB, 16, 4, SW>(wstream, x_f32, grid, a, s);
+  else if (nw == 8) launch_gemm<NT, RB, 8, 4, SW>(wstream, x_f32, grid, a, s);
+  else launch_gemm<NT, RB, 4, 4, SW>(wstream, x_f32, grid, a, s);
 }
 
 // Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
@@ -311,10 +378,14 @@ long long fo_gemm_workspace_floats(int M, int N, int K, int swiglu) {
 
 // Y = act(X @ W^T + bias) (+Y if residual).  X bf16 [M][ldx], K % 32 == 0.
 // swiglu != 0: Wp holds interleaved (gate, up) tile pairs, Y[m][n] = silu(gate) * up, n < N.
-int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
-            const float* scale, const float* shift, void* Y, int ldy, int out_bf16, int act, int residual, float* ws,
-            long long ws_floats, int* counters, int splitk, hipStream_t stream) {
+static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu,
+                     const float* bias, const float* scale, const float* shift, void* Y, int ldy, int out_bf16,
+                     int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
+                     const float* rstats, int rgroups, float reps, float* sout, const float* gnext, float* yg,
+                     int* sgroups, hipStream_t stream) {
   FO_REQUIRE(M > 0 && N > 0 && K > 0, "fo_gemm: bad shape M=%d N=%d K=%d", M, N, K);
+  FO_REQUIRE(!rstats || rgroups > 0, "fo_gemm: row statistics without a group count");
+  FO_REQUIRE(!sout || (!swiglu && !out_bf16 && (!yg || gnext)), "fo_gemm: row statistics need fp32 non-SwiGLU output");
   FO_REQUIRE((K & 31) == 0, "fo_gemm: K=%d must be a multiple of 32", K);
   FO_REQUIRE(ldx >= K, "fo_gemm: ldx=%d < K=%d", ldx, K);
   FO_REQUIRE(ldy >= N, "fo_gemm: ldy=%d < N=%d", ldy, N);
@@ -337,6 +408,12 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
   a.act = act;
   a.out_bf16 = out_bf16;
   a.residual = residual;
+  a.sout = sout;
+  a.gnext = gnext;
+  a.yg = yg;
+  a.rstats = rstats;
+  a.rgroups = rgroups;
+  a.reps = reps;
   a.ntiles = (swiglu ? 2 : 1) * ((N + 15) / 16);
   const int RB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   const int mt = (M + RB * 16 - 1) / (RB * 16);
@@ -356,9 +433,13 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
     FO_REQUIRE(NT == 1 || NT == 2 || NT == 4, "fo_gemm: tiles per workgroup %d", NT);
     FO_REQUIRE(!swiglu || NT >= 2, "fo_gemm: swiglu needs tile pairs");
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
+  } else if (RB == 2) {
+    if (g_force_nt == 1 || g_force_nt == 2) NT = swiglu ? 2 : g_force_nt;
+    if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   }
   const int groups = a.ntiles / NT;
   int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : fo_gemm_pick_split(M, groups, K));
+  if (rstats) S = 1;  // the rstd scale is applied before the epilogue of a single-pass GEMM
   if (S > (K >> 5)) S = K >> 5;
   a.S = S;
   if (S > 1) {
@@ -366,6 +447,7 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
     FO_REQUIRE(ws && need <= ws_floats, "fo_gemm: split-K workspace too small (%lld > %lld)", need, ws_floats);
   }
   dim3 grid(groups, mt, S);
+  if (sgroups) *sgroups = S > 1 ? (N + 255) / 256 : groups;
   const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
   const long long wgs = (long long)groups * mt * S;
   if (RB == 1) {
@@ -374,16 +456,19 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
     int nw = wgs <= 160 ? 16 : (wgs <= 256 ? (NT == 1 ? 16 : 8) : ((NT == 4 || wgs >= 1024) ? 4 : 8));
     if (g_force_nw) nw = g_force_nw;
     if (swiglu) {
-      if (NT == 4) launch_rb1_nw<4, true>(nw, wstream, x_f32, grid, a, stream);
-      else launch_rb1_nw<2, true>(nw, wstream, x_f32, grid, a, stream);
+      if (NT == 4) launch_nw<4, 1, true>(nw, wstream, x_f32, grid, a, stream);
+      else launch_nw<2, 1, true>(nw, wstream, x_f32, grid, a, stream);
     } else {
-      if (NT == 4) launch_rb1_nw<4, false>(nw, wstream, x_f32, grid, a, stream);
-      else if (NT == 2) launch_rb1_nw<2, false>(nw, wstream, x_f32, grid, a, stream);
-      else launch_rb1_nw<1, false>(nw, wstream, x_f32, grid, a, stream);
+      if (NT == 4) launch_nw<4, 1, false>(nw, wstream, x_f32, grid, a, stream);
+      else if (NT == 2) launch_nw<2, 1, false>(nw, wstream, x_f32, grid, a, stream);
+      else launch_nw<1, 1, false>(nw, wstream, x_f32, grid, a, stream);
     }
   } else if (RB == 2) {
-    if (swiglu) launch_gemm<2, 2, 8, 4, true>(wstream, x_f32, grid, a, stream);
-    else launch_gemm<1, 2, 8, 4, false>(wstream, x_f32, grid, a, stream);
+    int nw = wgs <= 128 ? 16 : 8;
+    if (g_force_nw) nw = g_force_nw;
+    if (swiglu) launch_nw<2, 2, true>(nw, wstream, x_f32, grid, a, stream);
+    else if (NT == 2) launch_nw<2, 2, false>(nw, wstream, x_f32, grid, a, stream);
+    else launch_nw<1, 2, false>(nw, wstream, x_f32, grid, a, stream);
   } else {
     if (x_f32) {
       if (swiglu) launch_gemm<2, 4, 4, 2, true>(wstream, x_f32, grid, a, stream);
@@ -396,12 +481,24 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
   if (S > 1) {
     int rc = fo::check_launch("fo_gemm/split");
     if (rc) return rc;
-    const long long total = (long long)M * N;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_gemm_reduce, dim3(blocks), dim3(256), 0, stream, a, swiglu, mt * RB * 16);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, mt * RB * 16);
   }
   return fo::check_launch("fo_gemm");
+}
+
+int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
+            const float* scale, const float* shift, void* Y, int ldy, int out_bf16, int act, int residual, float* ws,
+            long long ws_floats, int* counters, int splitk, hipStream_t stream) {
+  return gemm_impl(X, x_f32, ldx, M, K, Wp, N, swiglu, bias, scale, shift, Y, ldy, out_bf16, act, residual, ws,
+                   ws_floats, counters, splitk, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int fo_gemm_rms(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
+                void* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
+                const float* rstats, int rgroups, float eps, float* sout, const float* gnext, float* yg,
+                int* sgroups, hipStream_t stream) {
+  return gemm_impl(X, x_f32, ldx, M, K, Wp, N, swiglu, bias, nullptr, nullptr, Y, ldy, 0, act, residual, ws,
+                   ws_floats, counters, splitk, rstats, rgroups, eps, sout, gnext, yg, sgroups, stream);
 }
 
 // Force (waves, tiles per workgroup) of the M <= 16 kernels on this thread (0 = automatic); sweeps.

@@ -105,8 +105,13 @@ class PackedLinear:
     scale = None
     shift = None
 
-    def __call__(self, x, out=None, act="none", residual=False, out_dtype=F32, splitk=0, M=None):
-        """x: fp32 or bf16 [M, >=Kp] (row stride x.stride(0)); returns out [M, N]."""
+    def __call__(self, x, out=None, act="none", residual=False, out_dtype=F32, splitk=0, M=None, norm=None,
+                 stats_out=None):
+        """x: fp32 or bf16 [M, >=Kp] (row stride x.stride(0)); returns out [M, N].
+        norm: (RowStats, eps): x is the producer's yg (= residual * gamma) and rows are scaled by the
+        RMSNorm rstd from the producer's statistics; stats_out: RowStats this GEMM fills (see RowStats)."""
+        if norm is not None or stats_out is not None:
+            return self._call_norm(x, out, act, residual, out_dtype, splitk, M, norm, stats_out)
         _check_dev(x)
         if x.dtype not in (BF16, F32):
             raise TypeError("PackedLinear input must be fp32 or bf16")
@@ -122,6 +127,51 @@ class PackedLinear:
                   1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
                   stream(x.device))
         return out
+
+
+    def _call_norm(self, x, out, act, residual, out_dtype, splitk, M, norm, stats_out):
+        import ctypes
+        _check_dev(x)
+        if x.stride(-1) != 1 or x.shape[-1] < self.Kp or out_dtype != F32:
+            raise ValueError("fused RMSNorm GEMM needs unit-stride X and fp32 output")
+        M = x.shape[0] if M is None else M
+        if out is None:
+            out = torch.empty(M, self.N, dtype=F32, device=x.device)
+        rt = Runtime.get(x.device)
+        rst, rg, eps = (None, 0, 0.0) if norm is None else (norm[0].buf.data_ptr(), norm[0].groups, float(norm[1]))
+        if norm is not None and rg <= 0:
+            raise RuntimeError("RowStats consumed before any GEMM produced them")
+        so = gn = yg = None
+        if stats_out is not None:
+            so, gn, yg = stats_out.buf.data_ptr(), stats_out.gamma.data_ptr(), stats_out.yg.data_ptr()
+            if stats_out.yg.stride(0) != out.stride(0):
+                raise ValueError("yg must share the output's row stride")
+        sg = ctypes.c_int(0)
+        _lib.call("fo_gemm_rms", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                  self.packed.data_ptr(), self.N, 1 if self.swiglu else 0, ptr(self.bias), out.data_ptr(),
+                  out.stride(0), ACT[act], 1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(),
+                  rt.counters.data_ptr(), splitk, rst, rg, eps, so, gn, yg, ctypes.byref(sg), stream(x.device))
+        if stats_out is not None:
+            if sg.value > stats_out.max_groups:
+                raise RuntimeError(f"RowStats holds {stats_out.max_groups} groups per row, GEMM wrote {sg.value}")
+            stats_out.groups = sg.value
+        return out
+
+
+class RowStats:
+    """RMSNorm split across two GEMMs: the producer writes per-row partial sums of squares of its
+    output (buf) and yg = output * gamma (the next norm's weight); the consumer GEMM reads yg as its
+    input and scales rows by rsqrt(sum / K + eps).  set(gamma, yg) before each producer call."""
+
+    def __init__(self, rows, device, max_groups=256):
+        self.max_groups = max_groups
+        self.buf = torch.empty(rows * max_groups, dtype=F32, device=device)
+        self.groups = 0
+        self.gamma = self.yg = None
+
+    def set(self, gamma, yg):
+        self.gamma, self.yg = gamma, yg
+        return self
 
 
 # ---------------------------------------------------------------- kernel wrappers

@@ -57,7 +57,9 @@ class DecoderStack:
               "q": torch.empty(T, H * hd, dtype=F32, device=device),
               "att": torch.empty(T, H * hd, dtype=F32, device=device),
               "m": torch.empty(T, self.layers[0].gu.N, dtype=F32, device=device),
-              "nsplit": nsplit, "part_ml": None, "part_o": None}
+              "nsplit": nsplit, "part_ml": None, "part_o": None,
+              "sA": ops.RowStats(T, device), "sB": ops.RowStats(T, device),
+              "xg": torch.empty(T, self.D, dtype=F32, device=device)}
         if nsplit > 1:
             ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
@@ -73,17 +75,24 @@ class DecoderStack:
         h, qkv, q, att, m = ws["h"][:T], ws["qkv"][:T], ws["q"][:T], ws["att"][:T], ws["m"][:T]
         nsplit, part_ml, part_o = ws["nsplit"], ws["part_ml"], ws["part_o"]
         scale = hd ** -0.5
+        sA, sB, xg = ws["sA"], ws["sB"], ws["xg"][:T]
+        last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
-            ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=(self.first_fp16 and i == 0), M=T)
-            L.qkv(h, out=qkv, M=T)
+            if i == 0:  # the stream's first rows come from a gather: no producer statistics yet
+                ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
+                L.qkv(h, out=qkv, M=T)
+            else:       # input RMSNorm fused: x*gamma and row sums came from the previous down proj
+                L.qkv(xg, out=qkv, M=T, norm=(sA, self.eps))
             ops.rope_kv_write(qkv, T, H, KVH, hd, meta.tok_pos, meta.tok_slot, self.cos, self.sin, q,
                               self.pool.k[li], self.pool.v[li], self.pool.PS)
             ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
                           self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
                           att)
-            L.o(att, out=x, residual=True, M=T)
-            ops.rmsnorm(x, L.ln2, self.eps, out=h, M=T)
-            L.gu(h, out=m, M=T)
-            L.down(m, out=x, residual=True, M=T)
+            L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))
+            L.gu(xg, out=m, M=T, norm=(sB, self.eps))
+            if i == last:
+                L.down(m, out=x, residual=True, M=T)
+            else:
+                L.down(m, out=x, residual=True, M=T, stats_out=sA.set(self.layers[i + 1].ln1, xg))
         return x

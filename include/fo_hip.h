@@ -42,6 +42,15 @@ int fo_event_destroy(void* ev);
  *   adapter conv/project (models/adapter.py:670,679), TTS Llama layers + out_fnn
  *   (models/decoder/decoder.py:299-311,346).
  * W is packed once by fo_pack_weight into MFMA fragment order. */
+/* fo_gemm with RMSNorm fused across the residual update (Qwen2RMSNorm / LlamaRMSNorm,
+ * models/audioLLM.py:479-484, models/decoder/decoder.py:142-153): a producer GEMM (sout != 0) also
+ * writes per-row partial sums of squares of Y per workgroup column group (*sgroups of them) and
+ * yg = Y * gnext (gamma of the next norm); a consumer GEMM (rstats != 0) takes yg as X and scales its
+ * result rows by rsqrt(sum / K + eps) before bias / activation / SwiGLU. */
+int fo_gemm_rms(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
+                void* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
+                const float* rstats, int rgroups, float eps, float* sout, const float* gnext, float* yg,
+                int* sgroups, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
 long long fo_pack_weight_elems(int N, int K);
@@ -96,7 +105,7 @@ int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, c
 /* GQA attention over paged KV for a ragged batch (transformers sdpa/eager attention reached from
  * models/audioLLM.py:482 and models/decoder/decoder.py:142-153,299-311); token t sees the first
  * tok_nvis[t] keys of its sequence (causal: own cache index + 1, full/unmasked: all).  items
- * [n_items][3] = (sequence, first token, token count), token count * H/KVH <= max_rows <= 64.
+ * [n_items][3] = (sequence, first token, token count), token count * H/KVH <= max_rows <= 16.
  * Split-KV (nsplit from fo_attn_nsplit) + combine. */
 int fo_attention(const float* q, int T, const int* items, int n_items, int max_rows, const int* tok_nvis,
                  const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
