@@ -406,6 +406,97 @@ __global__ __launch_bounds__(256) void k_relpos_attn(const float* q, int ldq, co
   }
 }
 
+// Fused ring append + rel-pos attention for one (user, head): the chunk's new K/V rows come straight
+// from the QKV GEMM output and are written into the user's ring (MultiHeadedAttention.infer's
+// cat-and-trim, models/encoder/attention.py:415-428) while every key/value/position row this head
+// needs is staged in LDS with 16-B coalesced loads; scores, softmax and P.V then run out of LDS.
+__global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq, float* kr, float* vr, int cap,
+                                                      const int* start, const int* len, const int* ring,
+                                                      const float* ptab, const int* pstart, const float* bu,
+                                                      const float* bv, int T, int h, int dk, float scale, float* out,
+                                                      int ldo) {
+  extern __shared__ float smem[];
+  const int KP = dk + 4;  // padded rows: lanes on consecutive keys hit distinct banks
+  float* k_s = smem;                  // [cap][KP]
+  float* v_s = k_s + cap * KP;        // [cap][KP]
+  float* p_s = v_s + cap * KP;        // [cap][KP]
+  float* qu = p_s + cap * KP;         // [T][dk]
+  float* qv = qu + T * dk;            // [T][dk]
+  float* sc = qv + T * dk;            // [T][cap]
+  const int b = blockIdx.x, hh = blockIdx.y;
+  const int d = h * dk;
+  const size_t rb = ring ? (size_t)ring[b] : (size_t)b;
+  const int Lold = len[b], Lk = Lold + T;
+  const int st = start[b];
+  const int ps = pstart[b];
+  const int D4 = dk / 4;
+  for (int e = threadIdx.x; e < Lk * D4; e += blockDim.x) {
+    const int j = e / D4, c = (e % D4) * 4;
+    const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
+    float4 kk, vv;
+    if (j < Lold) {
+      kk = *reinterpret_cast<const float4*>(kr + ro);
+      vv = *reinterpret_cast<const float4*>(vr + ro);
+    } else {
+      const float* src = qkv + ((size_t)b * T + (j - Lold)) * ldq + hh * dk + c;
+      kk = *reinterpret_cast<const float4*>(src + d);
+      vv = *reinterpret_cast<const float4*>(src + 2 * d);
+      *reinterpret_cast<float4*>(kr + ro) = kk;
+      *reinterpret_cast<float4*>(vr + ro) = vv;
+    }
+    *reinterpret_cast<float4*>(k_s + j * KP + c) = kk;
+    *reinterpret_cast<float4*>(v_s + j * KP + c) = vv;
+    *reinterpret_cast<float4*>(p_s + j * KP + c) =
+        *reinterpret_cast<const float4*>(ptab + (size_t)(ps + j) * d + hh * dk + c);
+  }
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    const int i = e / dk, c = e % dk;
+    const float x = qkv[((size_t)b * T + i) * ldq + hh * dk + c];
+    qu[i * dk + c] = x + bu[hh * dk + c];
+    qv[i * dk + c] = x + bv[hh * dk + c];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * Lk; e += blockDim.x) {
+    const int i = e / Lk, j = e % Lk;
+    const float* kk = k_s + j * KP;
+    const float* pp = p_s + j * KP;
+    const float* a1 = qu + i * dk;
+    const float* a2 = qv + i * dk;
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = 0; c < dk; c += 4) {
+      const float4 k4 = *reinterpret_cast<const float4*>(kk + c), p4 = *reinterpret_cast<const float4*>(pp + c);
+      const float4 u4 = *reinterpret_cast<const float4*>(a1 + c), w4 = *reinterpret_cast<const float4*>(a2 + c);
+      s1 += u4.x * k4.x + u4.y * k4.y + u4.z * k4.z + u4.w * k4.w;
+      s2 += w4.x * p4.x + w4.y * p4.y + w4.z * p4.z + w4.w * p4.w;
+    }
+    sc[i * cap + j] = (s1 + s2) * scale;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = wave; i < T; i += blockDim.x / 64) {
+    float m = -INFINITY;
+    for (int j = lane; j < Lk; j += 64) m = fmaxf(m, sc[i * cap + j]);
+    m = wave_max(m);
+    float sum = 0.f;
+    for (int j = lane; j < Lk; j += 64) {
+      const float e = expf(sc[i * cap + j] - m);
+      sc[i * cap + j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float r = 1.f / sum;
+    for (int j = lane; j < Lk; j += 64) sc[i * cap + j] *= r;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+    const int i = e / dk, c = e % dk;
+    const float* pr = sc + i * cap;
+    float acc = 0.f;
+    for (int j = 0; j < Lk; ++j) acc += pr[j] * v_s[j * KP + c];
+    out[((size_t)b * T + i) * ldo + hh * dk + c] = acc;
+  }
+}
+
 inline int grid_for(long long n) {
   long long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -463,6 +554,18 @@ int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int 
   hipLaunchKernelGGL(k_enc_kv_write, dim3(grid_for(n)), dim3(256), 0, s, k, v, ldkv, B, T, d, start, len, ring, cap,
                      kr, vr);
   return fo::check_launch("fo_enc_kv_write");
+}
+
+int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, int cap, const int* start,
+                              const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
+                              const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,
+                              hipStream_t s) {
+  FO_REQUIRE(T >= 1 && T <= cap && dk % 4 == 0 && (ldq % 4) == 0, "fo_relpos_attention_fused: T=%d dk=%d", T, dk);
+  const size_t lds = (size_t)(3 * cap * (dk + 4) + 2 * T * dk + T * cap) * sizeof(float);
+  FO_REQUIRE(lds <= 160 * 1024, "fo_relpos_attention_fused: ring of %d x %d exceeds LDS", cap, dk);
+  hipLaunchKernelGGL(k_relpos_fused, dim3(B, h), dim3(256), lds, s, qkv, ldq, kr, vr, cap, start, len, ring, ptab,
+                     pstart, bu, bv, T, h, dk, scale, out, ldo);
+  return fo::check_launch("fo_relpos_attention_fused");
 }
 
 int fo_relpos_attention(const float* q, int ldq, const float* kr, const float* vr, int cap, const int* start,

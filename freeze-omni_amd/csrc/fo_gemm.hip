@@ -434,6 +434,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     FO_REQUIRE(!swiglu || NT >= 2, "fo_gemm: swiglu needs tile pairs");
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   } else if (RB == 2) {
+    // speech-encoder shapes (M = 32): narrow long-K layers (FFN w_2, subsampling out) split K 4 ways
+    if (!swiglu && a.ntiles <= 64 && KS >= 96) S_auto = 4;
     if (g_force_nt == 1 || g_force_nt == 2) NT = swiglu ? 2 : g_force_nt;
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   }

@@ -67,6 +67,8 @@ _SIGS = {
     "fo_attention": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int,
                              c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp]),
     "fo_enc_kv_write": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "fo_relpos_attention_fused": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                          c_int, c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),
     "fo_relpos_attention": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                     c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),
     "fo_fbank": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,

@@ -293,6 +293,12 @@ def enc_kv_write(k, v, B, T, d, start, length, ring, cap, kr, vr):
               length.data_ptr(), ptr(ring), cap, kr.data_ptr(), vr.data_ptr(), stream(k.device))
 
 
+def relpos_attention_fused(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out):
+    _lib.call("fo_relpos_attention_fused", qkv.data_ptr(), qkv.stride(0), kr.data_ptr(), vr.data_ptr(), cap,
+              start.data_ptr(), length.data_ptr(), ptr(ring), ptab.data_ptr(), pstart.data_ptr(), bu.data_ptr(),
+              bv.data_ptr(), B, T, h, dk, float(scale), out.data_ptr(), out.stride(0), stream(qkv.device))
+
+
 def relpos_attention(q, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out):
     _lib.call("fo_relpos_attention", q.data_ptr(), q.stride(0), kr.data_ptr(), vr.data_ptr(), cap, start.data_ptr(),
               length.data_ptr(), ptr(ring), ptab.data_ptr(), pstart.data_ptr(), bu.data_ptr(), bv.data_ptr(), B, T, h,

@@ -227,10 +227,8 @@ class SpeechEncoderEngine:
         for i, L in enumerate(self.layers):
             ops.layernorm(x, *L["ln1"], out=h)
             L["qkv"](h, out=qkv)
-            ops.enc_kv_write(qkv[:, self.d:], qkv[:, 2 * self.d:], B, T, self.d, st, ln, rg, self.cap,
-                             self.kr[i], self.vr[i])
-            ops.relpos_attention(qkv, self.kr[i], self.vr[i], self.cap, st, ln, rg, self.ptab[i], ps, L["bu"],
-                                 L["bv"], B, T, self.h, self.dk, scale, att)
+            ops.relpos_attention_fused(qkv, self.kr[i], self.vr[i], self.cap, st, ln, rg, self.ptab[i], ps,
+                                       L["bu"], L["bv"], B, T, self.h, self.dk, scale, att)
             L["out"](att, out=x, residual=True)
             ops.layernorm(x, *L["ln2"], out=h)
             L["ff1"](h, out=f, act="relu")

@@ -114,6 +114,12 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
  * (models/encoder/attention.py:407-459) */
 int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,
                     const int* ring, int cap, float* kr, float* vr, hipStream_t s);
+/* enc_kv_write + relpos_attention in one launch: new K/V rows read from the QKV output (columns
+ * [d, 2d) and [2d, 3d)), appended to the ring, attention over ring + new rows staged in LDS */
+int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, int cap, const int* start,
+                              const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
+                              const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,
+                              hipStream_t s);
 int fo_relpos_attention(const float* q, int ldq, const float* kr, const float* vr, int cap, const int* start,
                         const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
                         const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,
