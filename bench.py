@@ -235,14 +235,15 @@ def gather_list(dist, vals, world, dev):
     return [float(v) for g, n in zip(gl, sizes) for v in g[:int(n)].tolist()]
 
 
-def recorded_traffic(kernel_prefix):
+def recorded_traffic(kernel_regex):
     """HBM bytes per launch of the dominant kernel from the newest committed FETCH_SIZE pass of this
     command (profiles/rNN_fetch.json, written by scripts/summarize_profile.py: KiB x 1024 x 2)."""
     import glob
+    import re
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch.json")))
     if not files:
         return None, None
-    groups = [g for g in json.load(open(files[-1]))["groups"] if kernel_prefix in g["kernel"]]
+    groups = [g for g in json.load(open(files[-1]))["groups"] if re.search(kernel_regex, g["kernel"])]
     if not groups:
         return None, os.path.relpath(files[-1], ROOT)
     g = max(groups, key=lambda g: g["dispatches"])
@@ -344,7 +345,8 @@ def main():
         lat_gated = gather_list(dist, lat_gated, world, dev)
     if rank == 0:
         peak = 8000.0
-        traffic, traffic_src = recorded_traffic("k_gemm_wstream<2, 1, true, 4>")
+        # the SwiGLU (last template flag true) M<=16 weight stream: Qwen2 gate/up of every layer
+        traffic, traffic_src = recorded_traffic(r"k_gemm_wstream<\d, 1, true, \d+, \d, true>")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
