@@ -47,6 +47,18 @@ struct GemmArgs {
   const float* rstats;  // consumer: producer's partials
   int rgroups;          // consumer: partials per row
   float reps;           // consumer: eps
+  // fused RoPE + paged-KV append (the fused q|k|v projection of a Qwen2 / Llama layer): the weight
+  // is packed so each 16-column tile pair holds columns (i, i + hd/2) of one head; the epilogue
+  // rotates q and k heads by the token's position and writes q to rq [M][rH*rhd], k and v rows to
+  // the paged cache at the token's slot ([page][kv head][PS][hd]); Y is not written.
+  const int* rpos;
+  const int* rslot;
+  const float* rcos;  // [pos][hd/2]
+  const float* rsin;
+  float* rq;
+  float* rk;
+  float* rv;
+  int rH, rKVH, rhd, rPS;
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -88,6 +100,37 @@ __device__ __forceinline__ float epilogue_store(const GemmArgs& a, bool sw, int 
     y[o] = v;
   }
   return v;
+}
+
+// Columns (n, n + hd/2) of one head, n < hd/2 within the head (transformers rotate_half RoPE, the
+// reference's Qwen2 / Llama attention reached from models/audioLLM.py:482, models/decoder/decoder.py:299-311).
+__device__ __forceinline__ void rope_store(const GemmArgs& a, int m, int n, float x1, float x2) {
+  const int hd = a.rhd, half = hd >> 1;
+  const int h = n / hd, i = n - h * hd;
+  if (a.bias) {
+    x1 += a.bias[n];
+    x2 += a.bias[n + half];
+  }
+  const int sl = a.rslot[m];
+  const int page = sl / a.rPS, off = sl - page * a.rPS;
+  if (h < a.rH + a.rKVH) {
+    const int p = a.rpos[m];
+    const float c = a.rcos[(size_t)p * half + i], sn = a.rsin[(size_t)p * half + i];
+    const float o1 = x1 * c - x2 * sn, o2 = x2 * c + x1 * sn;
+    float* d = h < a.rH ? a.rq + (size_t)m * a.rH * hd + (size_t)h * hd
+                        : a.rk + (((size_t)page * a.rKVH + (h - a.rH)) * a.rPS + off) * hd;
+    d[i] = o1;
+    d[i + half] = o2;
+  } else {
+    float* d = a.rv + (((size_t)page * a.rKVH + (h - a.rH - a.rKVH)) * a.rPS + off) * hd;
+    d[i] = x1;
+    d[i + half] = x2;
+  }
+}
+// logical first column of rope tile pair P, column c
+__device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
+  const int per = a.rhd >> 5;  // tile pairs per head
+  return (P / per) * a.rhd + (P % per) * 16 + c;
 }
 
 // NT packed 16-column tiles per workgroup (SW: NT/2 interleaved gate/up pairs -> NT/2 output tiles)
@@ -234,6 +277,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     }
     return;
   }
+  if constexpr (NT == 2 && !SW) {
+    if (a.rq) {
+      for (int e = threadIdx.x; e < ROWS * 16; e += NTH) {
+        const int rr = e >> 4, c = e & 15, m = m0 + rr;
+        if (m < a.M) rope_store(a, m, rope_col(a, tg, c), red[0][0][rr][c], red[0][1][rr][c]);
+      }
+      return;
+    }
+  }
   constexpr int LT = SW ? NT / 2 : NT;  // logical output tiles
   for (int e = threadIdx.x; e < LT * ROWS * 16; e += NTH) {
     const int lt = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
@@ -268,6 +320,19 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
   const int m = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  if (a.rq) {  // rope: one thread per column pair, packed tiles (2P, 2P + 1)
+    if (n < a.N / 2) {
+      const int P = n >> 4, c = n & 15;
+      float x1 = 0.f, x2 = 0.f;
+      for (int q = 0; q < a.S; ++q) {
+        const float* p = a.ws + q * slab + (size_t)m * Ncols + P * 32 + c;
+        x1 += p[0];
+        x2 += p[16];
+      }
+      rope_store(a, m, rope_col(a, P, c), x1, x2);
+    }
+    return;
+  }
   float y = 0.f;
   if (n < a.N) {
     const int col = sw ? (n >> 4) * 32 + (n & 15) : n;
@@ -382,7 +447,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
                      const float* bias, const float* scale, const float* shift, void* Y, int ldy, int out_bf16,
                      int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
                      const float* rstats, int rgroups, float reps, float* sout, const float* gnext, float* yg,
-                     int* sgroups, hipStream_t stream) {
+                     int* sgroups, const GemmArgs* rope, hipStream_t stream) {
   FO_REQUIRE(M > 0 && N > 0 && K > 0, "fo_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   FO_REQUIRE(!rstats || rgroups > 0, "fo_gemm: row statistics without a group count");
   FO_REQUIRE(!sout || (!swiglu && !out_bf16 && (!yg || gnext)), "fo_gemm: row statistics need fp32 non-SwiGLU output");
@@ -415,6 +480,26 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.rgroups = rgroups;
   a.reps = reps;
   a.ntiles = (swiglu ? 2 : 1) * ((N + 15) / 16);
+  a.rpos = a.rslot = nullptr;
+  a.rcos = a.rsin = nullptr;
+  a.rq = a.rk = a.rv = nullptr;
+  a.rH = a.rKVH = a.rhd = a.rPS = 0;
+  if (rope) {
+    FO_REQUIRE(!swiglu && !sout && !residual && !out_bf16 && act == 0 && !scale, "fo_gemm_qkv_rope: plain epilogue only");
+    FO_REQUIRE(rope->rhd % 32 == 0 && N == (rope->rH + 2 * rope->rKVH) * rope->rhd,
+               "fo_gemm_qkv_rope: N=%d != (H + 2 KVH) * hd with hd %% 32 == 0", N);
+    a.rpos = rope->rpos;
+    a.rslot = rope->rslot;
+    a.rcos = rope->rcos;
+    a.rsin = rope->rsin;
+    a.rq = rope->rq;
+    a.rk = rope->rk;
+    a.rv = rope->rv;
+    a.rH = rope->rH;
+    a.rKVH = rope->rKVH;
+    a.rhd = rope->rhd;
+    a.rPS = rope->rPS;
+  }
   const int RB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   const int mt = (M + RB * 16 - 1) / (RB * 16);
   // tiles per workgroup: the activation rows are re-read by every workgroup, so workgroups that
@@ -439,6 +524,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (g_force_nt == 1 || g_force_nt == 2) NT = swiglu ? 2 : g_force_nt;
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   }
+  if (rope) NT = 2;  // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds
   const int groups = a.ntiles / NT;
   int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : fo_gemm_pick_split(M, groups, K));
   if (rstats) S = 1;  // the rstd scale is applied before the epilogue of a single-pass GEMM
@@ -474,9 +560,11 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   } else {
     if (x_f32) {
       if (swiglu) launch_gemm<2, 4, 4, 2, true>(wstream, x_f32, grid, a, stream);
+      else if (NT == 2) launch_gemm<2, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
       else launch_gemm<1, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
     } else {
       if (swiglu) launch_gemm<2, 4, 4, 4, true>(wstream, x_f32, grid, a, stream);
+      else if (NT == 2) launch_gemm<2, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
       else launch_gemm<1, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
     }
   }
@@ -492,7 +580,7 @@ int fo_gemm(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int
             const float* scale, const float* shift, void* Y, int ldy, int out_bf16, int act, int residual, float* ws,
             long long ws_floats, int* counters, int splitk, hipStream_t stream) {
   return gemm_impl(X, x_f32, ldx, M, K, Wp, N, swiglu, bias, scale, shift, Y, ldy, out_bf16, act, residual, ws,
-                   ws_floats, counters, splitk, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, stream);
+                   ws_floats, counters, splitk, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 int fo_gemm_rms(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, int swiglu, const float* bias,
@@ -500,7 +588,29 @@ int fo_gemm_rms(const void* X, int x_f32, int ldx, int M, int K, const void* Wp,
                 const float* rstats, int rgroups, float eps, float* sout, const float* gnext, float* yg,
                 int* sgroups, hipStream_t stream) {
   return gemm_impl(X, x_f32, ldx, M, K, Wp, N, swiglu, bias, nullptr, nullptr, Y, ldy, 0, act, residual, ws,
-                   ws_floats, counters, splitk, rstats, rgroups, eps, sout, gnext, yg, sgroups, stream);
+                   ws_floats, counters, splitk, rstats, rgroups, eps, sout, gnext, yg, sgroups, nullptr, stream);
+}
+
+int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,
+                     float* ws, long long ws_floats, int* counters, int splitk, const float* rstats, int rgroups,
+                     float eps, const int* pos, const int* slot, const float* cos_t, const float* sin_t, float* q_out,
+                     float* kc, float* vc, int H, int KVH, int hd, int PS, hipStream_t stream) {
+  FO_REQUIRE(pos && slot && cos_t && sin_t && q_out && kc && vc && PS > 0 && H > 0 && KVH > 0,
+             "fo_gemm_qkv_rope: missing rope/cache arguments");
+  GemmArgs r;
+  r.rpos = pos;
+  r.rslot = slot;
+  r.rcos = cos_t;
+  r.rsin = sin_t;
+  r.rq = q_out;
+  r.rk = kc;
+  r.rv = vc;
+  r.rH = H;
+  r.rKVH = KVH;
+  r.rhd = hd;
+  r.rPS = PS;
+  return gemm_impl(X, x_f32, ldx, M, K, Wp, N, 0, bias, nullptr, nullptr, q_out, N, 0, 0, 0, ws, ws_floats, counters,
+                   splitk, rstats, rgroups, eps, nullptr, nullptr, nullptr, nullptr, &r, stream);
 }
 
 // Force (waves, tiles per workgroup) of the M <= 16 kernels on this thread (0 = automatic); sweeps.

@@ -49,6 +49,9 @@ _SIGS = {
     "fo_gemm_rms": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int,
                             c_vp, c_ll, c_vp, c_int, c_vp, c_int, c_float, c_vp, c_vp, c_vp, ctypes.POINTER(c_int),
                             c_vp]),
+    "fo_gemm_qkv_rope": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_ll, c_vp, c_int, c_vp,
+                                 c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                 c_vp]),
     "fo_fill_hash": (c_int, [c_vp, c_int, c_ll, ctypes.c_ulonglong, c_float, c_float, c_vp]),
     "fo_rmsnorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
     "fo_layernorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_vp]),

@@ -70,7 +70,9 @@ class PackedLinear:
     computes silu(x W^T) * (x U^T).
     """
 
-    def __init__(self, w, bias=None, swiglu_up=None):
+    def __init__(self, w, bias=None, swiglu_up=None, rope_hd=None):
+        """rope_hd: w is a fused q|k|v projection with this head dim; tiles are packed in (i, i + hd/2)
+        pairs per head for the fused RoPE + KV-append epilogue (qkv_rope)."""
         _check_dev(w)
         w = w.contiguous()
         self.N, self.K = w.shape
@@ -84,7 +86,18 @@ class PackedLinear:
         src_bf16 = 1 if w.dtype == BF16 else 0
         if w.dtype not in (BF16, F32):
             w = w.float()
-        if self.swiglu:
+        self.rope_hd = rope_hd
+        if rope_hd is not None:
+            half = rope_hd // 2
+            if rope_hd % 32 or self.N % rope_hd:
+                raise ValueError(f"rope packing needs hd % 32 == 0 and N % hd == 0 (N={self.N}, hd={rope_hd})")
+            es = w.element_size()
+            for h in range(self.N // rope_hd):
+                for p in (0, 1):
+                    r0 = h * rope_hd + p * half
+                    _lib.call("fo_pack_weight", w.data_ptr() + r0 * self.K * es, src_bf16, half, self.K, self.K,
+                              self.packed.data_ptr(), h * (rope_hd // 16) + p, 2, s)
+        elif self.swiglu:
             u = swiglu_up.contiguous().to(w.dtype)
             _lib.call("fo_pack_weight", w.data_ptr(), src_bf16, self.N, self.K, self.K, self.packed.data_ptr(), 0, 2, s)
             _lib.call("fo_pack_weight", u.data_ptr(), src_bf16, self.N, self.K, self.K, self.packed.data_ptr(), 1, 2, s)
@@ -128,6 +141,25 @@ class PackedLinear:
                   stream(x.device))
         return out
 
+
+    def qkv_rope(self, x, M, pos, slot, cos_t, sin_t, q_out, kc, vc, H, KVH, PS, norm=None, splitk=0):
+        """Fused q|k|v projection + bias + RoPE + paged-KV append (weight packed with rope_hd):
+        q_out [M, H*hd] gets the rotated queries, kc/vc (one layer's pages) the token's K/V rows at slot[m]."""
+        _check_dev(x)
+        if self.rope_hd is None:
+            raise RuntimeError("qkv_rope needs a weight packed with rope_hd")
+        if x.stride(-1) != 1 or x.shape[-1] < self.Kp or x.dtype not in (F32, BF16):
+            raise ValueError("qkv_rope input needs unit stride, fp32/bf16 and >= Kp columns")
+        rt = Runtime.get(x.device)
+        rst, rg, eps = (None, 0, 0.0) if norm is None else (norm[0].buf.data_ptr(), norm[0].groups, float(norm[1]))
+        if norm is not None and rg <= 0:
+            raise RuntimeError("RowStats consumed before any GEMM produced them")
+        _lib.call("fo_gemm_qkv_rope", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                  self.packed.data_ptr(), self.N, ptr(self.bias), rt.ws.data_ptr(), rt.ws.numel(),
+                  rt.counters.data_ptr(), splitk, rst, rg, eps, pos.data_ptr(), slot.data_ptr(), cos_t.data_ptr(),
+                  sin_t.data_ptr(), q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(), H, KVH, self.rope_hd, PS,
+                  stream(x.device))
+        return q_out
 
     def _call_norm(self, x, out, act, residual, out_dtype, splitk, M, norm, stats_out):
         import ctypes

@@ -3,7 +3,7 @@ the AR speech decoder (pre_nn / layers_prefix / layers).
 
 Per layer (transformers Qwen2DecoderLayer / LlamaDecoderLayer, the call sites are
 models/audioLLM.py:479-484 and models/decoder/decoder.py:127-188,294-312):
-  rmsnorm -> fused QKV GEMM (+bias) -> RoPE + paged-KV append -> split-KV attention ->
+  rmsnorm -> fused QKV GEMM (+bias, RoPE and the paged-KV append in its epilogue) -> split-KV attention ->
   O GEMM (+residual, in place) -> rmsnorm -> fused gate/up GEMM with SiLU*up epilogue ->
   down GEMM (+residual, in place).
 The residual stream is fp32; GEMMs read it as fp32 (bf16 hi/lo split) against bf16 weights.
@@ -37,7 +37,7 @@ class DecoderStack:
             if bias:
                 b = torch.cat([src.get(q + "self_attn.q_proj.bias"), src.get(q + "self_attn.k_proj.bias"),
                                src.get(q + "self_attn.v_proj.bias")])
-            L.qkv = PackedLinear(torch.cat([wq, wk, wv]), b)
+            L.qkv = PackedLinear(torch.cat([wq, wk, wv]), b, rope_hd=self.hd)
             del wq, wk, wv
             L.o = PackedLinear(src.get(q + "self_attn.o_proj.weight", torch.bfloat16))
             L.gu = PackedLinear(src.get(q + "mlp.gate_proj.weight", torch.bfloat16),
@@ -53,7 +53,6 @@ class DecoderStack:
         """Preallocated per-forward buffers for T tokens (graph capture must not allocate)."""
         H, KVH, hd = self.H, self.KVH, self.hd
         ws = {"h": torch.empty(T, self.D, dtype=F32, device=device),
-              "qkv": torch.empty(T, (H + 2 * KVH) * hd, dtype=F32, device=device),
               "q": torch.empty(T, H * hd, dtype=F32, device=device),
               "att": torch.empty(T, H * hd, dtype=F32, device=device),
               "m": torch.empty(T, self.layers[0].gu.N, dtype=F32, device=device),
@@ -72,20 +71,20 @@ class DecoderStack:
         H, KVH, hd = self.H, self.KVH, self.hd
         if ws is None:
             ws = self.workspace(T, ops.attn_nsplit(meta.max_keys, meta.n_items, KVH), x.device)
-        h, qkv, q, att, m = ws["h"][:T], ws["qkv"][:T], ws["q"][:T], ws["att"][:T], ws["m"][:T]
+        h, q, att, m = ws["h"][:T], ws["q"][:T], ws["att"][:T], ws["m"][:T]
         nsplit, part_ml, part_o = ws["nsplit"], ws["part_ml"], ws["part_o"]
         scale = hd ** -0.5
         sA, sB, xg = ws["sA"], ws["sB"], ws["xg"][:T]
         last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
+            rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
+                    self.pool.PS)
             if i == 0:  # the stream's first rows come from a gather: no producer statistics yet
                 ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
-                L.qkv(h, out=qkv, M=T)
+                L.qkv.qkv_rope(h, T, *rope)
             else:       # input RMSNorm fused: x*gamma and row sums came from the previous down proj
-                L.qkv(xg, out=qkv, M=T, norm=(sA, self.eps))
-            ops.rope_kv_write(qkv, T, H, KVH, hd, meta.tok_pos, meta.tok_slot, self.cos, self.sin, q,
-                              self.pool.k[li], self.pool.v[li], self.pool.PS)
+                L.qkv.qkv_rope(xg, T, *rope, norm=(sA, self.eps))
             ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
                           self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
                           att)

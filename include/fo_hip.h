@@ -51,6 +51,16 @@ int fo_gemm_rms(const void* X, int x_f32, int ldx, int M, int K, const void* Wp,
                 void* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
                 const float* rstats, int rgroups, float eps, float* sout, const float* gnext, float* yg,
                 int* sgroups, hipStream_t stream);
+/* The fused q|k|v projection of a Qwen2 / Llama attention layer with bias, rotate_half RoPE and the
+ * paged-KV append in the epilogue (replaces the projection + apply_rotary_pos_emb + DynamicCache.update
+ * of models/audioLLM.py:482 / models/decoder/decoder.py:299-311 through transformers' Qwen2Attention /
+ * LlamaAttention).  Wp packed with (i, i + hd/2) tile pairs per head; N = (H + 2 KVH) * hd.  Rows m:
+ * q_out[m] = RoPE(q, pos[m]); K/V rows of kc/vc ([page][KVH][PS][hd]) at slot[m] = RoPE(k), v.
+ * rstats/rgroups/eps: optional fused RMSNorm consumer (as fo_gemm_rms). */
+int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,
+                     float* ws, long long ws_floats, int* counters, int splitk, const float* rstats, int rgroups,
+                     float eps, const int* pos, const int* slot, const float* cos_t, const float* sin_t, float* q_out,
+                     float* kc, float* vc, int H, int KVH, int hd, int PS, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
 long long fo_pack_weight_elems(int N, int K);

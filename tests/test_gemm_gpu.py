@@ -94,3 +94,43 @@ def test_gemm_deterministic_splitk(dev):
         assert torch.equal(y, ys[0])
     y1 = lin(x, splitk=1).cpu()
     torch.testing.assert_close(y1, ys[0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,H,KVH,hd,K,splitk", [(1, 28, 4, 128, 3584, 0), (16, 28, 4, 128, 3584, 0),
+                                                 (16, 28, 4, 128, 3584, 3), (40, 4, 2, 32, 128, 0),
+                                                 (70, 14, 14, 64, 896, 0), (8, 14, 14, 64, 896, 2),
+                                                 (24, 4, 4, 32, 128, 0)])
+def test_gemm_qkv_rope(dev, M, H, KVH, hd, K, splitk):
+    """Fused q|k|v projection + bias + rotate_half RoPE + paged-KV append vs an fp32 torch reference."""
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M * 7 + H + hd)
+    N = (H + 2 * KVH) * hd
+    PS, n_pages, half = 16, 24, hd // 2
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    x = torch.randn(M, K, generator=g)
+    pos = torch.randint(0, 300, (M,), generator=g, dtype=torch.int32)
+    slot = torch.randperm(n_pages * PS, generator=g)[:M].to(torch.int32)
+    inv = 1.0 / (1e6 ** (torch.arange(0, half, dtype=torch.float64) / half))
+    ang = torch.arange(512, dtype=torch.float64)[:, None] * inv[None]
+    cos, sin = torch.cos(ang).float(), torch.sin(ang).float()
+    lin = PackedLinear(w.to(dev), b.to(dev), rope_hd=hd)
+    q = torch.full((M, H * hd), float("nan"), device=dev)
+    kc = torch.zeros(n_pages, KVH, PS, hd, device=dev)
+    vc = torch.zeros(n_pages, KVH, PS, hd, device=dev)
+    lin.qkv_rope(x.to(dev), M, pos.to(dev), slot.to(dev), cos.to(dev), sin.to(dev), q, kc, vc, H, KVH, PS,
+                 splitk=splitk)
+    y = x.double() @ w.double().t() + b.double()
+    heads = y.view(M, H + 2 * KVH, hd)
+    c, s = cos.double()[pos.long()][:, None, :], sin.double()[pos.long()][:, None, :]
+    x1, x2 = heads[..., :half], heads[..., half:]
+    rot = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+    torch.testing.assert_close(q.cpu().double(), rot[:, :H].reshape(M, -1), rtol=2e-5, atol=2e-5)
+    kref = torch.zeros(n_pages, KVH, PS, hd, dtype=torch.float64)
+    vref = torch.zeros_like(kref)
+    for m in range(M):
+        pg, off = int(slot[m]) // PS, int(slot[m]) % PS
+        kref[pg, :, off] = rot[m, H:H + KVH]
+        vref[pg, :, off] = heads[m, H + KVH:]
+    torch.testing.assert_close(kc.cpu().double(), kref, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(vc.cpu().double(), vref, rtol=2e-5, atol=2e-5)
