@@ -23,7 +23,7 @@ from .params import all_shapes
 from .speech import AdapterEngine, FbankGPU, SpeechEncoderEngine
 from .tokenizer import load_tokenizer
 from .tts import TTSEngine
-from .weights import CheckpointSource, SynthSource
+from .weights import SynthSource
 
 
 def load_model_dir(model_path, llm_path=None):
@@ -48,11 +48,15 @@ def load_model_dir(model_path, llm_path=None):
     return cfg, synth, llm_path
 
 
-def make_source(cfg, synth, device):
+def make_source(cfg, synth, device, model_path=None, llm_path=None):
+    """synthetic.json in the model dir -> counter-hash weights generated on the device; otherwise the
+    reference's checkpoint files (fo.checkpoint: audiollm/final.pt, the Qwen2 safetensors,
+    decoder/final.pt, codec/final.pt)."""
     if synth is not None:
         return SynthSource(synth["seed"], all_shapes(cfg), device, {k: tuple(v) for k, v in
                                                                    synth.get("overrides", {}).items()})
-    raise RuntimeError("real checkpoints: use fo.checkpoint.load_reference_checkpoints (see DESIGN.md §next)")
+    from .checkpoint import load_reference_checkpoints
+    return load_reference_checkpoints(cfg, model_path, llm_path, device)
 
 
 class FreezeOmniEngine:
@@ -63,7 +67,7 @@ class FreezeOmniEngine:
         self.device = torch.device(device)
         torch.cuda.set_device(self.device)
         self.cfg, self.synth, self.llm_path = load_model_dir(model_path, llm_path)
-        src = source or make_source(self.cfg, self.synth, self.device)
+        src = source or make_source(self.cfg, self.synth, self.device, model_path, self.llm_path)
         self.src = src
         ty = self.cfg["train_yaml"]
         self.enc = {i: SpeechEncoderEngine(src, self.cfg, i, self.device, max_sessions) for i in ("user", "system")}
