@@ -59,6 +59,15 @@ struct GemmArgs {
   float* rk;
   float* rv;
   int rH, rKVH, rhd, rPS;
+  // LayerNorm on load (the pre-norm of a speech-encoder block, models/encoder/transformer.py:103-130):
+  // X rows are normalised ((x - mean) * rstd * lnw + lnb) as they are loaded, before the bf16 hi/lo
+  // split; mean and variance come from the producer GEMM's per-row partial sums of Y and Y^2
+  // (rstats1 / rstats), so the LayerNorm launch disappears.
+  const float* lnw;
+  const float* lnb;
+  float lneps;
+  float* sout1;          // producer: [M][groups] partial sums of Y (with sout: LayerNorm statistics)
+  const float* rstats1;  // LayerNorm consumer: the producer's partial sums (rstats: sums of squares)
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -134,9 +143,10 @@ __device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
 }
 
 // NT packed 16-column tiles per workgroup (SW: NT/2 interleaved gate/up pairs -> NT/2 output tiles)
-template <int NT, int RB, bool XF32, int NW, int U, bool SW>
+template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
+  static_assert(!LN || XF32, "LayerNorm on load needs fp32 X");
   // NW waves split K inside the workgroup; each keeps U k-steps of weights in flight
   constexpr int NTH = NW * 64;
   constexpr int ROWS = RB * 16;
@@ -167,7 +177,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       rpart[i] = v;
     }
   };
-  if (RPRE && a.rstats) load_rpart();
+  if (RPRE && a.rstats && !LN) load_rpart();
 
   f32x4 acc[NT][RB];
 #pragma unroll
@@ -186,6 +196,53 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     if (row > a.M - 1) row = a.M - 1;  // clamp: rows >= M are computed but never stored
     xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
+  float ln_mu[RB], ln_rs[RB];
+  if constexpr (LN) {
+    // per-row mean / rstd of this workgroup's rows from the producer's partial sums
+    __shared__ float ln_s[2][ROWS];
+    for (int rr = wave; rr < ROWS; rr += NW) {
+      const int m = min(m0 + rr, a.M - 1);
+      float s1 = 0.f, s2 = 0.f;
+      for (int j = lane; j < a.rgroups; j += 64) {
+        s1 += a.rstats1[(size_t)m * a.rgroups + j];
+        s2 += a.rstats[(size_t)m * a.rgroups + j];
+      }
+      const float mean = wave_sum(s1) / (float)a.K;
+      const float var = fmaxf(wave_sum(s2) / (float)a.K - mean * mean, 0.f);
+      if (lane == 0) {
+        ln_s[0][rr] = mean;
+        ln_s[1][rr] = 1.0f / sqrtf(var + a.lneps);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      ln_mu[r] = ln_s[0][r * 16 + (lane & 15)];
+      ln_rs[r] = ln_s[1][r * 16 + (lane & 15)];
+    }
+  }
+  // X fragment of row block r at k-step ks (LayerNorm applied on load when LN)
+  auto ldx = [&](int r, int ks, bf16x8& hi, bf16x8& lo) {
+    if constexpr (LN) {
+      const float* p = reinterpret_cast<const float*>(xr[r] + (size_t)ks * 32);
+      const int k0 = ks * 32 + 8 * (lane >> 4);
+      const float4 a0 = reinterpret_cast<const float4*>(p)[0], a1 = reinterpret_cast<const float4*>(p)[1];
+      const float4 w0 = *reinterpret_cast<const float4*>(a.lnw + k0), w1 = *reinterpret_cast<const float4*>(a.lnw + k0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(a.lnb + k0), b1 = *reinterpret_cast<const float4*>(a.lnb + k0 + 4);
+      const float f[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (f[j] - ln_mu[r]) * ln_rs[r] * w[j] + b[j];
+        const __bf16 h = (__bf16)v;
+        hi[j] = h;
+        lo[j] = (__bf16)(v - (float)h);
+      }
+    } else {
+      load_x<XT, XF32>(xr[r] + (size_t)ks * 32, hi, lo);
+    }
+  };
 
   // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
   // together); the < U leftover steps go one per wave, so no wave runs a serial tail.
@@ -203,7 +260,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < RB; ++r)
-        if (r < rbeff) load_x<XT, XF32>(xr[r] + (size_t)(ks + u) * 32, ah[u][r], al[u][r]);
+        if (r < rbeff) ldx(r, ks + u, ah[u][r], al[u][r]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -224,7 +281,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       for (int r = 0; r < RB; ++r)
         if (r < rbeff) {
           bf16x8 h, l;
-          load_x<XT, XF32>(xr[r] + (size_t)ks * 32, h, l);
+          ldx(r, ks, h, l);
           acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, b, acc[t][r], 0, 0, 0);
           if constexpr (XF32) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(l, b, acc[t][r], 0, 0, 0);
         }
@@ -248,7 +305,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
     red[0][t][rr][c] = v;
   }
-  if (a.rstats) {
+  if (a.rstats && !LN) {
     if (!RPRE) load_rpart();
     __shared__ float rstd_s[ROWS];
 #pragma unroll
@@ -308,6 +365,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       const float v = lane < cnt ? red[0][lane >> 4][rr][lane & 15] : 0.f;
       const float ss = wave_sum(v * v);
       if (lane == 0) a.sout[(size_t)m * gridDim.x + tg] = ss;
+      if (a.sout1) {
+        const float s1 = wave_sum(v);
+        if (lane == 0) a.sout1[(size_t)m * gridDim.x + tg] = s1;
+      }
       if (a.yg && lane < cnt) a.yg[(size_t)m * a.ldy + n0 + lane] = v * a.gnext[n0 + lane];
     }
   }
@@ -347,6 +408,10 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
   if (a.sout && !sw) {
     const float ss = block_sum<4>(n < a.N ? y * y : 0.f, red_s);
     if (threadIdx.x == 0) a.sout[(size_t)m * gridDim.x + blockIdx.x] = ss;
+    if (a.sout1) {
+      const float s1 = block_sum<4>(n < a.N ? y : 0.f, red_s);
+      if (threadIdx.x == 0) a.sout1[(size_t)m * gridDim.x + blockIdx.x] = s1;
+    }
     if (a.yg && n < a.N) a.yg[(size_t)m * a.ldy + n] = y * a.gnext[n];
   }
 }
@@ -358,6 +423,10 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(GemmArgs a) {
 template <int NT, int RB, bool XF32, int NW, int U, bool SW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
   gemm_body<NT, RB, XF32, NW, U, SW>(a);
+}
+template <int NT, int RB, int NW>
+__global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
+  gemm_body<NT, RB, true, NW, 4, false, true>(a);
 }
 
 template <int NT, int RB, int NW, int U, bool SW>
@@ -447,7 +516,9 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
                      const float* bias, const float* scale, const float* shift, void* Y, int ldy, int out_bf16,
                      int act, int residual, float* ws, long long ws_floats, int* counters, int splitk,
                      const float* rstats, int rgroups, float reps, float* sout, const float* gnext, float* yg,
-                     int* sgroups, const GemmArgs* rope, hipStream_t stream) {
+                     int* sgroups, const GemmArgs* rope, hipStream_t stream, const float* lnw = nullptr,
+                     const float* lnb = nullptr, float lneps = 0.f, float* sout1 = nullptr,
+                     const float* rstats1 = nullptr) {
   FO_REQUIRE(M > 0 && N > 0 && K > 0, "fo_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   FO_REQUIRE(!rstats || rgroups > 0, "fo_gemm: row statistics without a group count");
   FO_REQUIRE(!sout || (!swiglu && !out_bf16 && (!yg || gnext)), "fo_gemm: row statistics need fp32 non-SwiGLU output");
@@ -484,6 +555,16 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.rcos = a.rsin = nullptr;
   a.rq = a.rk = a.rv = nullptr;
   a.rH = a.rKVH = a.rhd = a.rPS = 0;
+  a.lnw = lnw;
+  a.lnb = lnb;
+  a.lneps = lneps;
+  a.sout1 = sout1;
+  a.rstats1 = rstats1;
+  FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
+  if (lnw) {
+    FO_REQUIRE(lnb && x_f32 && M <= 32 && !swiglu && rstats && rstats1 && rgroups > 0 && !rope && ldx % 4 == 0,
+               "fo_gemm_ln: fp32 X, M <= 32, producer statistics, plain epilogue only (M=%d K=%d)", M, K);
+  }
   if (rope) {
     FO_REQUIRE(!swiglu && !sout && !residual && !out_bf16 && act == 0 && !scale, "fo_gemm_qkv_rope: plain epilogue only");
     FO_REQUIRE(rope->rhd % 32 == 0 && N == (rope->rH + 2 * rope->rKVH) * rope->rhd,
@@ -524,10 +605,19 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (g_force_nt == 1 || g_force_nt == 2) NT = swiglu ? 2 : g_force_nt;
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   }
+  if (RB == 4 && !swiglu && mt >= 4 && a.ntiles % 4 == 0 && a.ntiles >= 64) {
+    // many row tiles (im2col convolutions, long prefills): X traffic (fp32, re-read by every column
+    // group) dominates the weights', so 4 column tiles share each X read; long K is split over
+    // workgroups until the grid covers the chip
+    NT = 4;
+    const int wg = a.ntiles / 4 * mt;
+    if (wg < 256 && KS >= 128) S_auto = KS >= 256 ? 4 : 2;
+  }
   if (rope) NT = 2;  // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds
+  if (lnw && NT > 2) NT = 2;
   const int groups = a.ntiles / NT;
   int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : fo_gemm_pick_split(M, groups, K));
-  if (rstats) S = 1;  // the rstd scale is applied before the epilogue of a single-pass GEMM
+  if (rstats && !lnw) S = 1;  // the rstd scale is applied before the epilogue of a single-pass GEMM
   if (S > (K >> 5)) S = K >> 5;
   a.S = S;
   if (S > 1) {
@@ -538,7 +628,19 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   if (sgroups) *sgroups = S > 1 ? (N + 255) / 256 : groups;
   const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
   const long long wgs = (long long)groups * mt * S;
-  if (RB == 1) {
+  if (lnw) {
+    const int nw = wgs <= 128 ? 16 : 8;
+    dim3 blk(nw * 64);
+#define FO_LN(NT_, RB_, NW_) hipLaunchKernelGGL((k_gemm_ln<NT_, RB_, NW_>), grid, blk, 0, stream, a)
+    if (RB == 1) {
+      if (NT == 2) { if (nw == 16) FO_LN(2, 1, 16); else FO_LN(2, 1, 8); }
+      else { if (nw == 16) FO_LN(1, 1, 16); else FO_LN(1, 1, 8); }
+    } else {
+      if (NT == 2) { if (nw == 16) FO_LN(2, 2, 16); else FO_LN(2, 2, 8); }
+      else { if (nw == 16) FO_LN(1, 2, 16); else FO_LN(1, 2, 8); }
+    }
+#undef FO_LN
+  } else if (RB == 1) {
     // measured (scripts/gemm_sweep.py, MI355X): one workgroup per CU wants 16 waves, a couple per
     // CU 8, many 4; 4 k-steps in flight per wave is the sweet spot everywhere on the hot path
     int nw = wgs <= 160 ? 16 : (wgs <= 256 ? (NT == 1 ? 16 : 8) : ((NT == 4 || wgs >= 1024) ? 4 : 8));
@@ -560,10 +662,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   } else {
     if (x_f32) {
       if (swiglu) launch_gemm<2, 4, 4, 2, true>(wstream, x_f32, grid, a, stream);
+      else if (NT == 4) launch_gemm<4, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
       else if (NT == 2) launch_gemm<2, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
       else launch_gemm<1, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
     } else {
       if (swiglu) launch_gemm<2, 4, 4, 4, true>(wstream, x_f32, grid, a, stream);
+      else if (NT == 4) launch_gemm<4, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
       else if (NT == 2) launch_gemm<2, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
       else launch_gemm<1, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
     }
@@ -589,6 +693,24 @@ int fo_gemm_rms(const void* X, int x_f32, int ldx, int M, int K, const void* Wp,
                 int* sgroups, hipStream_t stream) {
   return gemm_impl(X, x_f32, ldx, M, K, Wp, N, swiglu, bias, nullptr, nullptr, Y, ldy, 0, act, residual, ws,
                    ws_floats, counters, splitk, rstats, rgroups, eps, sout, gnext, yg, sgroups, nullptr, stream);
+}
+
+int fo_gemm_ln(const float* X, int ldx, int M, int K, const void* Wp, int N, const float* bias, const float* lnw,
+               const float* lnb, float eps, const float* rsum, const float* rsumsq, int rgroups, float* Y, int ldy,
+               int act, float* ws, long long ws_floats, int splitk, hipStream_t stream) {
+  FO_REQUIRE(lnw && lnb && rsum && rsumsq, "fo_gemm_ln: LayerNorm weight, bias and row statistics required");
+  return gemm_impl(X, 1, ldx, M, K, Wp, N, 0, bias, nullptr, nullptr, Y, ldy, 0, act, 0, ws, ws_floats, nullptr,
+                   splitk, rsumsq, rgroups, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, stream, lnw, lnb, eps,
+                   nullptr, rsum);
+}
+
+int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,
+                     float* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int splitk,
+                     float* rsum, float* rsumsq, int* sgroups, hipStream_t stream) {
+  FO_REQUIRE(rsum && rsumsq, "fo_gemm_rowstats: statistics buffers required");
+  return gemm_impl(X, x_f32, ldx, M, K, Wp, N, 0, bias, nullptr, nullptr, Y, ldy, 0, act, residual, ws, ws_floats,
+                   nullptr, splitk, nullptr, 0, 0.f, rsumsq, nullptr, nullptr, sgroups, nullptr, stream, nullptr,
+                   nullptr, 0.f, rsum, nullptr);
 }
 
 int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,

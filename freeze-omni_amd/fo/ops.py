@@ -142,6 +142,42 @@ class PackedLinear:
         return out
 
 
+    def ln(self, x, lnw, lnb, stats, eps=1e-5, out=None, act="none", M=None, splitk=0):
+        """act(LayerNorm(x) W^T + b) with the norm applied as X is loaded (fo_gemm_ln; M <= 32); stats:
+        the RowStats(with_sums=True) a rowstats() producer filled for x."""
+        _check_dev(x)
+        M = x.shape[0] if M is None else M
+        if x.dtype != F32 or x.stride(-1) != 1 or x.shape[-1] < self.Kp or self.Kp != self.K:
+            raise ValueError("fused LayerNorm GEMM needs fp32 unit-stride X with K % 32 == 0")
+        if stats.groups <= 0 or stats.buf1 is None:
+            raise RuntimeError("LayerNorm statistics consumed before a producer filled them")
+        if out is None:
+            out = torch.empty(M, self.N, dtype=F32, device=x.device)
+        rt = Runtime.get(x.device)
+        _lib.call("fo_gemm_ln", x.data_ptr(), x.stride(0), M, self.Kp, self.packed.data_ptr(), self.N, ptr(self.bias),
+                  lnw.data_ptr(), lnb.data_ptr(), float(eps), stats.buf1.data_ptr(), stats.buf.data_ptr(),
+                  stats.groups, out.data_ptr(), out.stride(0), ACT[act], rt.ws.data_ptr(), rt.ws.numel(), splitk,
+                  stream(x.device))
+        return out
+
+    def rowstats(self, x, out, stats, residual=False, act="none", M=None, splitk=0):
+        """fp32 GEMM that also fills stats (per-row partial sums of out and out^2) for ln()."""
+        import ctypes
+        _check_dev(x)
+        M = x.shape[0] if M is None else M
+        if stats.buf1 is None:
+            raise ValueError("rowstats needs RowStats(with_sums=True)")
+        rt = Runtime.get(x.device)
+        sg = ctypes.c_int(0)
+        _lib.call("fo_gemm_rowstats", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                  self.packed.data_ptr(), self.N, ptr(self.bias), out.data_ptr(), out.stride(0), ACT[act],
+                  1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), splitk, stats.buf1.data_ptr(),
+                  stats.buf.data_ptr(), ctypes.byref(sg), stream(x.device))
+        if sg.value > stats.max_groups:
+            raise RuntimeError(f"RowStats holds {stats.max_groups} groups per row, GEMM wrote {sg.value}")
+        stats.groups = sg.value
+        return out
+
     def qkv_rope(self, x, M, pos, slot, cos_t, sin_t, q_out, kc, vc, H, KVH, PS, norm=None, splitk=0):
         """Fused q|k|v projection + bias + RoPE + paged-KV append (weight packed with rope_hd):
         q_out [M, H*hd] gets the rotated queries, kc/vc (one layer's pages) the token's K/V rows at slot[m]."""
@@ -195,9 +231,10 @@ class RowStats:
     output (buf) and yg = output * gamma (the next norm's weight); the consumer GEMM reads yg as its
     input and scales rows by rsqrt(sum / K + eps).  set(gamma, yg) before each producer call."""
 
-    def __init__(self, rows, device, max_groups=256):
+    def __init__(self, rows, device, max_groups=256, with_sums=False):
         self.max_groups = max_groups
         self.buf = torch.empty(rows * max_groups, dtype=F32, device=device)
+        self.buf1 = torch.empty(rows * max_groups, dtype=F32, device=device) if with_sums else None  # LayerNorm
         self.groups = 0
         self.gamma = self.yg = None
 

@@ -14,6 +14,7 @@
 Batched: one launch sequence serves all users of a replica; per-user state lives in slot pools.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -185,6 +186,7 @@ class SpeechEncoderEngine:
                 "y2": e(B * H2 * W2, C), "z": e(B * T, C * self.F), "o": e(B * T, self.out.N),
                 "x": e(B * T, self.d), "h": e(B * T, self.d), "qkv": e(B * T, 3 * self.d),
                 "att": e(B * T, self.d), "f": e(B * T, self.layers[0]["ff1"].N),
+                "sA": ops.RowStats(B * T, dev, with_sums=True), "sB": ops.RowStats(B * T, dev, with_sums=True),
                 "meta": torch.empty(4 * B, dtype=I32, device=dev)}
 
     def host_meta(self, caches, pe_indices):
@@ -224,15 +226,29 @@ class SpeechEncoderEngine:
         st, ln, rg, ps = meta[:B], meta[B:2 * B], meta[2 * B:3 * B], meta[3 * B:]
         h, qkv, att, f = bufs["h"], bufs["qkv"], bufs["att"], bufs["f"]
         scale = 1.0 / math.sqrt(self.dk)
+        # pre-norms applied by the GEMMs on load (fo_gemm_ln) from the residual producers' row sums
+        fuse_ln = B * T <= 32 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
+        sA, sB = bufs["sA"], bufs["sB"]
+        last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
-            ops.layernorm(x, *L["ln1"], out=h)
-            L["qkv"](h, out=qkv)
+            if fuse_ln and i > 0:
+                L["qkv"].ln(x, *L["ln1"], sA, out=qkv)
+            else:
+                ops.layernorm(x, *L["ln1"], out=h)
+                L["qkv"](h, out=qkv)
             ops.relpos_attention_fused(qkv, self.kr[i], self.vr[i], self.cap, st, ln, rg, self.ptab[i], ps,
                                        L["bu"], L["bv"], B, T, self.h, self.dk, scale, att)
-            L["out"](att, out=x, residual=True)
-            ops.layernorm(x, *L["ln2"], out=h)
-            L["ff1"](h, out=f, act="relu")
-            L["ff2"](f, out=x, residual=True)
+            if fuse_ln:
+                L["out"].rowstats(att, x, sB, residual=True)
+                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu")
+            else:
+                L["out"](att, out=x, residual=True)
+                ops.layernorm(x, *L["ln2"], out=h)
+                L["ff1"](h, out=f, act="relu")
+            if fuse_ln and i < last:
+                L["ff2"].rowstats(f, x, sA, residual=True)
+            else:
+                L["ff2"](f, out=x, residual=True)
         ops.layernorm(x, *self.after, out=x)
         return x, T
 

@@ -61,6 +61,19 @@ int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void
                      float* ws, long long ws_floats, int* counters, int splitk, const float* rstats, int rgroups,
                      float eps, const int* pos, const int* slot, const float* cos_t, const float* sin_t, float* q_out,
                      float* kc, float* vc, int H, int KVH, int hd, int PS, hipStream_t stream);
+/* Linear layer with the preceding LayerNorm applied to X as it is loaded (a speech-encoder block's
+ * pre-norm + projection: norm1 -> linear_q/k/v and norm2 -> feed_forward.w_1,
+ * models/encoder/transformer.py:103-130): Y = act(LN(X; lnw, lnb, eps) W^T + bias), X fp32, M <= 32.
+ * Row mean / variance come from the producer GEMM's partial sums (fo_gemm_rowstats): rsum / rsumsq
+ * [M][rgroups]. */
+int fo_gemm_ln(const float* X, int ldx, int M, int K, const void* Wp, int N, const float* bias, const float* lnw,
+               const float* lnb, float eps, const float* rsum, const float* rsumsq, int rgroups, float* Y, int ldy,
+               int act, float* ws, long long ws_floats, int splitk, hipStream_t stream);
+/* fo_gemm (fp32 Y) that also writes per-row partial sums of Y and Y^2 per workgroup column group
+ * (*sgroups of them) for a following fo_gemm_ln (the residual-stream producers of an encoder block). */
+int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,
+                     float* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int splitk,
+                     float* rsum, float* rsumsq, int* sgroups, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
 long long fo_pack_weight_elems(int N, int K);

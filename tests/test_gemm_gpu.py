@@ -20,7 +20,8 @@ def _ref(x_bf, w_bf, bias, act, resid):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 64, 64), (3, 100, 96), (16, 4608, 3584), (17, 3584, 18944), (40, 1024, 9216),
-                                   (64, 896, 896), (130, 272, 160), (7, 152, 32)])
+                                   (64, 896, 896), (130, 272, 160), (7, 152, 32), (260, 1024, 288),
+                                   (608, 1024, 9216)])
 @pytest.mark.parametrize("act", ["none", "relu"])
 def test_gemm_matches_fp32(dev, M, N, K, act):
     from fo.ops import PackedLinear
@@ -134,3 +135,33 @@ def test_gemm_qkv_rope(dev, M, H, KVH, hd, K, splitk):
         vref[pg, :, off] = heads[m, H + KVH:]
     torch.testing.assert_close(kc.cpu().double(), kref, rtol=2e-5, atol=2e-5)
     torch.testing.assert_close(vc.cpu().double(), vref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("M,N,K,act,splitk,psplit", [(32, 3072, 1024, "none", 0, 0), (32, 4096, 1024, "relu", 0, 4),
+                                                     (17, 1024, 1024, "none", 2, 0), (8, 96, 32, "relu", 0, 0),
+                                                     (1, 64, 64, "none", 0, 2), (32, 64, 32, "none", 0, 0)])
+def test_gemm_layernorm_on_load(dev, M, N, K, act, splitk, psplit):
+    """fo_gemm_rowstats (residual producer writing row sums / sums of squares) -> fo_gemm_ln (LayerNorm
+    applied to X on load from those statistics) vs residual + LayerNorm + Linear in fp64."""
+    from fo import ops
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M + N + K)
+    Kp = 96
+    wp = (torch.randn(K, Kp, generator=g) / Kp ** 0.5).to(torch.bfloat16)
+    xp = torch.randn(M, Kp, generator=g)
+    r = torch.randn(M, K, generator=g) * 2 + 0.7
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g)
+    lw, lb = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1
+    prod, lin = PackedLinear(wp.to(dev)), PackedLinear(w.to(dev), b.to(dev))
+    st = ops.RowStats(M, dev, with_sums=True)
+    x = r.clone().to(dev)
+    prod.rowstats(xp.to(dev), x, st, residual=True, splitk=psplit)
+    y = lin.ln(x, lw.to(dev), lb.to(dev), st, 1e-5, act=act, splitk=splitk).cpu()
+    xr = r.double() + xp.double() @ wp.double().t()
+    torch.testing.assert_close(x.cpu().double(), xr, rtol=2e-5, atol=2e-5)
+    xn = torch.nn.functional.layer_norm(xr, (K,), lw.double(), lb.double(), 1e-5)
+    ref = xn @ w.double().t() + b.double()
+    if act == "relu":
+        ref = torch.relu(ref)
+    torch.testing.assert_close(y.double(), ref, rtol=5e-5, atol=5e-5)
