@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--codec-tokens", type=int, default=400)
     ap.add_argument("--top-k", type=int, default=1, help="speech decoder top_k (1 = parity/greedy)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="listen chunk by chunk (default: encoder stage of chunk c+1 overlaps the LLM of chunk c)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
@@ -79,6 +81,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
     fb = engine.fbank("A")
     CH = turns[0].framer.chunk
     n_chunks = int(math.ceil(len(pcms[0]) / CH))
+    pipe = engine.listen_pipe() if args.pipeline else None
     for c in range(n_chunks):
         wins, firsts = [], []
         for t in turns:
@@ -91,9 +94,16 @@ def run_turn(engine, base_kv, pcms, args, sync):
         feats = fb(np.stack(wins), firsts)
         items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=feats[b], kv=t.kv,
                       enc_cache=t.enc_cache, ada_cache=t.ada_cache, pe_index=t.pe) for b, t in enumerate(turns)]
-        res = engine.listen(items)
-        for t, r in zip(turns, res):
-            t.enc_cache, t.ada_cache, t.pe = r["enc_cache"], r["ada_cache"], r["pe_index"]
+        if pipe is not None and c > 0:
+            # steady state: this chunk's encoder stage overlaps the previous chunk's LLM stage
+            pe_next, _ = pipe.push(items)
+            for t, pe in zip(turns, pe_next):
+                t.pe = pe
+        else:
+            for t, r in zip(turns, engine.listen(items)):
+                t.enc_cache, t.ada_cache, t.pe = r["enc_cache"], r["ada_cache"], r["pe_index"]
+    if pipe is not None:
+        pipe.flush()
     # ---- dialog_ss (benchmark policy forces it at end of input, as bin/inference.py:138 does)
     sync()
     t_ss = time.perf_counter()

@@ -89,6 +89,11 @@ int fo_stream_create(void** s_out) {
   *s_out = (void*)s;
   return 0;
 }
+// Order stream s after event ev (cross-stream dependency of the pipelined listen stages).
+int fo_stream_wait_event(hipStream_t s, void* ev) {
+  FO_HIP(hipStreamWaitEvent(s, (hipEvent_t)ev, 0));
+  return 0;
+}
 int fo_stream_destroy(void* s) {
   FO_HIP(hipStreamDestroy((hipStream_t)s));
   return 0;

@@ -148,18 +148,25 @@ class FreezeOmniEngine:
                 return False
         return ident in ("user", "system")
 
-    def _listen_graph(self, items):
+    def _listen_graph_for(self, items, slots=1, extra=64):
         ident = items[0]["identity"]
         B, R = len(items), items[0]["feats"].shape[0]
-        need = max(it["kv"].length for it in items) + 64
-        key = (ident, B, R)
+        need = max(it["kv"].length for it in items) + extra
+        key = (ident, B, R, slots)
         g = self._lgraphs.get(key)
         if g is None or g.max_keys < need:
             if g is not None:
                 g.destroy()
-            g = ListenGraph(self, ident, B, R, max(need + 1024, 2048))
+            g = ListenGraph(self, ident, B, R, max(need + 1024, 2048), slots=slots)
             self._lgraphs[key] = g
-        return g.run(items)
+        return g
+
+    def _listen_graph(self, items):
+        return self._listen_graph_for(items).run(items)
+
+    def listen_pipe(self):
+        """A ListenPipe over this engine (encoder stage of chunk c+1 overlapped with the LLM of chunk c)."""
+        return ListenPipe(self)
 
     def _listen_eager(self, items):
         for it in items:
@@ -242,15 +249,52 @@ class FreezeOmniEngine:
         return out.cpu().tolist(), hid
 
 
+class _HostRing:
+    """Pinned host staging buffers for one metadata block, reused once their upload has run."""
+
+    def __init__(self, n, depth=4):
+        self.bufs = [torch.empty(n, dtype=I32).pin_memory() for _ in range(depth)]
+        self.events = []
+        for _ in self.bufs:
+            e = ctypes.c_void_p()
+            _lib.call("fo_event_create", ctypes.byref(e))
+            self.events.append(e)
+        self.i = 0
+
+    def next(self):
+        k = self.i % len(self.bufs)
+        if self.i >= len(self.bufs):
+            _lib.call("fo_event_sync", self.events[k])  # that buffer's previous upload has run
+        self.i += 1
+        return k, self.bufs[k].numpy()
+
+    def upload(self, k, dst, stream):
+        with torch.cuda.stream(stream):
+            dst.copy_(self.bufs[k], non_blocking=True)
+        _lib.call("fo_event_record", self.events[k], stream.cuda_stream)
+
+    def destroy(self):
+        for e in self.events:
+            _lib.call("fo_event_destroy", e)
+        self.events = []
+
+
 class ListenGraph:
     """Steady-state listen step for B sessions of one identity (status ipu_cl / ipu_el: no chat
-    prefix), captured once as a hipGraph: features -> encoder -> adapter -> fp16-rounded LLM rows ->
-    Qwen2 chunk prefill on paged KV -> final norm -> dialog-state head (models/audioLLM.py:350-429).
-    Per-call inputs go through static buffers: the features (device copy) and one metadata block
-    (encoder ring positions, adapter cache slots, LLM positions / cache slots / visible keys / block
-    tables) uploaded with a single async copy from pinned memory."""
+    prefix) as two captured hipGraphs (models/audioLLM.py:350-429):
+      encoder stage: features -> encoder -> adapter -> fp16-rounded LLM input rows (x slot)
+      LLM stage:     x slot -> Qwen2 chunk prefill on paged KV -> final norm -> dialog-state head
+    Per-call inputs go through static buffers: the features (device copy) and one metadata block per
+    stage (encoder ring positions / adapter cache slots; LLM positions, cache slots, visible keys,
+    block tables), each uploaded with a single async copy from pinned memory.
 
-    def __init__(self, eng, ident, B, R, max_keys):
+    run(items): both stages back to back on the engine stream.
+    pipelined: with slots=2, the encoder stage of chunk c+1 runs on a side stream while the LLM stage
+    of chunk c runs on the engine stream (ListenPipe); the two stages share nothing but the x slot,
+    ordered by events.  The state decision of chunk c does not depend on chunk c+1, so the results are
+    those of the sequential order."""
+
+    def __init__(self, eng, ident, B, R, max_keys, slots=1):
         dev = eng.device
         self.eng, self.ident, self.B, self.R, self.max_keys = eng, ident, B, R, max_keys
         enc, ada, llm = eng.enc[ident], eng.ada[ident], eng.llm
@@ -265,65 +309,99 @@ class ListenGraph:
         assert To * G <= 16, "listen graph: one attention work item per session"
         PS = llm.pool.PS
         self.maxb = (max_keys + PS - 1) // PS
-        # metadata block: [enc 4B | ada slots B | tok_pos n | tok_slot n | tok_nvis n | block table B*maxb]
-        self.n_meta = 5 * B + 3 * n + B * self.maxb
-        self.meta_d = torch.zeros(self.n_meta, dtype=I32, device=dev)
-        self.host = [torch.empty(self.n_meta, dtype=I32).pin_memory() for _ in range(4)]
-        self.host_ev = []
-        for _ in self.host:
-            e = ctypes.c_void_p()
-            _lib.call("fo_event_create", ctypes.byref(e))
-            self.host_ev.append(e)
-        self.hi = 0
-        m = self.meta_d
-        self.eb["meta"] = m[0:4 * B]
-        self.ab["slots"] = m[4 * B:5 * B]
-        o = 5 * B
+        # encoder metadata [enc 4B | ada slots B]; LLM metadata [tok_pos n | tok_slot n | tok_nvis n | block table]
+        self.emeta_d = torch.zeros(5 * B, dtype=I32, device=dev)
+        self.lmeta_d = torch.zeros(3 * n + B * self.maxb, dtype=I32, device=dev)
+        self.ering, self.lring = _HostRing(5 * B), _HostRing(3 * n + B * self.maxb)
+        self.eb["meta"] = self.emeta_d[0:4 * B]
+        self.ab["slots"] = self.emeta_d[4 * B:5 * B]
+        m = self.lmeta_d
         items = torch.tensor([[b, b * To, To] for b in range(B)], dtype=I32).reshape(-1).to(dev)
         self.rows = torch.tensor([b * To + To - 1 for b in range(B)], dtype=I32).to(dev)
-        self.meta = SimpleNamespace(T=n, S=B, tok_pos=m[o:o + n], tok_slot=m[o + n:o + 2 * n],
-                                    tok_nvis=m[o + 2 * n:o + 3 * n], block_table=m[o + 3 * n:].view(B, self.maxb),
-                                    items=items, n_items=B, max_rows=To * G, max_keys=max_keys)
-        self.x = torch.empty(n, llm.D, dtype=F32, device=dev)
+        self.meta = SimpleNamespace(T=n, S=B, tok_pos=m[0:n], tok_slot=m[n:2 * n], tok_nvis=m[2 * n:3 * n],
+                                    block_table=m[3 * n:].view(B, self.maxb), items=items, n_items=B,
+                                    max_rows=To * G, max_keys=max_keys)
+        self.slots = slots
+        self.xs = [torch.empty(n, llm.D, dtype=F32, device=dev) for _ in range(slots)]
+        self.x = self.xs[0]
         self.ws = llm.stack.workspace(n, ops.attn_nsplit(max_keys, B, llm.KVH), dev)
         self.predict = ident == "user" and bool(eng.predict_usr_state) and llm.head_w is not None
         self.probs = torch.empty(B, 3, dtype=F32, device=dev)
         self.probs_host = torch.empty(B, 3, dtype=F32).pin_memory()
-        self.exec = None
-        s = ops.stream(dev)
+        self.main = ops.engine_stream(dev)
+        self.side = ops.engine_stream(dev, side=True) if slots > 1 else self.main
+        self.enc_exec = [self._capture(self.main, lambda k=k: self._enc_body(k)) for k in range(slots)]
+        self.llm_exec = [self._capture(self.main, lambda k=k: self._llm_body(k)) for k in range(slots)]
+        self.ev_enc = [self._event() for _ in range(slots)]
+        self.ev_llm = [self._event() for _ in range(slots)]
+        self.llm_used = [False] * slots
+        self.exec = True
+
+    @staticmethod
+    def _event():
+        e = ctypes.c_void_p()
+        _lib.call("fo_event_create", ctypes.byref(e))
+        return e
+
+    @staticmethod
+    def _capture(stream, body):
+        s = stream.cuda_stream
         _lib.call("fo_graph_begin", s)
         try:
-            self._body()
+            with torch.cuda.stream(stream):
+                body()
         finally:
             ex = ctypes.c_void_p()
             _lib.call("fo_graph_end", s, ctypes.byref(ex))
-        self.exec = ex
+        return ex
 
-    def _body(self):
-        B, R, llm = self.B, self.R, self.llm
+    def _enc_body(self, k):
+        B, R = self.B, self.R
         xe, T = self.enc.run(self.feats, B, R, self.eb)
         emb, To = self.ada.run(xe, B, T, self.ab)
-        ops.gather_rows(emb, None, out=self.x, round_fp16=True)   # inputs_embeds.half()
-        llm.stack.forward(self.x, self.meta, self.ws)
-        ops.rmsnorm(self.x, llm.norm, llm.eps, out=self.x)
-        if self.predict:
-            ops.state_head(self.x, self.rows, llm.head_w, llm.head_b, self.probs)
+        ops.gather_rows(emb, None, out=self.xs[k], round_fp16=True)   # inputs_embeds.half()
 
-    def run(self, items):
-        B, To, maxb = self.B, self.To, self.maxb
-        enc = self.enc
+    def _llm_body(self, k):
+        llm, x = self.llm, self.xs[k]
+        llm.stack.forward(x, self.meta, self.ws)
+        ops.rmsnorm(x, llm.norm, llm.eps, out=x)
+        if self.predict:
+            ops.state_head(x, self.rows, llm.head_w, llm.head_b, self.probs)
+
+    # ---------------------------------------------------------------- stages
+    def submit_encoder(self, items, k=0):
+        """Encoder stage of one chunk into x slot k (side stream when pipelined).  Advances the
+        encoder caches; returns the per-session pe_index after this chunk."""
+        B = self.B
         caches = [it["enc_cache"] for it in items]
-        emeta, new_pe = enc.host_meta(caches, [it["pe_index"] or 0 for it in items])
-        slot = self.hi % len(self.host)
-        self.hi += 1
-        if self.hi > len(self.host):
-            _lib.call("fo_event_sync", self.host_ev[slot])  # that slot's previous upload has run
-        h = self.host[slot].numpy()
+        emeta, new_pe = self.enc.host_meta(caches, [it["pe_index"] or 0 for it in items])
+        j, h = self.ering.next()
         h[0:4 * B] = emeta
         h[4 * B:5 * B] = [it["ada_cache"].slot for it in items]
+        st = self.side
+        if self.slots > 1 and self.llm_used[k]:
+            _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_llm[k])  # slot k's last reader is done
+        with torch.cuda.stream(st):
+            f0 = items[0]["feats"]
+            if f0.is_contiguous() and all(it["feats"].data_ptr() == f0.data_ptr() + b * self.R * 80 * 4
+                                          for b, it in enumerate(items)):
+                self.feats.copy_(f0.as_strided((B, self.R, 80), (self.R * 80, 80, 1)))  # one batched tensor
+            else:
+                for b, it in enumerate(items):
+                    self.feats[b].copy_(it["feats"])
+        self.ering.upload(j, self.emeta_d, st)
+        _lib.call("fo_graph_launch", self.enc_exec[k], st.cuda_stream)
+        _lib.call("fo_event_record", self.ev_enc[k], st.cuda_stream)
+        self.enc.advance(caches, self.T)
+        return new_pe
+
+    def submit_llm(self, items, new_pe, k=0):
+        """LLM stage of the chunk whose encoder stage filled x slot k (engine stream); appends To KV
+        rows per session and returns the per-session results (reads the state head back)."""
+        B, To, maxb = self.B, self.To, self.maxb
         n = B * To
-        o = 5 * B
-        bt = h[o + 3 * n:].reshape(B, maxb)
+        j, h = self.lring.next()
+        bt = h[3 * n:].reshape(B, maxb)
         for b, it in enumerate(items):
             kv = it["kv"]
             old = kv.length
@@ -332,40 +410,85 @@ class ListenGraph:
                 raise RuntimeError("listen graph block table too small")
             for i in range(To):
                 r = b * To + i
-                h[o + r] = old + i
-                h[o + n + r] = kv.slot(old + i)
-                h[o + 2 * n + r] = old + i + 1
+                h[r] = old + i
+                h[n + r] = kv.slot(old + i)
+                h[2 * n + r] = old + i + 1
             bt[b, :len(kv.pages)] = kv.pages
             kv.length = old + To
-        f0 = items[0]["feats"]
-        if f0.is_contiguous() and all(it["feats"].data_ptr() == f0.data_ptr() + b * self.R * 80 * 4
-                                      for b, it in enumerate(items)):
-            self.feats.copy_(f0.as_strided((B, self.R, 80), (self.R * 80, 80, 1)))  # one batched feature tensor
-        else:
-            for b, it in enumerate(items):
-                self.feats[b].copy_(it["feats"])
-        st = ops.stream(self.eng.device)
-        self.meta_d.copy_(self.host[slot], non_blocking=True)
-        _lib.call("fo_event_record", self.host_ev[slot], st)
-        _lib.call("fo_graph_launch", self.exec, st)
-        enc.advance(caches, self.T)
+        st = self.main
+        self.lring.upload(j, self.lmeta_d, st)
+        if self.side is not self.main:
+            _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_enc[k])
+        _lib.call("fo_graph_launch", self.llm_exec[k], st.cuda_stream)
+        _lib.call("fo_event_record", self.ev_llm[k], st.cuda_stream)
+        self.llm_used[k] = True
         probs = None
         if self.predict:
-            self.probs_host.copy_(self.probs, non_blocking=False)
+            with torch.cuda.stream(st):
+                self.probs_host.copy_(self.probs, non_blocking=False)
             probs = self.probs_host.numpy()
         res = []
         for b, it in enumerate(items):
             r = {"enc_cache": it["enc_cache"], "ada_cache": it["ada_cache"], "pe_index": new_pe[b],
-                 "hidden_row": (self.x, b * To + To - 1), "probs": None}
+                 "hidden_row": (self.xs[k], b * To + To - 1), "probs": None}
             if probs is not None:
                 r["probs"] = {"state_1": float(probs[b, 1]), "state_2": float(probs[b, 2])}
             res.append(r)
         return res
 
+    def run(self, items):
+        return self.submit_llm(items, self.submit_encoder(items, 0), 0)
+
     def destroy(self):
         if self.exec is not None:
-            _lib.call("fo_graph_destroy", self.exec)
+            for ex in self.enc_exec + self.llm_exec:
+                _lib.call("fo_graph_destroy", ex)
+            for e in self.ev_enc + self.ev_llm:
+                _lib.call("fo_event_destroy", e)
+            self.ering.destroy()
+            self.lring.destroy()
             self.exec = None
-        for e in self.host_ev:
-            _lib.call("fo_event_destroy", e)
-        self.host_ev = []
+
+
+class ListenPipe:
+    """Pipelined steady-state listen for one batch of sessions (ListenGraph with two x slots): the
+    encoder stage of the chunk just pushed overlaps the LLM stage of the previous chunk.
+
+        pipe = engine.listen_pipe()
+        pe_next, prev = pipe.push(items_c)   # chunk c's next pe_index per session; results of chunk c-1
+        ...; last = pipe.flush()
+    (encoder / adapter caches are advanced in place at submission, like listen(); pe_index is returned
+    at submission so the caller can build the next chunk's items before chunk c's LLM stage ran)
+
+    Every push must be graphable (same identity and batch, no chat prefix, open caches); the results
+    are identical to calling listen() chunk by chunk."""
+
+    def __init__(self, eng):
+        self.eng, self.g, self.pending, self.k = eng, None, None, 0
+
+    def push(self, items):
+        eng = self.eng
+        with torch.cuda.stream(ops.engine_stream(eng.device)):
+            if not eng._graphable(items):
+                raise ValueError("ListenPipe.push: items must be steady-state chunks (no chat prefix, open caches)")
+            g = eng._listen_graph_for(items, slots=2, extra=64 * 2)
+            if self.g is not None and g is not self.g:
+                raise RuntimeError("ListenPipe: the batch changed (flush before changing sessions)")
+            self.g = g
+            k = self.k
+            pe = g.submit_encoder(items, k)
+            out = None
+            if self.pending is not None:
+                pitems, ppe, pk = self.pending
+                out = g.submit_llm(pitems, ppe, pk)
+            self.pending = (items, pe, k)
+            self.k = 1 - k
+            return pe, out
+
+    def flush(self):
+        if self.pending is None:
+            return None
+        with torch.cuda.stream(ops.engine_stream(self.eng.device)):
+            items, pe, k = self.pending
+            self.pending = None
+            return self.g.submit_llm(items, pe, k)

@@ -24,18 +24,20 @@ def stream(device=None):
 _ENGINE_STREAMS = {}
 
 
-def engine_stream(device):
+def engine_stream(device, side=False):
     """A blocking HIP stream per device (fo_stream_create) wrapped for torch: it orders against the
-    legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it."""
+    legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it.
+    side=True: a second such stream, for work that overlaps the main one (pipelined listen stages)."""
     import ctypes
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
-    if idx not in _ENGINE_STREAMS:
+    key = (idx, bool(side))
+    if key not in _ENGINE_STREAMS:
         h = ctypes.c_void_p()
         with torch.cuda.device(idx):
             _lib.call("fo_stream_create", ctypes.byref(h))
-        _ENGINE_STREAMS[idx] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
-    return _ENGINE_STREAMS[idx]
+        _ENGINE_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    return _ENGINE_STREAMS[key]
 
 
 class Runtime:

@@ -26,6 +26,7 @@ int fo_graph_launch(void* exec, hipStream_t s);
 int fo_graph_destroy(void* exec);
 int fo_stream_create(void** s_out);
 int fo_stream_destroy(void* s);
+int fo_stream_wait_event(hipStream_t s, void* ev);
 int fo_host_alloc(long long bytes, void** host_ptr, void** dev_ptr);
 int fo_host_free(void* host_ptr);
 int fo_event_sync(void* ev);

@@ -50,3 +50,55 @@ def test_listen_graph_matches_eager(eng, dev):
         np.testing.assert_allclose(np.array(pg), np.array(pe), atol=1e-5)
         for a, b in zip(hg, he):
             np.testing.assert_allclose(a, b, atol=2e-5, rtol=1e-5)
+
+
+def _session_pipe(eng, feats_seq, n_users):
+    """Chunk 0 through listen() (chat prefix), the rest through a ListenPipe."""
+    base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    kvs = [base.fork() for _ in range(n_users)]
+    state = [dict(enc_cache=None, ada_cache=None, pe_index=0) for _ in range(n_users)]
+    out = []
+    pipe = eng.listen_pipe()
+
+    def record(res):
+        out.append(([(r["probs"]["state_1"], r["probs"]["state_2"]) for r in res],
+                    [r["hidden_row"][0][r["hidden_row"][1]].cpu().numpy().copy() for r in res],
+                    None, [r["pe_index"] for r in res]))
+
+    for c, f in enumerate(feats_seq):
+        items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=f[u], kv=kvs[u], **state[u])
+                 for u in range(n_users)]
+        if c == 0:
+            res = eng.listen(items)
+            for u, r in enumerate(res):
+                state[u] = dict(enc_cache=r["enc_cache"], ada_cache=r["ada_cache"], pe_index=r["pe_index"])
+            record(res)
+            continue
+        pe_next, prev = pipe.push(items)
+        for u in range(n_users):
+            state[u]["pe_index"] = pe_next[u]
+        if prev is not None:
+            record(prev)
+    record(pipe.flush())
+    lens = [kv.length for kv in kvs]
+    for kv in kvs:
+        kv.free()
+    base.free()
+    return out, lens
+
+
+def test_listen_pipe_matches_sequential(eng, dev):
+    """Encoder stage of chunk c+1 overlapped with the LLM stage of chunk c gives the sequential results."""
+    g = np.load(os.path.join(G, "fbank.npz"))
+    n_users = 3
+    feats = torch.from_numpy(g["A_feats"]).to(dev)
+    seq = [torch.stack([feats[(c + 5 * u) % 13] for u in range(n_users)]) for c in range(9)]
+    ref = _session_run(eng, seq, True, n_users)
+    got, lens = _session_pipe(eng, seq, n_users)
+    assert len(got) == len(ref)
+    assert lens == ref[-1][2]
+    for (pe, he, _, qe), (pg, hg, _, qg) in zip(ref, got):
+        assert qe == qg
+        np.testing.assert_array_equal(np.array(pg), np.array(pe))
+        for a, b in zip(hg, he):
+            np.testing.assert_array_equal(a, b)
