@@ -260,16 +260,19 @@ def recorded_traffic(kernel_regex):
     return g["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
-def gemm_probe(engine, M, reps=20):
+def gemm_probe(engine, M, reps=2):
     """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the
-    k_gemm_wstream<2,...> launch of every layer) with HIP events on the launching stream."""
+    k_gemm_wstream<4,1,true,...,true> launch of every layer) with HIP events on the launching stream.
+    The launches walk all layers' gate/up weights in order, as a chunk step does, so no launch finds
+    its weights in the Infinity Cache from the previous one (273 MB per layer > 256 MB MALL)."""
     import torch
     from fo import _lib, ops
-    L = engine.llm.stack.layers[0]
+    layers = engine.llm.stack.layers
+    L = layers[0]
     x = torch.randn(M, engine.llm.D, device=engine.device)
     out = torch.empty(M, L.gu.N, device=engine.device)
-    for _ in range(3):
-        L.gu(x, out=out)
+    for Lw in layers[:3]:
+        Lw.gu(x, out=out)
     lib = _lib.load()
     import ctypes
     e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
@@ -277,17 +280,20 @@ def gemm_probe(engine, M, reps=20):
     lib.fo_event_create(ctypes.byref(e1))
     s = ops.stream(engine.device)
     lib.fo_event_record(e0, s)
+    n = 0
     for _ in range(reps):
-        L.gu(x, out=out)
+        for Lw in layers:
+            Lw.gu(x, out=out)
+            n += 1
     lib.fo_event_record(e1, s)
     ms = ctypes.c_float()
     lib.fo_event_elapsed_ms(e0, e1, ctypes.byref(ms))
     lib.fo_event_destroy(e0)
     lib.fo_event_destroy(e1)
-    t = ms.value / reps / 1e3
+    t = ms.value / n / 1e3
     weight_bytes = L.gu.nbytes
     algo = weight_bytes + M * engine.llm.D * 4 + M * L.gu.N * 4
-    return {"bytes": algo, "seconds": t, "gbps": algo / t / 1e9}
+    return {"bytes": algo, "seconds": t, "gbps": algo / t / 1e9, "launches": n}
 
 
 def main():
@@ -388,7 +394,7 @@ def main():
                          "frac": round(probe["gbps"] / peak, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
-                         "kernel": "k_gemm_wstream<2,1,true> (Qwen2 gate/up SwiGLU weight stream)",
+                         "kernel": "k_gemm_wstream<4,1,true,4,4,true> (Qwen2 gate/up SwiGLU weight stream, M=16, all 28 layers in turn)",
                          "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2)},
             "cpu_baseline": cpu,
         }

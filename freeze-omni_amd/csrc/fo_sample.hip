@@ -51,10 +51,30 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
   __syncthreads();
 }
 
+// The next decode step's input, produced by the sampler itself (AR speech decoder step,
+// models/decoder/decoder.py:341-367: embed(id) -> first LlamaRMSNorm): the drawn id is recorded into
+// a history row, its embedding row becomes the residual stream x, and the first layer's RMSNorm of
+// it goes to h -- three launches of the step folded into the sampler.
+struct NextInput {
+  int* hist;            // [*][hist_ld]: hist[hist_row[0] * hist_ld + row] = id (host-mapped, read lazily)
+  const int* hist_row;
+  int hist_ld;
+  const bf16_t* emb;    // [vocab][emb_ld] bf16 embedding table
+  long long emb_ld;
+  int D;
+  float* x;             // [B][ldx] residual stream
+  int ldx;
+  const float* gamma;   // first RMSNorm weight
+  float eps;
+  float* h;             // [B][ldh] RMSNorm(x) * gamma
+  int ldh;
+};
+
+template <bool NEXT>
 __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, int V, const int* top_k_rows,
                                                  const float* temp_rows, const float* top_p_rows,
                                                  unsigned long long seed, const int* step_rows, const int* key_rows, int ban_id,
-                                                 int* out_ids, float* out_val) {
+                                                 int* out_ids, float* out_val, NextInput nx) {
   __shared__ float bv[1024];
   __shared__ int bi[1024];
   __shared__ int taken[KMAXS];
@@ -114,6 +134,37 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
     }
     out_ids[row] = pick;
     if (out_val) out_val[row] = tv[0];
+    if (NEXT) {
+      taken[0] = pick;
+      if (nx.hist) nx.hist[(size_t)nx.hist_row[0] * nx.hist_ld + row] = pick;
+    }
+  }
+  if constexpr (NEXT) {
+    __syncthreads();
+    const int id = taken[0];
+    const bf16_t* er = nx.emb + (size_t)id * nx.emb_ld;
+    float* xr = nx.x + (size_t)row * nx.ldx;
+    // same per-thread float4 sums and wave order as k_rmsnorm's 256-thread block (threads >= 256 add
+    // zeros), so h is bit-identical to the gather + rmsnorm launches it replaces
+    float s = 0.f;
+    if (threadIdx.x < 256) {
+      for (int i = threadIdx.x * 4; i < nx.D; i += 1024) {
+        const float4 v = make_float4(bf2f(er[i]), bf2f(er[i + 1]), bf2f(er[i + 2]), bf2f(er[i + 3]));
+        *reinterpret_cast<float4*>(xr + i) = v;
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
+    }
+    s = block_sum<16>(s, bv);
+    const float r = rsqrtf(s / (float)nx.D + nx.eps);
+    if (threadIdx.x < 256) {
+      float* hr = nx.h + (size_t)row * nx.ldh;
+      for (int i = threadIdx.x * 4; i < nx.D; i += 1024) {
+        const float4 v = make_float4(bf2f(er[i]), bf2f(er[i + 1]), bf2f(er[i + 2]), bf2f(er[i + 3]));
+        const float4 g = *reinterpret_cast<const float4*>(nx.gamma + i);
+        *reinterpret_cast<float4*>(hr + i) = make_float4(g.x * (v.x * r), g.y * (v.y * r), g.z * (v.z * r),
+                                                         g.w * (v.w * r));
+      }
+    }
   }
 }
 
@@ -127,9 +178,25 @@ int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const
               const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id, int* out_ids,
               float* out_maxlogit, hipStream_t s) {
   FO_REQUIRE(B > 0 && V > 0, "fo_sample: bad shape");
-  hipLaunchKernelGGL(k_sample, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step, key,
-                     ban_id, out_ids, out_maxlogit);
+  NextInput nx{};
+  hipLaunchKernelGGL(k_sample<false>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
+                     key, ban_id, out_ids, out_maxlogit, nx);
   return fo::check_launch("fo_sample");
+}
+
+// fo_sample, then for every row: hist[hist_row[0] * hist_ld + row] = id (hist nullable),
+// x[row] = emb[id] (bf16 -> fp32, D % 4 == 0) and h[row] = RMSNorm(x[row]) * gamma.
+int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
+                    const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
+                    int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
+                    int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, hipStream_t s) {
+  FO_REQUIRE(B > 0 && V > 0 && D > 0 && (D % 4) == 0 && D <= 4096, "fo_sample_embed: bad shape B=%d V=%d D=%d", B, V, D);
+  FO_REQUIRE(emb && x && gamma && h && (!hist || (hist_row && hist_ld >= B)), "fo_sample_embed: missing buffers");
+  FO_REQUIRE((ldx % 4) == 0 && (ldh % 4) == 0, "fo_sample_embed: row strides must be float4-aligned");
+  NextInput nx{hist, hist_row, hist_ld, (const bf16_t*)emb, emb_ld, D, x, ldx, gamma, eps, h, ldh};
+  hipLaunchKernelGGL(k_sample<true>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
+                     key, ban_id, out_ids, nullptr, nx);
+  return fo::check_launch("fo_sample_embed");
 }
 
 }  // extern "C"

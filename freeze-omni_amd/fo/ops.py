@@ -483,3 +483,16 @@ def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0,
               int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), ptr(out_max),
               stream(logits.device))
     return out_ids
+
+
+def sample_embed(logits, V, out_ids, emb, x, gamma, eps, h, top_k=None, temperature=None, top_p=None, seed=0,
+                 step=None, B=None, ban_id=-1, key=None, hist_ptr=None, hist_row=None, hist_ld=0):
+    """sample(), then the next decode step's input from the drawn ids: x[b] = emb[id_b] (fp32), h[b] =
+    RMSNorm(x[b]) * gamma, and (hist_ptr) hist[hist_row[0] * hist_ld + b] = id_b -- one launch."""
+    B = logits.shape[0] if B is None else B
+    _lib.call("fo_sample_embed", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), hist_ptr,
+              ptr(hist_row), hist_ld, emb.data_ptr(), emb.stride(0), emb.shape[1], x.data_ptr(), x.stride(0),
+              gamma.data_ptr(), float(eps), h.data_ptr(), h.stride(0), stream(logits.device))
+    return out_ids
+

@@ -152,8 +152,9 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
                 if g is None or ng.B != g.B:
                     ng.ids.fill_(tts.sos) if step == 0 else ng.ids.copy_(torch.tensor(
                         [states[i].all_ids[-1] for i in live], dtype=I32).to(dev))
+                    ng.prime()
                 else:
-                    ng.ids.copy_(g.ids)  # same batch, other sampler bound: ids stay on the device
+                    ng.adopt(g)  # same batch, other sampler bound: ids and input rows stay on the device
                 g = ng
             ev = g.launch([states[i].seq for i in live], live, step, step)
             pending.append((step, list(live), g, ev))

@@ -64,9 +64,14 @@ class DecoderStack:
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
         return ws
 
-    def forward(self, x, meta: BatchMeta, ws=None):
+    def forward(self, x, meta: BatchMeta, ws=None, pre_normed=False, final_norm=None):
         """x: fp32 [T, D] residual stream, updated in place; KV for meta's tokens is appended.
-        ws: optional workspace() of at least meta.T tokens (then nothing is allocated here)."""
+        ws: optional workspace() of at least meta.T tokens (then nothing is allocated here).
+        pre_normed: ws["h"] already holds the first layer's input RMSNorm of x (written by the
+        previous decode step's sampler, fo_sample_embed).
+        final_norm: gamma of the norm after the stack; the last down projection then also writes
+        ws["xg"] = x * gamma and ws["sA"] row statistics, so the consumer GEMM (the output head) applies
+        that RMSNorm on load instead of a separate norm launch."""
         T = meta.T
         H, KVH, hd = self.H, self.KVH, self.hd
         if ws is None:
@@ -81,7 +86,8 @@ class DecoderStack:
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
                     self.pool.PS)
             if i == 0:  # the stream's first rows come from a gather: no producer statistics yet
-                ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
+                if not pre_normed:
+                    ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
                 L.qkv.qkv_rope(h, T, *rope)
             else:       # input RMSNorm fused: x*gamma and row sums came from the previous down proj
                 L.qkv.qkv_rope(xg, T, *rope, norm=(sA, self.eps))
@@ -90,8 +96,10 @@ class DecoderStack:
                           att)
             L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))
             L.gu(xg, out=m, M=T, norm=(sB, self.eps))
-            if i == last:
+            if i == last and final_norm is None:
                 L.down(m, out=x, residual=True, M=T)
+            elif i == last:
+                L.down(m, out=x, residual=True, M=T, stats_out=sA.set(final_norm, xg))
             else:
                 L.down(m, out=x, residual=True, M=T, stats_out=sA.set(self.layers[i + 1].ln1, xg))
         return x

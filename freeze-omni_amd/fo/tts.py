@@ -93,13 +93,21 @@ class TTSEngine:
     def step(self, seqs, tokens):
         """tokens: device int32 [B] (current input ids).  Returns logits [B, vocab+4] (fp32)."""
         dev = self.device
-        x = ops.gather_rows(self.embedding, tokens)
+        B = len(seqs)
         meta = BatchMeta([(s.kv, 1, s.kv.length - s.P, False) for s in seqs], dev)
-        self.main.forward(x, meta)
-        ops.rmsnorm(x, self.norm, self.eps, out=x)
+        ws = self.main.workspace(B, ops.attn_nsplit(meta.max_keys, meta.n_items, self.H), dev)
+        x = self.embed_input(tokens, ws, B)
+        self.main.forward(x, meta, ws, pre_normed=True, final_norm=self.norm)
         for s in seqs:
             s.generated += 1
-        return self.out_fnn(x)
+        return self.out_fnn(ws["xg"][:B], norm=(ws["sA"], self.eps))
+
+    def embed_input(self, tokens, ws, B, x=None):
+        """x = embedding[tokens] (fp32) and ws["h"] = the first layer's RMSNorm of it: the decode step's
+        input, as fo_sample_embed writes it for the next step inside the captured graph."""
+        x = ops.gather_rows(self.embedding, tokens, out=x, M=B)
+        ops.rmsnorm(x, self.main.layers[0].ln1, self.eps, out=ws["h"], M=B)
+        return x
 
     def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows):
         """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows)."""
@@ -164,14 +172,24 @@ class DecodeGraph:
         self._capture()
 
     def _body(self):
+        # x / ws["h"] hold this step's input (prime() or the previous replay's sampler); the sampler
+        # records the drawn ids and writes the next step's input rows (fo_sample_embed)
         t = self.tts
-        ops.gather_rows(t.embedding, self.ids, out=self.x)
-        t.main.forward(self.x, self.meta, self.ws)
-        ops.rmsnorm(self.x, t.norm, t.eps, out=self.x)
-        t.out_fnn(self.x, out=self.logits)
-        ops.sample(self.logits, self.V_sample, self.ids, self.topk, None, None, seed=self.seed, step=self.meta.step,
-                   B=self.B, key=self.meta.key)
-        ops.record_ids(self.ids, self.B, self.hist.dev, self.B, self.meta.hist_row)
+        t.main.forward(self.x, self.meta, self.ws, pre_normed=True, final_norm=t.norm)
+        t.out_fnn(self.ws["xg"], out=self.logits, norm=(self.ws["sA"], t.eps))
+        ops.sample_embed(self.logits, self.V_sample, self.ids, t.embedding, self.x, t.main.layers[0].ln1, t.eps,
+                         self.ws["h"], top_k=self.topk, seed=self.seed, step=self.meta.step, B=self.B,
+                         key=self.meta.key, hist_ptr=self.hist.dev, hist_row=self.meta.hist_row, hist_ld=self.B)
+
+    def prime(self):
+        """Input rows of the next replay from self.ids (first step of a batch, or after the batch changed)."""
+        self.tts.embed_input(self.ids, self.ws, self.B, x=self.x)
+
+    def adopt(self, other):
+        """Continue another graph's batch (same sessions, other sampler bound): take its ids and input rows."""
+        self.ids.copy_(other.ids)
+        self.x.copy_(other.x)
+        self.ws["h"].copy_(other.ws["h"])
 
     def _capture(self):
         s = ops.stream(self.tts.device)

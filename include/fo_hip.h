@@ -192,6 +192,13 @@ int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s);
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
               const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
               int* out_ids, float* out_maxlogit, hipStream_t s);
+/* fo_sample fused with the next AR decode step's input (models/decoder/decoder.py:341-346: embed(id) ->
+ * first LlamaRMSNorm): hist[hist_row[0] * hist_ld + row] = id (hist nullable), x[row] = emb[id] (bf16
+ * table -> fp32), h[row] = RMSNorm(x[row]) * gamma. */
+int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
+                    const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
+                    int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
+                    int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, hipStream_t s);
 
 #ifdef __cplusplus
 }
