@@ -581,14 +581,21 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.rhd = rope->rhd;
     a.rPS = rope->rPS;
   }
-  const int RB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  // mid-size row counts on large weights (the Qwen2 prefills of a turn: assistant prefix, the first
+  // chunk with its chat prefix, the system prompt; 17..64 rows): one row tile of ceil(M/16) row blocks
+  // against 4-tile column groups, so X (fp32, re-read by every column group) costs about what the
+  // weights do, and no grid of 64-row tiles streams X four times per weight byte
+  const bool mid = x_f32 && !lnw && M > 16 && M <= 64 && (long long)a.ntiles * 16 * K >= (8ll << 20);
+  const int RB = mid ? (M + 15) / 16 : (M <= 16 ? 1 : (M <= 32 ? 2 : 4));
   const int mt = (M + RB * 16 - 1) / (RB * 16);
   // tiles per workgroup: the activation rows are re-read by every workgroup, so workgroups that
   // cover more output columns read X fewer times per weight byte (measured, gemm_sweep.py)
   int NT = swiglu ? 2 : 1;
   int S_auto = 0;
   const int KS = K >> 5;
-  if (RB == 1) {
+  if (mid) {
+    NT = a.ntiles % 4 == 0 ? 4 : 2;
+  } else if (RB == 1) {
     // measured policy (gemm_sweep.py): wide layers (>= 1024 tiles: Qwen2 gate/up, lm_head) take 4
     // tiles per workgroup; long-K layers (Qwen2 down) 4 tiles and a 4-way K split; mid-size grids
     // (> 256 tiles: Qwen2 qkv) 2 tiles; small ones 1
@@ -616,7 +623,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   if (rope) NT = 2;  // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds
   if (lnw && NT > 2) NT = 2;
   const int groups = a.ntiles / NT;
-  int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : fo_gemm_pick_split(M, groups, K));
+  if (mid && !rstats) {  // narrow layers (Qwen2 q|k|v, o, down): split K until the grid covers the chip
+    S_auto = groups >= 192 ? 1 : (256 + groups - 1) / groups;
+    if (S_auto > 4) S_auto = 4;
+    if (S_auto > KS / 16) S_auto = KS / 16 > 0 ? KS / 16 : 1;
+  }
+  int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : (mid ? 1 : fo_gemm_pick_split(M, groups, K)));
   if (rstats && !lnw) S = 1;  // the rstd scale is applied before the epilogue of a single-pass GEMM
   if (S > (K >> 5)) S = K >> 5;
   a.S = S;
@@ -640,6 +652,18 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       else { if (nw == 16) FO_LN(1, 2, 16); else FO_LN(1, 2, 8); }
     }
 #undef FO_LN
+  } else if (mid) {
+    // 2 k-steps in flight per wave keep the RB x NT accumulators and fragments within 4 waves / SIMD
+    const int nw = (NT == 4 || wgs >= 384) ? 4 : 8;
+#define FO_MID(NT_, RB_, NW_, SW_) hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, true, NW_, 2, SW_>), grid, dim3(NW_ * 64), 0, stream, a)
+#define FO_MID_RB(NT_, NW_, SW_) { if (RB == 2) FO_MID(NT_, 2, NW_, SW_); else if (RB == 3) FO_MID(NT_, 3, NW_, SW_); else FO_MID(NT_, 4, NW_, SW_); }
+    if (swiglu) {
+      if (NT == 4) FO_MID_RB(4, 4, true) else if (nw == 4) FO_MID_RB(2, 4, true) else FO_MID_RB(2, 8, true)
+    } else {
+      if (NT == 4) FO_MID_RB(4, 4, false) else if (nw == 4) FO_MID_RB(2, 4, false) else FO_MID_RB(2, 8, false)
+    }
+#undef FO_MID_RB
+#undef FO_MID
   } else if (RB == 1) {
     // measured (scripts/gemm_sweep.py, MI355X): one workgroup per CU wants 16 waves, a couple per
     // CU 8, many 4; 4 k-steps in flight per wave is the sweet spot everywhere on the hot path

@@ -146,7 +146,12 @@ class FreezeOmniEngine:
                 return False
             if it["feats"].shape[0] != R or (self.chat_template and it["status"] == "ipu_sl"):
                 return False
-        return ident in ("user", "system")
+        if ident not in ("user", "system"):
+            return False
+        # the captured step gives each session one 16-row attention work item (framing B's 4 LLM
+        # tokens x 7 query heads per kv head do not fit: those chunks run eagerly)
+        To = self.ada[ident].out_len(self.enc[ident].dims(R)[2])
+        return To * (self.llm.H // self.llm.KVH) <= 16
 
     def _listen_graph_for(self, items, slots=1, extra=64):
         ident = items[0]["identity"]
@@ -330,7 +335,9 @@ class ListenGraph:
         self.probs_host = torch.empty(B, 3, dtype=F32).pin_memory()
         self.main = ops.engine_stream(dev)
         self.side = ops.engine_stream(dev, side=True) if slots > 1 else self.main
-        self.enc_exec = [self._capture(self.main, lambda k=k: self._enc_body(k)) for k in range(slots)]
+        # the encoder stage is captured on the stream it replays on, so its split-K scratch (ops.Runtime)
+        # is not the LLM stage's while the two overlap
+        self.enc_exec = [self._capture(self.side, lambda k=k: self._enc_body(k)) for k in range(slots)]
         self.llm_exec = [self._capture(self.main, lambda k=k: self._llm_body(k)) for k in range(slots)]
         self.ev_enc = [self._event() for _ in range(slots)]
         self.ev_llm = [self._event() for _ in range(slots)]

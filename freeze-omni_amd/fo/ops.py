@@ -41,7 +41,9 @@ def engine_stream(device, side=False):
 
 
 class Runtime:
-    """Per-device scratch shared by all kernels of one replica (single stream discipline)."""
+    """Scratch (split-K slabs, counters) of the kernels issued on one stream of one device.  Keyed by
+    (device, current stream): work on two streams may overlap (the pipelined listen stages), so each
+    stream owns its scratch, and a graph's scratch is that of the stream it was captured on."""
 
     _inst = {}
 
@@ -53,9 +55,10 @@ class Runtime:
     @classmethod
     def get(cls, device):
         d = torch.device(device)
-        key = (d.type, d.index if d.index is not None else torch.cuda.current_device())
+        idx = d.index if d.index is not None else torch.cuda.current_device()
+        key = (d.type, idx, torch.cuda.current_stream(idx).cuda_stream)
         if key not in cls._inst:
-            cls._inst[key] = Runtime(torch.device("cuda", key[1]))
+            cls._inst[key] = Runtime(torch.device("cuda", idx))
         return cls._inst[key]
 
 

@@ -83,6 +83,32 @@ def test_gemm_fp32_activations_split(dev, M, N, K):
     assert err < 2e-4 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("M", [17, 40, 56, 64])
+@pytest.mark.parametrize("N,K,sw", [(3584, 3584, False), (3584, 18944, False), (4096, 3584, True)])
+def test_gemm_mid_rows(dev, M, N, K, sw):
+    """17..64 fp32 rows on Qwen2-sized weights (the turn's prefills): one row tile of ceil(M/16) row
+    blocks, K split for narrow layers; vs an fp64 reference (hi/lo split accuracy)."""
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M * 31 + N + K)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g)
+    if sw:
+        u = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+        lin = PackedLinear(w.to(dev), swiglu_up=u.to(dev))
+        y = lin(x.to(dev)).cpu().double()
+        ref = torch.nn.functional.silu(x.double() @ w.double().t()) * (x.double() @ u.double().t())
+    else:
+        b = torch.randn(N, generator=g)
+        r = torch.randn(M, N, generator=g)
+        lin = PackedLinear(w.to(dev), b.to(dev))
+        out = r.clone().to(dev)
+        lin(x.to(dev), out=out, residual=True)
+        y = out.cpu().double()
+        ref = x.double() @ w.double().t() + b.double() + r.double()
+    err = (y - ref).abs().max().item()
+    assert err < 2e-4 * ref.abs().max().item(), err
+
+
 def test_gemm_deterministic_splitk(dev):
     from fo.ops import PackedLinear
     g = torch.Generator().manual_seed(3)
@@ -100,7 +126,8 @@ def test_gemm_deterministic_splitk(dev):
 @pytest.mark.parametrize("M,H,KVH,hd,K,splitk", [(1, 28, 4, 128, 3584, 0), (16, 28, 4, 128, 3584, 0),
                                                  (16, 28, 4, 128, 3584, 3), (40, 4, 2, 32, 128, 0),
                                                  (70, 14, 14, 64, 896, 0), (8, 14, 14, 64, 896, 2),
-                                                 (24, 4, 4, 32, 128, 0)])
+                                                 (24, 4, 4, 32, 128, 0), (40, 28, 4, 128, 3584, 0),
+                                                 (56, 28, 4, 128, 3584, 0)])
 def test_gemm_qkv_rope(dev, M, H, KVH, hd, K, splitk):
     """Fused q|k|v projection + bias + rotate_half RoPE + paged-KV append vs an fp32 torch reference."""
     from fo.ops import PackedLinear

@@ -70,6 +70,12 @@ def test_byte_fallback_tokenizer_roundtrip_and_chat_specials():
     assert t.decode(ids) == "<|im_start|>system\nYou are 你好.<|im_end|>"
     assert t(["<|im_end|>"])["input_ids"][0][0] == 151645
     assert all(i < 152064 for i in ids)
+    # the chat template encodes to Qwen2-7B-Instruct's own ids (and lengths): the benchmark's prefills
+    # have the real prompt sizes
+    tpl = "<|im_start|>system\nYou are a helpful assistant.<|im_end|>\n<|im_start|>user\n"
+    assert t.encode(tpl) == [151644, 8948, 198, 2610, 525, 264, 10950, 17847, 13, 151645, 198, 151644, 872, 198]
+    assert t.encode("<|im_end|>\n<|im_start|>assistant\n") == [151645, 198, 151644, 77091, 198]
+    assert t.decode(t.encode(tpl)) == tpl
 
 
 def test_tiny_tokenizer_chat_template_ids_match_reference():
