@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="listen chunk by chunk (default: encoder stage of chunk c+1 overlaps the LLM of chunk c)")
+    ap.add_argument("--scenario", default="turn", choices=["turn", "duplex"],
+                    help="turn: config 3 (default, the headline line); duplex: config 5 sessions")
+    ap.add_argument("--duplex-sec", type=float, default=60.0, help="duplex: seconds of audio per session")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
@@ -296,6 +299,117 @@ def gemm_probe(engine, M, reps=2):
     return {"bytes": algo, "seconds": t, "gbps": algo / t / 1e9, "launches": n}
 
 
+def duplex_plan(seconds, offset, speech=3.0, silence=1.5, answer=3.75):
+    """SURVEY §8(d) config 5 script for one session: the user talks `speech` s, pauses `silence` s, ...;
+    the system answers `answer` s from the end of each user IPU, so the user's next IPU barges in at
+    silence / answer = 40 % of the answer."""
+    user, system = [], []
+    t = 0.5 + offset
+    while t < seconds:
+        user.append((t, t + speech))
+        system.append((t + speech, t + speech + answer))
+        t += speech + silence
+    return user, system
+
+
+def run_duplex(eng, args, seconds, sync):
+    """Config 5 on one replica: args.users duplex sessions (framing B, 224 ms chunks) with scripted VAD,
+    system audio re-encoded and prefilled, user barge-in; all sessions' chunks per tick in one batched
+    prefill (fo.duplex.DuplexScheduler).  Returns per-tick wall times and counts."""
+    from fo.duplex import DuplexScheduler, DuplexSession, ScriptedVAD
+    from models.pipeline import inferencePipeline
+    pipe = inferencePipeline.from_engine(eng)
+    ch = 3584
+    n = int(seconds * 16000 / ch)
+    sch = DuplexScheduler(pipe)
+    chunks = []   # [session][k] -> {identity: s16le bytes}
+    for u in range(args.users):
+        up, sp = duplex_plan(seconds, 0.224 * u)
+        sch.add(DuplexSession(pipe, sid=u, vad={"user": ScriptedVAD(ch, up), "system": ScriptedVAD(ch, sp)}))
+        pcm = {"user": synth_pcm(n * ch, 4321 + u), "system": synth_pcm(n * ch, 8765 + u)}
+        chunks.append([{i: np.round(pcm[i][k * ch:(k + 1) * ch] * 32767).astype(np.int16).tobytes()
+                        for i in ("user", "system")} for k in range(n)])
+    sync()
+    ticks, counts = [], {"user": 0, "system": 0, "dialog_ss": 0}
+
+    def account(done):
+        for _, d, st in done:
+            counts[d["identity"]] += 1
+            counts["dialog_ss"] += st == "dialog_ss"
+
+    t_all = time.perf_counter()
+    for k in range(n):
+        # chunk k of both parties arrives for every session; the tick that follows carries the VAD,
+        # fbank, gating, serialisation and the batched prefill + state decision (read on the host)
+        t = time.perf_counter()
+        for u, s in enumerate(sch.sessions):
+            for ident in ("user", "system"):
+                s.enqueue_audio_data(ident, {"audio": chunks[u][k][ident], "sr": 16000, "enc": "s16le",
+                                             "time_stamp": k * ch / 16000.0})
+        done = sch.tick()
+        ticks.append(time.perf_counter() - t)
+        account(done)
+    while True:   # features still queued behind the last chunk
+        done = sch.tick()
+        if not done:
+            break
+        account(done)
+    sync()
+    wall = time.perf_counter() - t_all
+    for s in sch.sessions:
+        s.release()
+    return {"wall": wall, "ticks": ticks, "counts": counts, "audio_s": args.users * n * ch / 16000.0}
+
+
+def main_duplex(args, eng, dev, dist, world, rank, load_s):
+    import torch
+
+    def sync():
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        run_duplex(eng, args, 6.0, sync)
+    if dist is not None:
+        dist.barrier()
+    runs = [run_duplex(eng, args, args.duplex_sec, sync) for _ in range(args.steps)]
+    wall = sum(r["wall"] for r in runs)
+    audio = sum(r["audio_s"] for r in runs)
+    ticks = [t * 1e3 for r in runs for t in r["ticks"]]
+    if dist is not None:
+        t = torch.tensor([wall, audio], dtype=torch.float64, device=dev)
+        allw = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allw, t)
+        wall = max(float(x[0]) for x in allw)
+        audio = sum(float(x[1]) for x in allw)
+        ticks = gather_list(dist, ticks, world, dev)
+    if rank == 0:
+        c = runs[-1]["counts"]
+        line = {
+            "metric": "duplex: real-time factor of two-party dialogue audio processed + p50 state-decision latency",
+            "value": round(audio / wall, 3),
+            "unit": "x real-time (seconds of per-session dialogue per wall second, all sessions)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16w-fp32a",
+            "data": "synthetic (counter-hash weights; synthetic 16 kHz PCM for both parties; scripted VAD)",
+            "config": {"workload": f"config 5: {args.users} duplex sessions/GPU x {args.duplex_sec:.0f} s, framing B "
+                                   "(224 ms chunks), user 3.0 s speech / 1.5 s pause, system answers 3.75 s, barge-in "
+                                   "at 40 %", "users_per_gpu": args.users, "global_users": args.users * world,
+                       "parallelism": f"dp{world} (session-pinned replicas)"},
+            "p50_decision_ms": round(float(np.percentile(ticks, 50)), 2) if ticks else None,
+            "p90_decision_ms": round(float(np.percentile(ticks, 90)), 2) if ticks else None,
+            "chunk_period_ms": 224.0,
+            "ticks": len(runs[-1]["ticks"]), "user_chunks": c["user"], "system_chunks": c["system"],
+            "dialog_ss": c["dialog_ss"], "load_s": round(load_s, 2),
+            "roofline": None, "cpu_baseline": None,
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+
+
 def main():
     args = parse()
     import torch
@@ -324,6 +438,12 @@ def main():
         bcast_n, bcast_bytes = broadcast_frozen(eng, dist)
         torch.cuda.synchronize()
         bcast_s = time.perf_counter() - tb
+
+    if args.scenario == "duplex":
+        main_duplex(args, eng, dev, dist, world, rank, load_s)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     def sync():
         torch.cuda.synchronize()

@@ -17,10 +17,14 @@ class ContextSerializer:
         self.user_in_actual_ipu = False
         self.system_in_pseudo_ipu = False
         self.feature_queue = []
+        self._seq = 0
 
     def add_feature_chunk(self, feature_chunk):
+        # heap key (timestamp, identity, status) as the reference's tuple; an arrival counter breaks the
+        # remaining ties so feature payloads (device tensors here) are never compared
         entry = (feature_chunk.get("time_stamp"), feature_chunk.get("identity"), feature_chunk.get("status"),
-                 feature_chunk.get("feature"), feature_chunk.get("ipu_id"))
+                 self._seq, feature_chunk.get("feature"), feature_chunk.get("ipu_id"))
+        self._seq += 1
         heapq.heappush(self.feature_queue, entry)
 
     def gate_feature(self, identity, status):
@@ -40,7 +44,7 @@ class ContextSerializer:
     def get_next_feature(self):
         if not self.feature_queue:
             return None
-        ts, identity, status, feature, ipu_id = heapq.heappop(self.feature_queue)
+        ts, identity, status, _, feature, ipu_id = heapq.heappop(self.feature_queue)
         send, force_sl = self.gate_feature(identity, status)
         if not send:
             return None

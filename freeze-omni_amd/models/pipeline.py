@@ -39,6 +39,17 @@ class inferencePipeline:
         self.model.init_template_compilation()
         self.logger = None
 
+    @classmethod
+    def from_engine(cls, engine, top_k=1, top_p=0.0, temperature=1.0):
+        """A pipeline over an already loaded FreezeOmniEngine (replica-local serving, benchmarks)."""
+        self = cls.__new__(cls)
+        self.args = {"device": str(engine.device)}
+        self.device = engine.device
+        self.id = uuid.uuid4().hex[:22]
+        self.model = AudioLLM(engine, top_k=top_k, top_p=top_p, temperature=temperature)
+        self.logger = None
+        return self
+
     # ------------------------------------------------------------------ speech_dialogue
     def speech_dialogue(self, audio, identity=None, status=None, role=None, past_key_values=None,
                         adapter_cache=None, encoder_cache=None, pe_index=0, stat=None, **upstream):

@@ -1,0 +1,118 @@
+"""Duplex sessions on the device path (fo.duplex over models.pipeline, tiny config): the batched
+scheduler (one speech_dialogue_batch per tick for every session) gives each session the results of
+its own sequential llm_prefill loop (bin/dialog_state_pred.py:719-844), with user barge-in over
+system speech."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = os.path.join(ROOT, "configs", "tiny")
+
+
+@pytest.fixture(scope="module")
+def pipe(dev):
+    from models.pipeline import inferencePipeline
+    return inferencePipeline({"model_path": TINY, "llm_path": os.path.join(TINY, "llm"), "device": "cuda:0",
+                              "top_k": 1})
+
+
+def _pcm(n, seed):
+    rng = np.random.default_rng(seed)
+    w = np.convolve(rng.standard_normal(n + 64), np.hanning(33), mode="same")[:n]
+    t = np.arange(n) / 16000.0
+    return 0.1 * w / (np.abs(w).max() + 1e-9) * 0.5 * (1 + np.sin(2 * np.pi * 4 * t))
+
+
+PLANS = [([(0.3, 1.6), (2.6, 3.8)], [(1.8, 3.2)]),   # barge-in at 2.6 s into the system's answer
+         ([(0.0, 2.5)], [(2.7, 3.9)]),
+         ([(1.0, 1.7), (2.2, 3.0)], [(0.1, 0.9)])]
+
+
+def _run(pipe, batched, seconds=4.0):
+    from fo.duplex import DuplexScheduler, DuplexSession, ScriptedVAD
+    sess = []
+    for i, (u, s) in enumerate(PLANS):
+        ch = 3584
+        vad = {"user": ScriptedVAD(ch, u), "system": ScriptedVAD(ch, s)}
+        ds = DuplexSession(pipe, sid=i, vad=vad)
+        n = int(seconds * 16000 / ch)
+        pcm = {"user": _pcm(n * ch, 100 + i), "system": _pcm(n * ch, 200 + i)}
+        for k in range(n):
+            for ident in ("user", "system"):
+                x = (np.clip(pcm[ident][k * ch:(k + 1) * ch], -1, 1) * 32767).astype(np.int16)
+                ds.enqueue_audio_data(ident, {"audio": x.tobytes(), "sr": 16000, "enc": "s16le",
+                                              "time_stamp": k * ch / 16000})
+        sess.append(ds)
+    if batched:
+        sch = DuplexScheduler(pipe)
+        for s in sess:
+            sch.add(s)
+        sch.drain()
+    else:
+        for s in sess:
+            s.pump()
+            while (d := s.next_feature()) is not None:
+                s.llm_prefill(d)
+    out = [(list(s.states), s.past_key_values.get_seq_length(), s.caches["user"]["pe_index"]) for s in sess]
+    for s in sess:
+        s.release()
+    return out
+
+
+def test_dialog_state_params_api(dev):
+    """The reference class surface: DialogStateParams(sid, socketio, event_outlet, outlets) from the pool,
+    enqueue_audio_data / start_all_threads / reset_context / release; two sessions share one replica's
+    scheduler and pipeline."""
+    import copy
+    from bin.dialog_state_pred import DialogStateParams
+    from fo.duplex import DEFAULT_CONFIG, ScriptedVAD
+    cfg = copy.deepcopy(DEFAULT_CONFIG)
+    cfg.update(model_path=TINY, llm_path=os.path.join(TINY, "llm"), device="cuda:0")
+    DialogStateParams.DIALOG_STATE_PRED_CONFIGS = cfg
+    DialogStateParams.PIPELINE_POOL = None
+    events = []
+    sess = [DialogStateParams(f"sid{i}", None, events.append, [],
+                              vad={"user": ScriptedVAD(3584, [(0.2, 1.2)]), "system": ScriptedVAD(3584, [(1.3, 2.0)])})
+            for i in range(2)]
+    assert sess[0].pipeline_obj is sess[1].pipeline_obj and sess[0].pipeline_obj.user_count == 2
+    for s in sess:
+        s.start_all_threads()
+        s.reset_context()
+    assert sess[0].scheduler is sess[1].scheduler and len(sess[0].scheduler.sessions) == 2
+    pcm = (_pcm(9 * 3584, 7) * 32767).astype(np.int16)
+    for s in sess:
+        for k in range(9):
+            for ident in ("user", "system"):
+                s.enqueue_audio_data(ident, {"audio": pcm[k * 3584:(k + 1) * 3584].tobytes(), "sr": 16000,
+                                             "enc": "s16le", "time_stamp": k * 0.224})
+    n = sess[0].run_scheduler()
+    assert n > 0 and len(events) == 2                       # one user IPU opened per session
+    for s in sess:
+        idents = [x[0] for x in s.states]
+        assert idents[0] == "user" and "system" in idents
+        assert all(x[2] in ("dialog_ss", "dialog_cl") for x in s.states if x[0] == "user")
+    obj = sess[0].pipeline_obj
+    for s in sess:
+        s.release()
+    assert obj.user_count == 0
+    DialogStateParams.PIPELINE_POOL = None
+
+
+def test_duplex_scheduler_matches_per_session(pipe):
+    bat, seq = _run(pipe, True), _run(pipe, False)
+    n_sys = 0
+    for (sb, nb, pb), (ss, ns, ps) in zip(bat, seq):
+        assert nb == ns and pb == ps
+        assert [x[:2] for x in sb] == [x[:2] for x in ss]
+        n_sys += sum(1 for x in sb if x[0] == "system")
+        for (i1, _, st1, p1), (_, _, st2, p2) in zip(sb, ss):
+            if i1 == "user":
+                assert abs(p1["state_1"] - p2["state_1"]) < 1e-4 and abs(p1["state_2"] - p2["state_2"]) < 1e-4
+                if abs(p2["state_1"] - 0.5) > 1e-3:
+                    assert st1 == st2
+            else:
+                assert p1 is None and st1 is None
+    assert n_sys > 0   # system speech really went through the system encoder / prefill
