@@ -44,7 +44,7 @@ def silence_cut(buffer, syn, N, threshold, res):
 
 
 def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
-          max_tokens=1000, min_tokens=0, states_out=None, seed=0, graph=True, window=16):
+          max_tokens=1000, min_tokens=0, states_out=None, seed=0, graph=True, window=32):
     """items: list of (hidden [T1, D] device, prefix [T2, D] device or None).
     min_tokens > 0 masks EOS until that many tokens (benchmark policy).
     Yields (session index, pcm segment device 1-D) as segments become available; the per-session
@@ -196,7 +196,15 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
 
 
 def _vocode(engine, states, idx, up, pad, N, thr, res, final):
-    """One batched vocoder call for sessions idx (equal token counts share a launch)."""
+    """One batched vocoder call for sessions idx (equal token counts share a launch), on the engine's
+    side stream: the MFMA-bound vocoder overlaps the launch-bound AR decode steps already queued on
+    the engine stream instead of stalling them (the side stream is blocking w.r.t. the legacy default
+    stream, so callers reading the yielded PCM there are ordered after it)."""
+    with torch.cuda.stream(ops.engine_stream(engine.device, side=True)):
+        yield from _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final)
+
+
+def _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final):
     groups = {}
     for i in idx:
         groups.setdefault(len(states[i].tokens), []).append(i)
