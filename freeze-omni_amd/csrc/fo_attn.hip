@@ -10,8 +10,9 @@
 //    see keys at positions <= its own, full mode (the reference's eager attention with
 //    attention_mask=None / all-ones masks, decoder.py:140,175,302) sees the whole sequence.
 //    Work items group a sequence's batch tokens (x the GQA group of query heads sharing one kv
-//    head) so its keys are read once per kv head; split-KV over key ranges when the grid would
-//    otherwise not cover the chip, merged by a combine kernel.
+//    head) so its keys are read once per kv head; split-KV over key ranges sized from each item's
+//    own key count at run time, merged in the same launch by the last split to finish (or, without
+//    a ticket buffer, static splits merged by a combine kernel).
 // 2. Encoder rel-pos attention over a per-user ring buffer (models/encoder/attention.py:407-459):
 //    scores = ((q+u).K^T + (q+v).P^T)/sqrt(dk), no mask, no rel_shift; P rows come from a
 //    table of linear_pos(sinusoid(position)) precomputed at load for every position.
@@ -67,6 +68,11 @@ struct AttnArgs {
   float* out;      // [T][H*hd]
   int H, KVH, PS, maxb, nsplit;
   float scale;
+  // in-launch merge: a work item uses min(nsplit, ceil(keys / kps)) splits, chosen from its own key
+  // count at run time (one captured graph serves a context as it grows); the last split to finish
+  // (arrival ticket cnt[item][kv head], reset by that split) merges the partials -- no combine launch
+  int* cnt;        // nullable: static nsplit splits + k_attn_combine
+  int kps;
 };
 
 constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
@@ -92,6 +98,63 @@ __device__ __forceinline__ float row16_sum(float v) {
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Split `sp` of work item `it` has written its partial (part_o / part_ml): publish it and take an
+// arrival ticket; the split that draws ns - 1 merges all ns partials of the item's R rows with
+// k_attn_combine's arithmetic and resets the ticket for the next launch.  Protocol: every wave drains
+// its stores, lane 0 releases at agent scope before the relaxed ticket add, the merging split acquires
+// at agent scope before reading (correct for any placement of the splits over XCDs).
+// last_s / w_s: the kernel's existing LDS (no second __shared__ object for the flag).
+template <int HD>
+__device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns, int t0, int R, int G,
+                                      int& last_s, float* w_s) {
+  const int tid = threadIdx.x;
+  int* ticket = a.cnt + (size_t)it * a.KVH + kvh;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = old == ns - 1;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // per row: split weights exp(m_q - M) (0 for empty splits) and 1 / l into LDS (w_s: [16][KT + 4],
+  // the kernel's P tile, ns <= KT), then every (row, d) sums its ns partials with independent loads
+  for (int r = tid; r < R; r += blockDim.x) {
+    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+    const float* ml = a.part_ml + th * a.nsplit * 2;
+    float M = -INFINITY;
+    for (int q = 0; q < ns; ++q)
+      if (ml[2 * q + 1] > 0.f) M = fmaxf(M, ml[2 * q]);
+    float l = 0.f;
+    for (int q = 0; q < ns; ++q) {
+      const float ls = ml[2 * q + 1];
+      const float w = ls > 0.f ? expf(ml[2 * q] - M) : 0.f;
+      if (ls > 0.f) l += ls * w;
+      w_s[r * (KT + 4) + q] = w;
+    }
+    w_s[r * (KT + 4) + KT] = 1.f / l;
+  }
+  __syncthreads();
+  for (int e = tid; e < R * HD; e += blockDim.x) {
+    const int r = e / HD, d = e - (e / HD) * HD;
+    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+    const float* po = a.part_o + th * a.nsplit * HD + d;
+    const float* w = w_s + r * (KT + 4);
+    float o = 0.f;
+    for (int q = 0; q < ns; ++q)
+      if (w[q] != 0.f) o += po[(size_t)q * HD] * w[q];
+    a.out[th * HD + d] = o * w[KT];
+  }
 }
 
 // One work item = up to 16 query rows (a sequence's batch tokens x the GQA group sharing one kv head)
@@ -124,7 +187,12 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   const int grp = lane >> 4, col = lane & 15;
   int Lmax = 0;
   for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
-  const int per = ((Lmax + a.nsplit - 1) / a.nsplit + KT - 1) / KT * KT;
+  int ns = a.nsplit;
+  if (a.cnt) {
+    ns = min(ns, max(1, (Lmax + a.kps - 1) / a.kps));
+    if (sp >= ns) return;  // beyond this item's splits: never counted, never read
+  }
+  const int per = ((Lmax + ns - 1) / ns + KT - 1) / KT * KT;
   const int c0 = sp * per, c1 = min(Lmax, c0 + per);
   if (c0 >= c1) {  // empty split: neutral partial
     for (int r = tid; r < R; r += 256) {
@@ -132,6 +200,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
       a.part_ml[o * 2] = -INFINITY;
       a.part_ml[o * 2 + 1] = 0.f;
     }
+    if (a.cnt) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
     return;
   }
   const int* bt = a.block_table + (size_t)seq * a.maxb;
@@ -292,17 +361,18 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
       const int dt = wave + 4 * n;
       if (dt >= NTILE) continue;
       const int d = 16 * dt + col;
-      if (a.nsplit == 1) {
+      if (ns == 1) {
         a.out[th * HD + d] = acc[n][i] / l;
       } else {
         a.part_o[(th * a.nsplit + sp) * HD + d] = acc[n][i];
       }
     }
-    if (a.nsplit > 1 && wave == 0 && col == 0) {
+    if (ns > 1 && wave == 0 && col == 0) {
       a.part_ml[(th * a.nsplit + sp) * 2] = m_run[i];
       a.part_ml[(th * a.nsplit + sp) * 2 + 1] = l;
     }
   }
+  if (a.cnt && ns > 1) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
 }
 
 // merge split partials: grid (T, H)
@@ -529,21 +599,26 @@ int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, c
 
 // q [T][H*hd] -> out [T][H*hd].  items [n_items][3] (sequence, first token, tokens) with
 // tokens * (H/KVH) <= max_rows <= 64; part_ml >= T*H*nsplit*2 and part_o >= T*H*nsplit*hd floats
-// when nsplit > 1.
+// when nsplit > 1.  tickets (nullable): n_items*KVH zero-initialised ints; then each item takes
+// min(nsplit, ceil(keys / keys_per_split)) splits and the last one merges them in this launch (the
+// tickets are left zeroed); without tickets nsplit static splits are merged by a second launch.
 int fo_attention(const float* q, int T, const int* items, int n_items, int max_rows, const int* tok_nvis,
                  const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
-                 float scale, int nsplit, float* part_ml, float* part_o, float* out, hipStream_t s) {
+                 float scale, int nsplit, float* part_ml, float* part_o, float* out, int* tickets,
+                 int keys_per_split, hipStream_t s) {
   FO_REQUIRE(T > 0 && n_items > 0 && KVH > 0 && H % KVH == 0, "fo_attention: bad shape");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
   FO_REQUIRE(max_rows >= 1 && max_rows <= 16, "fo_attention: %d query rows per item (max 16)", max_rows);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
-  AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale};
+  FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
+  AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
+             tickets, keys_per_split};
   dim3 grid(n_items, KVH, nsplit);
   if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
   else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_attn_mfma<32>), grid, dim3(256), 0, s, a);
   int rc = fo::check_launch("fo_attention/rows");
-  if (rc || nsplit == 1) return rc;
+  if (rc || nsplit == 1 || tickets) return rc;
   hipLaunchKernelGGL(k_attn_combine, dim3(T, H), dim3(hd < 64 ? 64 : hd), 0, s, a, hd);
   return fo::check_launch("fo_attention/combine");
 }

@@ -73,7 +73,7 @@ _SIGS = {
     "fo_rope_kv_write": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_int, c_vp]),
     "fo_attention": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int,
-                             c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp]),
+                             c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "fo_enc_kv_write": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "fo_relpos_attention_fused": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_int, c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),

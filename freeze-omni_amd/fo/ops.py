@@ -354,11 +354,18 @@ def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS
               stream(qkv.device))
 
 
+ATTN_KEYS_PER_SPLIT = 256
+
+
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,
-              part_ml, part_o, out):
+              part_ml, part_o, out, tickets=None, keys_per_split=ATTN_KEYS_PER_SPLIT):
+    """tickets: zeroed int32 [>= n_items * KVH] -> splits sized from each item's key count (at most
+    nsplit) merged inside the launch; None -> nsplit static splits + a combine launch."""
+    if tickets is not None and tickets.numel() < n_items * KVH:
+        raise ValueError("attention tickets buffer smaller than n_items * KVH")
     _lib.call("fo_attention", q.data_ptr(), T, items.data_ptr(), n_items, max_rows, tok_nvis.data_ptr(),
               block_table.data_ptr(), block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd, float(scale),
-              nsplit, ptr(part_ml), ptr(part_o), out.data_ptr(), stream(q.device))
+              nsplit, ptr(part_ml), ptr(part_o), out.data_ptr(), ptr(tickets), int(keys_per_split), stream(q.device))
     return out
 
 

@@ -58,7 +58,8 @@ class DecoderStack:
               "m": torch.empty(T, self.layers[0].gu.N, dtype=F32, device=device),
               "nsplit": nsplit, "part_ml": None, "part_o": None,
               "sA": ops.RowStats(T, device), "sB": ops.RowStats(T, device),
-              "xg": torch.empty(T, self.D, dtype=F32, device=device)}
+              "xg": torch.empty(T, self.D, dtype=F32, device=device),
+              "tickets": torch.zeros(T * KVH, dtype=torch.int32, device=device)}
         if nsplit > 1:
             ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
@@ -93,7 +94,7 @@ class DecoderStack:
                 L.qkv.qkv_rope(xg, T, *rope, norm=(sA, self.eps))
             ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
                           self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
-                          att)
+                          att, tickets=ws["tickets"])
             L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))
             L.gu(xg, out=m, M=T, norm=(sB, self.eps))
             if i == last and final_norm is None:

@@ -133,7 +133,8 @@ int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, c
  * Split-KV (nsplit from fo_attn_nsplit) + combine. */
 int fo_attention(const float* q, int T, const int* items, int n_items, int max_rows, const int* tok_nvis,
                  const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
-                 float scale, int nsplit, float* part_ml, float* part_o, float* out, hipStream_t s);
+                 float scale, int nsplit, float* part_ml, float* part_o, float* out, int* tickets,
+                 int keys_per_split, hipStream_t s);
 /* encoder MultiHeadedAttention.infer left-chunk buffer as a ring + rel-pos scores
  * (models/encoder/attention.py:407-459) */
 int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,

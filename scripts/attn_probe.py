@@ -52,6 +52,16 @@ def main():
                     kv_bytes = 8 * (L + ntok) * KVH * hd * 4 * 2
                     print(f"H={H} KVH={KVH} hd={hd} L={L} ntok={ntok} nsplit={ns}: {us:7.2f} us  "
                           f"{kv_bytes / us / 1e3:7.1f} GB/s", flush=True)
+                tk = torch.zeros(meta.n_items * KVH, dtype=torch.int32, device=dev)
+                pm = torch.empty(T * H * 16 * 2, device=dev)
+                po = torch.empty(T * H * 16 * hd, device=dev)
+                for kps in (64, 128, 256, 512):
+                    us = timeit(lambda: ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis,
+                                                      meta.block_table, 16, pool.k[0], pool.v[0], H, KVH, hd,
+                                                      1 / math.sqrt(hd), 16, pm, po, out, tickets=tk,
+                                                      keys_per_split=kps))
+                    print(f"H={H} KVH={KVH} hd={hd} L={L} ntok={ntok} merged in-launch, keys/split {kps}: "
+                          f"{us:7.2f} us", flush=True)
                 for s in seqs:
                     s.free()
 

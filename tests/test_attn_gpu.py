@@ -31,8 +31,10 @@ def _reference(q, pool, seqs, meta_host, H, KVH, hd, scale):
 
 @pytest.mark.parametrize("H,KVH,hd", [(28, 4, 128), (14, 14, 64), (4, 2, 32)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("nsplit", [None, 1, 3])
-def test_attention_matches_reference(dev, H, KVH, hd, causal, nsplit):
+@pytest.mark.parametrize("nsplit,kps", [(None, 0), (1, 0), (3, 0), (8, 64), (16, 256), (2, 64)])
+def test_attention_matches_reference(dev, H, KVH, hd, causal, nsplit, kps):
+    """kps > 0: splits sized per item from its key count (<= nsplit), merged in the same launch by the
+    last split to arrive (tickets must come back zeroed for the next launch / graph replay)."""
     g = torch.Generator().manual_seed(H * 1000 + hd + causal)
     pool = KVPool(1, KVH, hd, 256, 16, dev)
     pool.k.copy_(torch.randn(pool.k.shape, generator=g))
@@ -56,7 +58,13 @@ def test_attention_matches_reference(dev, H, KVH, hd, causal, nsplit):
     part_o = torch.empty(T * H * ns * hd, device=dev) if ns > 1 else None
     out = torch.empty(T, H * hd, device=dev)
     scale = 1 / math.sqrt(hd)
-    ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0],
-                  pool.v[0], H, KVH, hd, scale, ns, part_ml, part_o, out)
+    tickets = torch.zeros(meta.n_items * KVH, dtype=torch.int32, device=dev) if kps else None
     ref = _reference(q, pool, seqs, host, H, KVH, hd, scale)
-    torch.testing.assert_close(out.cpu().double(), ref, atol=2e-5, rtol=1e-4)
+    for _ in range(2 if kps else 1):  # twice: the second launch starts from the tickets the first left
+        out.fill_(float("nan"))
+        ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS,
+                      pool.k[0], pool.v[0], H, KVH, hd, scale, ns, part_ml, part_o, out, tickets=tickets,
+                      keys_per_split=kps or 256)
+        torch.testing.assert_close(out.cpu().double(), ref, atol=2e-5, rtol=1e-4)
+        if kps:
+            assert int(tickets.abs().sum()) == 0
