@@ -20,8 +20,10 @@ class Layer:
 
 
 class DecoderStack:
-    def __init__(self, src, prefix, n_layers, D, H, KVH, eps, bias, rope, pool, kv_layer0=0, first_fp16=False):
+    def __init__(self, src, prefix, n_layers, D, H, KVH, eps, bias, rope, pool, kv_layer0=0, first_fp16=False,
+                 attn_keys_per_split=ops.ATTN_KEYS_PER_SPLIT):
         self.n, self.D, self.H, self.KVH, self.hd, self.eps = n_layers, D, H, KVH, D // H, eps
+        self.attn_kps = attn_keys_per_split
         self.cos, self.sin = rope
         self.pool, self.kv_layer0, self.first_fp16 = pool, kv_layer0, first_fp16
         self.layers = []
@@ -94,7 +96,7 @@ class DecoderStack:
                 L.qkv.qkv_rope(xg, T, *rope, norm=(sA, self.eps))
             ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
                           self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
-                          att, tickets=ws["tickets"])
+                          att, tickets=ws["tickets"], keys_per_split=self.attn_kps)
             L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))
             L.gu(xg, out=m, M=T, norm=(sB, self.eps))
             if i == last and final_norm is None:
