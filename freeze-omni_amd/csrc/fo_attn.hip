@@ -375,6 +375,93 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   if (a.cnt && ns > 1) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
 }
 
+// Single-row decode attention (the AR speech decoder's step, models/decoder/decoder.py:341-349: one
+// token per session, one query head per kv head): one work group per (session, head) reads the
+// session's keys once, in fp32 -- scores one key per thread (16-B loads of the key row), block
+// max / sum, then P.V with the waves on interleaved keys, a float4 of the row per lane.  No MFMA tile would be
+// more than 1/16 full here, and no split / merge round trip is needed at <= 4096 keys.
+constexpr int DEC_MAXK = MAXPG * 16;
+constexpr int DEC_NW = 8, DEC_NT = DEC_NW * 64;  // 8 waves: a key per thread up to 512 keys
+template <int HD>
+__global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
+  static_assert(HD % 4 == 0 && HD <= 128, "decode attention: head_dim");
+  __shared__ float s_s[DEC_MAXK];
+  __shared__ float q_s[HD];
+  __shared__ float acc_s[DEC_NW][HD];
+  __shared__ float red_s[DEC_NW];
+  __shared__ int pg_s[MAXPG];
+  const int it = blockIdx.x, h = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int seq = a.items[3 * it], t0 = a.items[3 * it + 1];
+  const int L = a.tok_nvis[t0];
+  float* orow = a.out + ((size_t)t0 * a.H + h) * HD;
+  if (L > DEC_MAXK || (L + a.PS - 1) / a.PS > MAXPG) {  // host contract broken: poison, never read wrong keys
+    if (tid < HD) orow[tid] = NAN;
+    return;
+  }
+  const int* bt = a.block_table + (size_t)seq * a.maxb;
+  for (int i = tid; i < (L + a.PS - 1) / a.PS; i += DEC_NT) pg_s[i] = bt[i];
+  const float* qr = a.q + ((size_t)t0 * a.H + h) * HD;
+  for (int d = tid; d < HD; d += DEC_NT) q_s[d] = qr[d] * a.scale;
+  __syncthreads();
+  const size_t page_sz = (size_t)a.KVH * a.PS * HD, head_off = (size_t)h * a.PS * HD;
+  float mx = -INFINITY;
+  for (int j = tid; j < L; j += DEC_NT) {
+    const float* kr = a.kc + (size_t)pg_s[j / a.PS] * page_sz + head_off + (size_t)(j % a.PS) * HD;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; d += 4) {
+      const float4 k4 = *reinterpret_cast<const float4*>(kr + d);
+      s += q_s[d] * k4.x + q_s[d + 1] * k4.y + q_s[d + 2] * k4.z + q_s[d + 3] * k4.w;
+    }
+    s_s[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red_s[wave] = mx;
+  __syncthreads();
+  mx = red_s[0];
+#pragma unroll
+  for (int w = 1; w < DEC_NW; ++w) mx = fmaxf(mx, red_s[w]);
+  float sum = 0.f;
+  for (int j = tid; j < L; j += DEC_NT) {
+    const float p = expf(s_s[j] - mx);
+    s_s[j] = p;
+    sum += p;
+  }
+  sum = block_sum<DEC_NW>(sum, red_s);  // its barriers also publish s_s
+  // P.V: HD/4 lanes per key (one float4 of the V row each), 64/(HD/4) keys per wave-instruction, the 4
+  // waves on interleaved keys; 8 keys per lane in flight
+  constexpr int LPK = HD / 4, KPW = 64 / LPK;
+  const int sub = lane / LPK, l4 = lane % LPK;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int j = wave * KPW + sub; j < L; j += DEC_NW * KPW) {
+    const float p = s_s[j];
+    const float4 v = *reinterpret_cast<const float4*>(a.vc + (size_t)pg_s[j / a.PS] * page_sz + head_off +
+                                                      (size_t)(j % a.PS) * HD + 4 * l4);
+    acc.x += p * v.x;
+    acc.y += p * v.y;
+    acc.z += p * v.z;
+    acc.w += p * v.w;
+  }
+#pragma unroll
+  for (int o = LPK; o < 64; o <<= 1) {
+    acc.x += __shfl_xor(acc.x, o, 64);
+    acc.y += __shfl_xor(acc.y, o, 64);
+    acc.z += __shfl_xor(acc.z, o, 64);
+    acc.w += __shfl_xor(acc.w, o, 64);
+  }
+  if (sub == 0) *reinterpret_cast<float4*>(&acc_s[wave][4 * l4]) = acc;
+  __syncthreads();
+  for (int d = tid; d < HD; d += DEC_NT) {
+    float o = 0.f;
+#pragma unroll
+    for (int w = 0; w < DEC_NW; ++w) o += acc_s[w][d];
+    orow[d] = o / sum;
+  }
+}
+
 // merge split partials: grid (T, H)
 __global__ void k_attn_combine(AttnArgs a, int hd) {
   const int t = blockIdx.x, h = blockIdx.y;
@@ -613,6 +700,13 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
              tickets, keys_per_split};
+  if (max_rows == 1 && (long long)maxb * PS <= DEC_MAXK) {  // one query row per (session, head): decode kernel
+    dim3 g1(n_items, H);
+    if (hd == 128) hipLaunchKernelGGL((k_attn_decode<128>), g1, dim3(DEC_NT), 0, s, a);
+    else if (hd == 64) hipLaunchKernelGGL((k_attn_decode<64>), g1, dim3(DEC_NT), 0, s, a);
+    else hipLaunchKernelGGL((k_attn_decode<32>), g1, dim3(DEC_NT), 0, s, a);
+    return fo::check_launch("fo_attention/decode");
+  }
   dim3 grid(n_items, KVH, nsplit);
   if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
   else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);

@@ -68,3 +68,30 @@ def test_attention_matches_reference(dev, H, KVH, hd, causal, nsplit, kps):
         torch.testing.assert_close(out.cpu().double(), ref, atol=2e-5, rtol=1e-4)
         if kps:
             assert int(tickets.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("hd", [64, 128, 32])
+def test_single_row_decode_attention(dev, hd):
+    """One token per session with one query head per kv head (the AR speech decoder step) takes the
+    decode kernel (fp32, one work group per session x head): vs float64, keys across page boundaries."""
+    H = KVH = 14 if hd == 64 else 4
+    g = torch.Generator().manual_seed(hd)
+    pool = KVPool(1, KVH, hd, 256, 16, dev)
+    pool.k.copy_(torch.randn(pool.k.shape, generator=g))
+    pool.v.copy_(torch.randn(pool.v.shape, generator=g))
+    seqs = [KVSeq(pool) for _ in range(5)]
+    for s, n in zip(seqs, [1, 15, 16, 333, 1200]):
+        BatchMeta([(s, n, 0, True)], dev)
+    meta = BatchMeta([(s, 1, s.length, False) for s in seqs], dev, gqa=1)
+    assert meta.max_rows == 1
+    T = meta.T
+    q = torch.randn(T, H * hd, generator=g).to(dev)
+    nvis = meta.tok_nvis.cpu().tolist()
+    host = [(meta.tok_seq.cpu()[t].item(), nvis[t]) for t in range(T)]
+    out = torch.full((T, H * hd), float("nan"), device=dev)
+    scale = 1 / math.sqrt(hd)
+    ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0],
+                  pool.v[0], H, KVH, hd, scale, 1, None, None, out)
+    ref = _reference(q, pool, seqs, host, H, KVH, hd, scale)
+    torch.testing.assert_close(out.cpu().double(), ref, atol=1e-5, rtol=1e-5)
+
