@@ -596,11 +596,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   if (mid) {
     NT = a.ntiles % 4 == 0 ? 4 : 2;
   } else if (RB == 1) {
-    // measured policy (gemm_sweep.py): wide layers (>= 1024 tiles: Qwen2 gate/up, lm_head) take 4
+    // measured policy (gemm_sweep.py, gemm_graph_sweep.py): wide layers (>= 1024 tiles: Qwen2 gate/up, lm_head) take 4
     // tiles per workgroup; long-K layers (Qwen2 down) 4 tiles and a 4-way K split; mid-size grids
     // (> 256 tiles: Qwen2 qkv) 2 tiles; small ones 1
     if (a.ntiles >= 1024) NT = 4;
     else if (KS >= 256 && a.ntiles >= 128) { NT = 4; S_auto = 4; }
+    else if (KS >= 128 && a.ntiles <= 64) S_auto = 4;  // narrow long-K (TTS down): 10.9 -> 8.2 us in a graph
     else if (a.ntiles > 256) NT = 2;
     if (g_force_nt) NT = g_force_nt;
     FO_REQUIRE(NT == 1 || NT == 2 || NT == 4, "fo_gemm: tiles per workgroup %d", NT);
