@@ -585,7 +585,10 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   // chunk with its chat prefix, the system prompt; 17..64 rows): one row tile of ceil(M/16) row blocks
   // against 4-tile column groups, so X (fp32, re-read by every column group) costs about what the
   // weights do, and no grid of 64-row tiles streams X four times per weight byte
-  const bool mid = x_f32 && !lnw && M > 16 && M <= 64 && (long long)a.ntiles * 16 * K >= (8ll << 20);
+  // (small weights with 33..64 rows -- the duplex encoder at 8 sessions x 7 frames -- take the same
+  // one-row-tile kernels with single-tile column groups instead of 64-row tiles on 64 workgroups)
+  const bool big_w = (long long)a.ntiles * 16 * K >= (8ll << 20);
+  const bool mid = x_f32 && !lnw && M > 16 && M <= 64 && (big_w || M > 32);
   const int RB = mid ? (M + 15) / 16 : (M <= 16 ? 1 : (M <= 32 ? 2 : 4));
   const int mt = (M + RB * 16 - 1) / (RB * 16);
   // tiles per workgroup: the activation rows are re-read by every workgroup, so workgroups that
@@ -594,7 +597,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   int S_auto = 0;
   const int KS = K >> 5;
   if (mid) {
-    NT = a.ntiles % 4 == 0 ? 4 : 2;
+    NT = big_w ? (a.ntiles % 4 == 0 ? 4 : 2) : (swiglu ? 2 : 1);
   } else if (RB == 1) {
     // measured policy (gemm_sweep.py, gemm_graph_sweep.py): wide layers (>= 1024 tiles: Qwen2 gate/up, lm_head) take 4
     // tiles per workgroup; long-K layers (Qwen2 down) 4 tiles and a 4-way K split; mid-size grids
@@ -660,6 +663,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
 #define FO_MID_RB(NT_, NW_, SW_) { if (RB == 2) FO_MID(NT_, 2, NW_, SW_); else if (RB == 3) FO_MID(NT_, 3, NW_, SW_); else FO_MID(NT_, 4, NW_, SW_); }
     if (swiglu) {
       if (NT == 4) FO_MID_RB(4, 4, true) else if (nw == 4) FO_MID_RB(2, 4, true) else FO_MID_RB(2, 8, true)
+    } else if (NT == 1) {
+      if (nw == 4) FO_MID_RB(1, 4, false) else FO_MID_RB(1, 8, false)
     } else {
       if (NT == 4) FO_MID_RB(4, 4, false) else if (nw == 4) FO_MID_RB(2, 4, false) else FO_MID_RB(2, 8, false)
     }

@@ -42,7 +42,14 @@ def graph_time(fn, reps):
     return ms.value / reps * 1e3
 
 
-shapes = [("tts_qkv", 2688, 896, 8, False), ("tts_o", 896, 896, 8, False), ("tts_gu", 4864, 896, 8, True),
+if len(sys.argv) > 1 and sys.argv[1] == "mid":   # duplex: 8 sessions x 7 encoder frames / x 4(+5) LLM rows
+    shapes = [("enc_qkv56", 3072, 1024, 56, False), ("enc_o56", 1024, 1024, 56, False),
+              ("enc_ff1_56", 4096, 1024, 56, False), ("enc_ff2_56", 1024, 4096, 56, False),
+              ("qwen_gu32", 18944, 3584, 32, True), ("qwen_gu48", 18944, 3584, 48, True),
+              ("qwen_down32", 3584, 18944, 32, False), ("qwen_qkv32", 4608, 3584, 32, False)]
+else:
+    shapes = None
+shapes = shapes or [("tts_qkv", 2688, 896, 8, False), ("tts_o", 896, 896, 8, False), ("tts_gu", 4864, 896, 8, True),
           ("tts_down", 896, 4864, 8, False), ("tts_out", 1028, 896, 8, False),
           ("qwen_qkv", 4608, 3584, 16, False), ("qwen_o", 3584, 3584, 16, False),
           ("qwen_down", 3584, 18944, 16, False), ("qwen_gu", 18944, 3584, 16, True)]

@@ -84,7 +84,8 @@ def test_gemm_fp32_activations_split(dev, M, N, K):
 
 
 @pytest.mark.parametrize("M", [17, 40, 56, 64])
-@pytest.mark.parametrize("N,K,sw", [(3584, 3584, False), (3584, 18944, False), (4096, 3584, True)])
+@pytest.mark.parametrize("N,K,sw", [(3584, 3584, False), (3584, 18944, False), (4096, 3584, True), (1024, 4096, False),
+                                    (3072, 1024, False)])
 def test_gemm_mid_rows(dev, M, N, K, sw):
     """17..64 fp32 rows on Qwen2-sized weights (the turn's prefills): one row tile of ceil(M/16) row
     blocks, K split for narrow layers; vs an fp64 reference (hi/lo split accuracy)."""
