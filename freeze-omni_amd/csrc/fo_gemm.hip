@@ -305,7 +305,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
     red[0][t][rr][c] = v;
   }
-  if (a.rstats && !LN) {
+  if (a.rstats && !LN && a.S == 1) {  // (split over K: k_gemm_reduce scales the summed partials)
     if (!RPRE) load_rpart();
     __shared__ float rstd_s[ROWS];
 #pragma unroll
@@ -381,6 +381,17 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
   const int m = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  float rs = 1.f;
+  if (a.rstats && !a.lnw) {  // RMSNorm consumer split over K: the row's rstd scales the summed partials
+    if (threadIdx.x == 0) {
+      float ss = 0.f;
+      for (int j = 0; j < a.rgroups; ++j) ss += a.rstats[(size_t)m * a.rgroups + j];
+      red_s[0] = rsqrtf(ss / (float)a.K + a.reps);
+    }
+    __syncthreads();
+    rs = red_s[0];
+    __syncthreads();
+  }
   if (a.rq) {  // rope: one thread per column pair, packed tiles (2P, 2P + 1)
     if (n < a.N / 2) {
       const int P = n >> 4, c = n & 15;
@@ -390,7 +401,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
         x1 += p[0];
         x2 += p[16];
       }
-      rope_store(a, m, rope_col(a, P, c), x1, x2);
+      rope_store(a, m, rope_col(a, P, c), x1 * rs, x2 * rs);
     }
     return;
   }
@@ -403,7 +414,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       v += p[0];
       if (sw) u += p[16];
     }
-    y = epilogue_store(a, sw != 0, m, n, v, u);
+    y = epilogue_store(a, sw != 0, m, n, v * rs, u * rs);
   }
   if (a.sout && !sw) {
     const float ss = block_sum<4>(n < a.N ? y * y : 0.f, red_s);
@@ -627,13 +638,13 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   if (rope) NT = 2;  // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds
   if (lnw && NT > 2) NT = 2;
   const int groups = a.ntiles / NT;
-  if (mid && !rstats) {  // narrow layers (Qwen2 q|k|v, o, down): split K until the grid covers the chip
-    S_auto = groups >= 192 ? 1 : (256 + groups - 1) / groups;
+  if (mid) {  // split K: 2 ways on wide layers (Qwen2 gate/up), until the grid covers the chip on narrow ones
+    S_auto = groups >= 192 ? (big_w ? 2 : 1) : (256 + groups - 1) / groups;
     if (S_auto > 4) S_auto = 4;
     if (S_auto > KS / 16) S_auto = KS / 16 > 0 ? KS / 16 : 1;
   }
   int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : (mid ? 1 : fo_gemm_pick_split(M, groups, K)));
-  if (rstats && !lnw) S = 1;  // the rstd scale is applied before the epilogue of a single-pass GEMM
+  if (rstats && !lnw && !mid) S = 1;  // (split RMSNorm consumers: k_gemm_reduce applies the rstd)
   if (S > (K >> 5)) S = K >> 5;
   a.S = S;
   if (S > 1) {

@@ -110,6 +110,37 @@ def test_gemm_mid_rows(dev, M, N, K, sw):
     assert err < 2e-4 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("M", [8, 16, 40, 56])
+@pytest.mark.parametrize("sw", [False, True])
+def test_gemm_rmsnorm_across_gemms(dev, M, sw):
+    """RMSNorm fused across two GEMMs (RowStats): the producer (+residual) writes y * gamma and row
+    partial sums, the consumer scales rows by rstd -- single pass or split over K (mid rows: the reduce
+    launch applies rstd); vs fp64 residual -> RMSNorm -> projection."""
+    from fo import ops
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M * 5 + sw)
+    D, N = 3584, 4096 if sw else 4608
+    wp = (torch.randn(D, 1024, generator=g) / 32).to(torch.bfloat16)
+    wc = (torch.randn(N, D, generator=g) / D ** 0.5).to(torch.bfloat16)
+    wu = (torch.randn(N, D, generator=g) / D ** 0.5).to(torch.bfloat16)
+    gamma = torch.rand(D, generator=g) + 0.5
+    xin = torch.randn(M, 1024, generator=g)
+    res = torch.randn(M, D, generator=g)
+    prod = PackedLinear(wp.to(dev))
+    cons = PackedLinear(wc.to(dev), swiglu_up=wu.to(dev)) if sw else PackedLinear(wc.to(dev))
+    st = ops.RowStats(M, dev)
+    x = res.clone().to(dev)
+    yg = torch.empty(M, D, device=dev)
+    prod(xin.to(dev), out=x, residual=True, stats_out=st.set(gamma.to(dev), yg))
+    out = cons(yg, norm=(st, 1e-6))
+    y = res.double() + xin.double() @ wp.double().t()
+    h = y * torch.rsqrt((y * y).mean(-1, keepdim=True) + 1e-6) * gamma.double()
+    ref = torch.nn.functional.silu(h @ wc.double().t()) * (h @ wu.double().t()) if sw else h @ wc.double().t()
+    torch.testing.assert_close(x.cpu().double(), y, rtol=1e-5, atol=1e-4)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err < 2e-4 * ref.abs().max().item(), err
+
+
 def test_gemm_deterministic_splitk(dev):
     from fo.ops import PackedLinear
     g = torch.Generator().manual_seed(3)
