@@ -85,6 +85,8 @@ def run_turn(engine, base_kv, pcms, args, sync):
     CH = turns[0].framer.chunk
     n_chunks = int(math.ceil(len(pcms[0]) / CH))
     pipe = engine.listen_pipe() if args.pipeline else None
+    from fo import ops
+    side = ops.engine_stream(engine.device, side=True)
     for c in range(n_chunks):
         wins, firsts = [], []
         for t in turns:
@@ -94,7 +96,11 @@ def run_turn(engine, base_kv, pcms, args, sync):
             w, f = t.framer.push(seg)
             wins.append(w)
             firsts.append(f)
-        feats = fb(np.stack(wins), firsts)
+        if pipe is not None and c > 0:
+            with torch.cuda.stream(side):   # the encoder stage's stream: no legacy-stream barrier
+                feats = fb(np.stack(wins), firsts)
+        else:
+            feats = fb(np.stack(wins), firsts)
         items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=feats[b], kv=t.kv,
                       enc_cache=t.enc_cache, ada_cache=t.ada_cache, pe_index=t.pe) for b, t in enumerate(turns)]
         if pipe is not None and c > 0:

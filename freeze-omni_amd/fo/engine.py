@@ -332,7 +332,8 @@ class ListenGraph:
         self.ws = llm.stack.workspace(n, ops.attn_nsplit(max_keys, B, llm.KVH), dev)
         self.predict = ident == "user" and bool(eng.predict_usr_state) and llm.head_w is not None
         self.probs = torch.empty(B, 3, dtype=F32, device=dev)
-        self.probs_host = torch.empty(B, 3, dtype=F32).pin_memory()
+        self.probs_host = [torch.empty(B, 3, dtype=F32).pin_memory() for _ in range(slots)]
+        self.inflight = [None] * slots
         self.main = ops.engine_stream(dev)
         self.side = ops.engine_stream(dev, side=True) if slots > 1 else self.main
         # the encoder stage is captured on the stream it replays on, so its split-K scratch (ops.Runtime)
@@ -402,9 +403,10 @@ class ListenGraph:
         self.enc.advance(caches, self.T)
         return new_pe
 
-    def submit_llm(self, items, new_pe, k=0):
+    def submit_llm(self, items, new_pe, k=0, wait=True):
         """LLM stage of the chunk whose encoder stage filled x slot k (engine stream); appends To KV
-        rows per session and returns the per-session results (reads the state head back)."""
+        rows per session.  wait=True returns the per-session results (reads the state head back);
+        wait=False only queues the stage and its state-head copy: collect_llm(k) reads them later."""
         B, To, maxb = self.B, self.To, self.maxb
         n = B * To
         j, h = self.lring.next()
@@ -427,13 +429,21 @@ class ListenGraph:
         if self.side is not self.main:
             _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_enc[k])
         _lib.call("fo_graph_launch", self.llm_exec[k], st.cuda_stream)
-        _lib.call("fo_event_record", self.ev_llm[k], st.cuda_stream)
-        self.llm_used[k] = True
-        probs = None
         if self.predict:
             with torch.cuda.stream(st):
-                self.probs_host.copy_(self.probs, non_blocking=False)
-            probs = self.probs_host.numpy()
+                self.probs_host[k].copy_(self.probs, non_blocking=True)
+        _lib.call("fo_event_record", self.ev_llm[k], st.cuda_stream)
+        self.llm_used[k] = True
+        self.inflight[k] = (items, new_pe)
+        return self.collect_llm(k) if wait else None
+
+    def collect_llm(self, k):
+        """Results of the LLM stage queued in slot k (waits for it)."""
+        items, new_pe = self.inflight[k]
+        self.inflight[k] = None
+        To = self.To
+        _lib.call("fo_event_sync", self.ev_llm[k])
+        probs = self.probs_host[k].numpy() if self.predict else None
         res = []
         for b, it in enumerate(items):
             r = {"enc_cache": it["enc_cache"], "ada_cache": it["ada_cache"], "pe_index": new_pe[b],
@@ -458,23 +468,32 @@ class ListenGraph:
 
 
 class ListenPipe:
-    """Pipelined steady-state listen for one batch of sessions (ListenGraph with two x slots): the
-    encoder stage of the chunk just pushed overlaps the LLM stage of the previous chunk.
+    """Pipelined steady-state listen for one batch of sessions (ListenGraph with two x slots).
 
         pipe = engine.listen_pipe()
-        pe_next, prev = pipe.push(items_c)   # chunk c's next pe_index per session; results of chunk c-1
+        pe_next, prev = pipe.push(items_c, decide)   # chunk c's next pe_index per session; results of c-1
         ...; last = pipe.flush()
-    (encoder / adapter caches are advanced in place at submission, like listen(); pe_index is returned
-    at submission so the caller can build the next chunk's items before chunk c's LLM stage ran)
+
+    push(items_c): queues chunk c's encoder stage (side stream), waits for chunk c-1's LLM stage and
+    reads its results (the state decision), then -- unless decide(results of c-1) returns False, the
+    reference's "stop listening on dialog_ss" -- queues chunk c's LLM stage and returns at once.  So the
+    LLM stage of chunk c is never queued before the decision on chunk c-1 (no speculation), the encoder
+    stage of chunk c overlaps the LLM stage of chunk c-1, and the caller prepares chunk c+1 (framing,
+    fbank) while chunk c's LLM stage runs.  A refused chunk's encoder stage has run (its caches are reset
+    on dialog_ss anyway, bin/inference.py:133-135) but nothing was appended to the context.
+    (encoder / adapter caches are advanced in place at submission, like listen().)
 
     Every push must be graphable (same identity and batch, no chat prefix, open caches); the results
     are identical to calling listen() chunk by chunk."""
 
     def __init__(self, eng):
         self.eng, self.g, self.pending, self.k = eng, None, None, 0
+        self.stopped = False
 
-    def push(self, items):
+    def push(self, items, decide=None):
         eng = self.eng
+        if self.stopped:
+            raise RuntimeError("ListenPipe: decide() stopped this pipe (flush and start a new one)")
         with torch.cuda.stream(ops.engine_stream(eng.device)):
             if not eng._graphable(items):
                 raise ValueError("ListenPipe.push: items must be steady-state chunks (no chat prefix, open caches)")
@@ -486,9 +505,13 @@ class ListenPipe:
             pe = g.submit_encoder(items, k)
             out = None
             if self.pending is not None:
-                pitems, ppe, pk = self.pending
-                out = g.submit_llm(pitems, ppe, pk)
-            self.pending = (items, pe, k)
+                out = g.collect_llm(self.pending)
+                self.pending = None
+            if decide is not None and out is not None and not decide(out):
+                self.stopped = True
+                return pe, out
+            g.submit_llm(items, pe, k, wait=False)
+            self.pending = k
             self.k = 1 - k
             return pe, out
 
@@ -496,6 +519,5 @@ class ListenPipe:
         if self.pending is None:
             return None
         with torch.cuda.stream(ops.engine_stream(self.eng.device)):
-            items, pe, k = self.pending
-            self.pending = None
-            return self.g.submit_llm(items, pe, k)
+            k, self.pending = self.pending, None
+            return self.g.collect_llm(k)
