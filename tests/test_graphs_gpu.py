@@ -102,3 +102,44 @@ def test_listen_pipe_matches_sequential(eng, dev):
         np.testing.assert_array_equal(np.array(pg), np.array(pe))
         for a, b in zip(hg, he):
             np.testing.assert_array_equal(a, b)
+
+
+def test_listen_pipe_decide_stops_before_queuing(eng, dev):
+    """decide(results of chunk c-1) returning False (dialog_ss) queues nothing for chunk c: the context
+    holds exactly the chunks before it, and the states seen match the sequential run's."""
+    g = np.load(os.path.join(G, "fbank.npz"))
+    n_users = 2
+    feats = torch.from_numpy(g["A_feats"]).to(dev)
+    seq = [torch.stack([feats[(c + 3 * u) % 13] for u in range(n_users)]) for c in range(8)]
+    ref = _session_run(eng, seq[:5], True, n_users)           # chunks 0..4
+    base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    kvs = [base.fork() for _ in range(n_users)]
+    state = [dict(enc_cache=None, ada_cache=None, pe_index=0) for _ in range(n_users)]
+    seen = []
+
+    def decide(res):
+        seen.append([(r["probs"]["state_1"], r["probs"]["state_2"]) for r in res])
+        return len(seen) < 4                                  # stop after the decision on chunk 4
+
+    pipe = eng.listen_pipe()
+    for c, f in enumerate(seq):
+        items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=f[u], kv=kvs[u], **state[u])
+                 for u in range(n_users)]
+        if c == 0:
+            for u, r in enumerate(eng.listen(items)):
+                state[u] = dict(enc_cache=r["enc_cache"], ada_cache=r["ada_cache"], pe_index=r["pe_index"])
+            continue
+        pe, _ = pipe.push(items, decide)
+        for u in range(n_users):
+            state[u]["pe_index"] = pe[u]
+        if pipe.stopped:
+            break
+    assert pipe.stopped and c == 5 and pipe.flush() is None
+    assert [kv.length for kv in kvs] == ref[-1][2]             # chunk 5 never reached the context
+    for (pe_ref, _, _, _), pg in zip(ref[1:], seen):
+        np.testing.assert_array_equal(np.array(pg), np.array(pe_ref))
+    with pytest.raises(RuntimeError):
+        pipe.push(items)
+    for kv in kvs:
+        kv.free()
+    base.free()
