@@ -28,7 +28,7 @@ class TTSEngine:
     def __init__(self, src, decoder_json, device, kv_tokens=1 << 16, page_size=16):
         idim, odim, a = decoder_json
         self.device = torch.device(device)
-        self.vocab = odim
+        self.vocab, self.idim = odim, idim
         self.D, self.H = a["transformer_attention_dim"], a["transformer_attention_heads"]
         self.hd = self.D // self.H
         self.nb = a["transformer_num_blocks"]

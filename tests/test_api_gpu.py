@@ -139,3 +139,22 @@ def test_pools(dev):
     tp.acquire()
     with pytest.raises(Exception):
         tp.acquire()
+
+
+def test_offline_driver_wav_to_wav(dev, tmp_path):
+    """freeze-omni_amd/bin/inference.py end to end on the tiny config: 1.2 s at 8 kHz in (resampled),
+    24 kHz 16-bit PCM out, text decode bounded by --max_text_tokens."""
+    import importlib
+    m = importlib.import_module("bin.inference")
+    rng = np.random.default_rng(3)
+    t = np.arange(9600) / 8000.0
+    x = 0.3 * np.sin(2 * np.pi * 300.0 * t) + 0.05 * rng.standard_normal(t.shape[0])
+    inp, out = str(tmp_path / "in.wav"), str(tmp_path / "out.wav")
+    m.write_wav(inp, x, 8000)
+    text, pcm = m.main(["--model_path", TINY, "--llm_path", os.path.join(TINY, "llm"), "--input_wav", inp,
+                        "--output_wav", out, "--top_k", "1", "--max_text_tokens", "12"])
+    assert isinstance(text, str)
+    y, fs = m.read_wav(out)
+    assert fs == 24000 and y.shape[0] == pcm.shape[0]
+    assert np.all(np.isfinite(pcm)) and np.max(np.abs(pcm)) <= 1.0
+    np.testing.assert_allclose(y, np.clip(np.round(pcm * 32768.0), -32768, 32767) / 32768.0, atol=0)
