@@ -405,6 +405,20 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
   for (int d = tid; d < HD; d += DEC_NT) q_s[d] = qr[d] * a.scale;
   __syncthreads();
   const size_t page_sz = (size_t)a.KVH * a.PS * HD, head_off = (size_t)h * a.PS * HD;
+  // P.V layout: HD/4 lanes per key (one float4 of the V row each), 64/(HD/4) keys per wave-instruction,
+  // the waves on interleaved keys.  The first NPF rounds of V rows are loaded here, in flight together
+  // with the K rows, so the P.V pass after the softmax waits on no memory for up to 256-512 keys.
+  constexpr int LPK = HD / 4, KPW = 64 / LPK, VSTR = DEC_NW * KPW;
+  constexpr int NPF = 512 / VSTR < 16 ? 512 / VSTR : 16;
+  const int sub = lane / LPK, l4 = lane % LPK;
+  float4 vpf[NPF];
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int j = wave * KPW + sub + i * VSTR;
+    if (j < L)
+      vpf[i] = *reinterpret_cast<const float4*>(a.vc + (size_t)pg_s[j / a.PS] * page_sz + head_off +
+                                                (size_t)(j % a.PS) * HD + 4 * l4);
+  }
   float mx = -INFINITY;
   for (int j = tid; j < L; j += DEC_NT) {
     const float* kr = a.kc + (size_t)pg_s[j / a.PS] * page_sz + head_off + (size_t)(j % a.PS) * HD;
@@ -430,13 +444,20 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
     sum += p;
   }
   sum = block_sum<DEC_NW>(sum, red_s);  // its barriers also publish s_s
-  // P.V: HD/4 lanes per key (one float4 of the V row each), 64/(HD/4) keys per wave-instruction, the 4
-  // waves on interleaved keys; 8 keys per lane in flight
-  constexpr int LPK = HD / 4, KPW = 64 / LPK;
-  const int sub = lane / LPK, l4 = lane % LPK;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int j = wave * KPW + sub + i * VSTR;
+    if (j < L) {
+      const float p = s_s[j];
+      acc.x += p * vpf[i].x;
+      acc.y += p * vpf[i].y;
+      acc.z += p * vpf[i].z;
+      acc.w += p * vpf[i].w;
+    }
+  }
 #pragma unroll 8
-  for (int j = wave * KPW + sub; j < L; j += DEC_NW * KPW) {
+  for (int j = wave * KPW + sub + NPF * VSTR; j < L; j += VSTR) {
     const float p = s_s[j];
     const float4 v = *reinterpret_cast<const float4*>(a.vc + (size_t)pg_s[j / a.PS] * page_sz + head_off +
                                                       (size_t)(j % a.PS) * HD + 4 * l4);
