@@ -83,6 +83,7 @@ class FreezeOmniEngine:
             self.tokenizer.eod_id = self.tokenizer.eos_token_id
         self._fbank = {}
         self._lgraphs = {}
+        self._tgraphs = {}
         self.use_graphs = True
         self.predict_usr_state = ty["model_conf"].get("predict_usr_state", 0)
         self._chat_template(ty["model_conf"].get("chat_template"))
@@ -236,9 +237,14 @@ class FreezeOmniEngine:
         return results
 
     # ------------------------------------------------------------------ text decode (A17 reconstruction)
-    def text_step(self, items, top_k=1, top_p=0.0, temperature=1.0, seed=0):
+    def text_step(self, items, top_k=1, top_p=0.0, temperature=1.0, seed=0, graph=True):
         """items: list of (kv, input_ids list): forward those tokens, sample the next from the last
-        position.  Returns (next ids list, last hidden rows [B, D] device)."""
+        position.  Returns (next ids list, last hidden rows [B, D] device).  One token per session
+        (every step after the assistant prefix) replays a captured TextGraph; the result is the same
+        launch sequence as the eager path."""
+        if graph and self.use_graphs and items and all(len(t) == 1 for _, t in items):
+            with torch.cuda.stream(ops.engine_stream(self.device)):
+                return self._text_graph_for(items, top_k, top_p, temperature, seed).run(items)
         B = len(items)
         ids = [t for _, toks in items for t in toks]
         x = self.llm.embed(ids, round_fp16=True)
@@ -252,6 +258,19 @@ class FreezeOmniEngine:
         out = torch.empty(B, dtype=I32, device=self.device)
         ops.sample(logits, self.llm.V, out, par, tp[:B], tp[B:], seed=seed, step=step)
         return out.cpu().tolist(), hid
+
+
+    def _text_graph_for(self, items, top_k, top_p, temperature, seed, extra=64):
+        B = len(items)
+        need = max(kv.length for kv, _ in items) + extra
+        key = (B, top_k, float(top_p), float(temperature), seed)
+        g = self._tgraphs.get(key)
+        if g is None or g.max_keys < need:
+            if g is not None:
+                g.destroy()
+            g = TextGraph(self, B, max(need + 1024, 2048), top_k, top_p, temperature, seed)
+            self._tgraphs[key] = g
+        return g
 
 
 class _HostRing:
@@ -464,6 +483,84 @@ class ListenGraph:
                 _lib.call("fo_event_destroy", e)
             self.ering.destroy()
             self.lring.destroy()
+            self.exec = None
+
+
+class TextGraph:
+    """One text-decode step for B sessions (A17 reconstruction, the caller contract of
+    bin/inference.py:152-179: one token per session in, the next token out) as one captured hipGraph:
+    embedding rows rounded to fp16 (inputs_embeds.half(), models/audioLLM.py:338), the Qwen2 layers on
+    paged KV, the final norm, lm_head and the sampler (models/audioLLM.py:431-477).  Per-call inputs
+    (token ids, positions, cache slots, visible keys, sampler steps, block tables) go up in one pinned
+    upload and the drawn ids come back in one pinned download."""
+
+    def __init__(self, eng, B, max_keys, top_k, top_p, temperature, seed):
+        dev = eng.device
+        llm = eng.llm
+        self.eng, self.B, self.max_keys, self.seed = eng, B, max_keys, seed
+        PS = llm.pool.PS
+        self.maxb = (max_keys + PS - 1) // PS
+        # metadata [ids B | tok_pos B | tok_slot B | tok_nvis B | sampler step B | block table B x maxb]
+        n_meta = 5 * B + B * self.maxb
+        self.meta_d = torch.zeros(n_meta, dtype=I32, device=dev)
+        self.ring = _HostRing(n_meta)
+        m = self.meta_d
+        self.ids, self.step = m[0:B], m[4 * B:5 * B]
+        items = torch.tensor([[b, b, 1] for b in range(B)], dtype=I32).reshape(-1).to(dev)
+        self.meta = SimpleNamespace(T=B, S=B, tok_pos=m[B:2 * B], tok_slot=m[2 * B:3 * B], tok_nvis=m[3 * B:4 * B],
+                                    block_table=m[5 * B:].view(B, self.maxb), items=items, n_items=B,
+                                    max_rows=llm.H // llm.KVH, max_keys=max_keys)
+        self.x = torch.empty(B, llm.D, dtype=F32, device=dev)
+        self.logits = torch.empty(B, llm.lm_head.N, dtype=F32, device=dev)
+        self.ws = llm.stack.workspace(B, ops.attn_nsplit(max_keys, B, llm.KVH), dev)
+        self.par = torch.tensor([top_k] * B, dtype=I32).to(dev)
+        self.tp = torch.tensor([temperature] * B + [top_p] * B, dtype=F32).to(dev)
+        self.out = torch.empty(B, dtype=I32, device=dev)
+        self.out_host = torch.empty(B, dtype=I32).pin_memory()
+        self.main = ops.engine_stream(dev)
+        self.exec = ListenGraph._capture(self.main, self._body)
+        self.ev = ListenGraph._event()
+
+    def _body(self):
+        llm, B = self.eng.llm, self.B
+        ops.gather_rows(llm.embed_tokens, self.ids, out=self.x, round_fp16=True)
+        llm.stack.forward(self.x, self.meta, self.ws)
+        ops.rmsnorm(self.x, llm.norm, llm.eps, out=self.x)
+        llm.lm_head(self.x, out=self.logits)
+        ops.sample(self.logits, llm.V, self.out, self.par, self.tp[:B], self.tp[B:], seed=self.seed, step=self.step)
+
+    def run(self, items):
+        """items: list of (kv, [token id]) in batch order; appends one KV position per session."""
+        B, maxb = self.B, self.maxb
+        j, h = self.ring.next()
+        bt = h[5 * B:].reshape(B, maxb)
+        for b, (kv, toks) in enumerate(items):
+            L = kv.length
+            kv.reserve(L + 1)
+            if len(kv.pages) > maxb:
+                raise RuntimeError("text graph block table too small")
+            h[b] = toks[0]
+            h[B + b] = L
+            h[2 * B + b] = kv.slot(L)
+            h[3 * B + b] = L + 1
+            h[4 * B + b] = L + 1   # the eager path's sampler step: the sequence length after the forward
+            bt[b, :len(kv.pages)] = kv.pages
+            kv.length = L + 1
+        st = self.main
+        self.ring.upload(j, self.meta_d, st)
+        _lib.call("fo_graph_launch", self.exec, st.cuda_stream)
+        with torch.cuda.stream(st):
+            self.out_host.copy_(self.out, non_blocking=True)
+            hid = self.x.clone()
+        _lib.call("fo_event_record", self.ev, st.cuda_stream)
+        _lib.call("fo_event_sync", self.ev)
+        return self.out_host.tolist(), hid
+
+    def destroy(self):
+        if self.exec is not None:
+            _lib.call("fo_graph_destroy", self.exec)
+            _lib.call("fo_event_destroy", self.ev)
+            self.ring.destroy()
             self.exec = None
 
 

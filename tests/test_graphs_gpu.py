@@ -143,3 +143,31 @@ def test_listen_pipe_decide_stops_before_queuing(eng, dev):
     for kv in kvs:
         kv.free()
     base.free()
+
+
+def _text_run(eng, graph, n_users, steps, top_k):
+    base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    kvs = [base.fork() for _ in range(n_users)]
+    pre = eng.prefix_ids["system"]
+    ids, hid = eng.text_step([(kv, pre) for kv in kvs], top_k=top_k, seed=7)   # prefix: eager either way
+    out = [(list(ids), hid.cpu().numpy().copy())]
+    for _ in range(steps):
+        ids, hid = eng.text_step([(kv, [i]) for kv, i in zip(kvs, ids)], top_k=top_k, seed=7, graph=graph)
+        out.append((list(ids), hid.cpu().numpy().copy()))
+    lens = [kv.length for kv in kvs]
+    for kv in kvs:
+        kv.free()
+    base.free()
+    return out, lens
+
+
+@pytest.mark.parametrize("top_k", [1, 5])
+def test_text_graph_matches_eager(eng, top_k):
+    """The captured text-decode step (fo.engine.TextGraph) draws the same ids as the eager step (same
+    kernels and counter RNG), with the same hidden rows and KV lengths."""
+    eager, le = _text_run(eng, False, 3, 12, top_k)
+    graph, lg = _text_run(eng, True, 3, 12, top_k)
+    assert len(eng._tgraphs) >= 1 and le == lg
+    for (ie, he), (ig, hg) in zip(eager, graph):
+        assert ie == ig
+        np.testing.assert_allclose(hg, he, atol=2e-5, rtol=1e-5)
