@@ -485,6 +485,7 @@ def main():
         audio = sum(float(x[1]) for x in allw)
         lat = gather_list(dist, lat, world, dev)
         lat_gated = gather_list(dist, lat_gated, world, dev)
+        rtf_user = gather_list(dist, rtf_user, world, dev)
     if rank == 0:
         peak = 8000.0
         # the SwiGLU (last template flag true) M<=16 weight stream: Qwen2 gate/up of every layer
