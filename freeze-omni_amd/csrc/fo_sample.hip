@@ -168,6 +168,27 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
   }
 }
 
+// Repetition penalty of the AR speech decoder (models/decoder/decoder.py:348-351): every entry of the
+// last W generated ids (SOS included) divides its logit by `penalty`.  The reference iterates
+// set(generated_tokens[0][-W:]) over 0-d tensors, whose hash is their identity, so a token present
+// k times in the window is divided k times; this kernel keeps that multiplicity.  win [B][W] is a
+// per-row ring indexed by step % W: the step's input id (the last generated id) is stored first.
+// One lane per row, divisions in window order (x / p each time, as the reference's in-place /=).
+__global__ __launch_bounds__(64) void k_penalty(float* logits, int ld, int B, int V, const int* ids, int* win, int W,
+                                                const int* step_rows, float penalty) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  const int st = step_rows[row];
+  int* w = win + (size_t)row * W;
+  w[st % W] = ids[row];
+  const int n = st + 1 < W ? st + 1 : W;
+  float* lg = logits + (size_t)row * ld;
+  for (int j = 0; j < n; ++j) {
+    const int t = w[j];
+    if (t >= 0 && t < V) lg[t] = lg[t] / penalty;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -197,6 +218,16 @@ int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k,
   hipLaunchKernelGGL(k_sample<true>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
                      key, ban_id, out_ids, nullptr, nx);
   return fo::check_launch("fo_sample_embed");
+}
+
+// logits[row][win ids] /= penalty once per window entry (see k_penalty); win [B][W] device ring,
+// step[row] = this step's index (0 = the SOS input).
+int fo_penalty(float* logits, int ld, int B, int V, const int* ids, int* win, int W, const int* step, float penalty,
+               hipStream_t s) {
+  FO_REQUIRE(B > 0 && V > 0 && W > 0 && ld >= V, "fo_penalty: bad shape B=%d V=%d W=%d", B, V, W);
+  FO_REQUIRE(logits && ids && win && step && penalty > 0.f, "fo_penalty: missing buffers or penalty <= 0");
+  hipLaunchKernelGGL(k_penalty, dim3((B + 63) / 64), dim3(64), 0, s, logits, ld, B, V, ids, win, W, step, penalty);
+  return fo::check_launch("fo_penalty");
 }
 
 }  // extern "C"

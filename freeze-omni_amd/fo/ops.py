@@ -495,6 +495,15 @@ def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0,
     return out_ids
 
 
+def penalty(logits, V, ids, win, step, penalty, B=None):
+    """Repetition penalty (models/decoder/decoder.py:348-351) in place on logits [B, >=V]: stores this
+    step's input ids into the ring win [B, W] at step % W, then divides each windowed id's logit."""
+    B = logits.shape[0] if B is None else B
+    _lib.call("fo_penalty", logits.data_ptr(), logits.stride(0), B, V, ids.data_ptr(), win.data_ptr(), win.shape[1],
+              step.data_ptr(), float(penalty), stream(logits.device))
+    return logits
+
+
 def sample_embed(logits, V, out_ids, emb, x, gamma, eps, h, top_k=None, temperature=None, top_p=None, seed=0,
                  step=None, B=None, ban_id=-1, key=None, hist_ptr=None, hist_row=None, hist_ld=0):
     """sample(), then the next decode step's input from the drawn ids: x[b] = emb[id_b] (fp32), h[b] =

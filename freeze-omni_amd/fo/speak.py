@@ -12,6 +12,7 @@ import torch
 
 from . import _lib, ops
 from .ops import F32, I32
+from .tts import penalty_ring
 
 
 class SpeakState:
@@ -44,14 +45,17 @@ def silence_cut(buffer, syn, N, threshold, res):
 
 
 def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
-          max_tokens=1000, min_tokens=0, states_out=None, seed=0, graph=True, window=32):
+          max_tokens=1000, min_tokens=0, states_out=None, seed=0, graph=True, window=32, penalty_window_size=-1,
+          penalty=1.1):
     """items: list of (hidden [T1, D] device, prefix [T2, D] device or None).
     min_tokens > 0 masks EOS until that many tokens (benchmark policy).
     Yields (session index, pcm segment device 1-D) as segments become available; the per-session
     SpeakState objects are appended to states_out.
     graph=True replays a captured decode step (fo.tts.DecodeGraph) and reads sampled ids back lazily,
     up to `window` steps behind the GPU; graph=False is the step-by-step eager loop.  Both produce the
-    same ids (same kernels, same RNG stream)."""
+    same ids (same kernels, same RNG stream).
+    penalty_window_size > 0 applies the reference's repetition penalty (decoder.py:348-351, fo_penalty)."""
+    pen = (int(penalty_window_size), float(penalty)) if penalty_window_size and penalty_window_size > 0 else None
     es = ops.engine_stream(engine.device)
     with torch.cuda.stream(es):
         seqs = engine.tts.start(items)
@@ -60,7 +64,7 @@ def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=
         states_out.extend(states)
     run = _speak_graph if graph else _speak_eager
     gen = run(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens, min_tokens,
-              seed, window)
+              seed, window, pen)
     try:
         while True:
             with torch.cuda.stream(es):  # the engine stream is current only while engine code runs
@@ -100,7 +104,7 @@ def _emit(engine, states, chunk_due, finished, up, pad, N, thr, res):
 
 
 def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
-                 min_tokens, seed, window):
+                 min_tokens, seed, window, pen=None):
     tts = engine.tts
     dev = engine.device
     up = engine.codec.upsample
@@ -116,6 +120,9 @@ def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
         # also emit the BOS/SOS/PAD specials that a trained decoder never produces)
         forced = bool(min_tokens and step < min_tokens)
         st = torch.tensor([step] * len(live) + live, dtype=I32).to(dev)  # RNG (step, session) per row
+        if pen:
+            win = torch.tensor([penalty_ring([tts.sos] + states[i].all_ids, pen[0]) for i in live], dtype=I32).to(dev)
+            ops.penalty(lg, tts.vocab + 4, cur, win, st, pen[1], B=len(live))
         ops.sample(lg, tts.vocab if forced else tts.vocab + 4, out_ids, topk_d, None, None, seed=seed,
                    step=st[:len(live)], B=len(live), key=st[len(live):])
         ids = out_ids[:len(live)].cpu().tolist()
@@ -132,7 +139,7 @@ def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
 
 
 def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
-                 min_tokens, seed, window):
+                 min_tokens, seed, window, pen=None):
     tts = engine.tts
     dev = engine.device
     up = engine.codec.upsample
@@ -147,11 +154,12 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
         while live and len(pending) < window and step < max_tokens:
             forced = bool(min_tokens and step < min_tokens)
             ng = tts.decode_graph(len(live), tts.vocab if forced else tts.vocab + 4, top_k, seed, max_keys,
-                                  max_tokens + 1)
+                                  max_tokens + 1, pen)
             if ng is not g:
                 if g is None or ng.B != g.B:
                     ng.ids.fill_(tts.sos) if step == 0 else ng.ids.copy_(torch.tensor(
                         [states[i].all_ids[-1] for i in live], dtype=I32).to(dev))
+                    ng.set_window([[tts.sos] + states[i].all_ids for i in live])
                     ng.prime()
                 else:
                     ng.adopt(g)  # same batch, other sampler bound: ids and input rows stay on the device

@@ -109,22 +109,33 @@ class TTSEngine:
         ops.rmsnorm(x, self.main.layers[0].ln1, self.eps, out=ws["h"], M=B)
         return x
 
-    def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows):
-        """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows)."""
-        key = (B, V_sample, top_k, seed)
+    def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None):
+        """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows).
+        pen = (window, penalty) adds the repetition penalty before the draw (None: off)."""
+        key = (B, V_sample, top_k, seed, pen)
         g = self._graphs.get(key) if hasattr(self, "_graphs") else None
         if g is None or g.max_keys < max_keys or g.hist_rows < hist_rows:
             if not hasattr(self, "_graphs"):
                 self._graphs = {}
             if g is not None:
                 g.destroy()
-            g = DecodeGraph(self, B, V_sample, top_k, seed, max(max_keys, 1024), max(hist_rows, 1024))
+            g = DecodeGraph(self, B, V_sample, top_k, seed, max(max_keys, 1024), max(hist_rows, 1024), pen)
             self._graphs[key] = g
         return g
 
     def free(self, seqs):
         for s in seqs:
             s.kv.free()
+
+
+def penalty_ring(generated, W):
+    """Ring image of the penalty window for one session: generated = [SOS] + ids drawn so far; the id
+    with generation index k sits at slot k % W (what fo_penalty writes step by step); empty slots -1."""
+    ring = [-1] * W
+    n = len(generated)
+    for k in range(max(0, n - W), n):
+        ring[k % W] = generated[k]
+    return ring
 
 
 class DecodeGraph:
@@ -141,8 +152,10 @@ class DecodeGraph:
 
     RING = 64
 
-    def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows):
+    def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None):
         dev = tts.device
+        self.pen = pen
+        self.win = torch.full((B, pen[0]), -1, dtype=I32, device=dev) if pen else None
         PS = tts.pool.PS
         self.tts, self.B, self.V_sample, self.seed = tts, B, V_sample, seed
         self.max_keys, self.hist_rows = max_keys, hist_rows
@@ -177,6 +190,8 @@ class DecodeGraph:
         t = self.tts
         t.main.forward(self.x, self.meta, self.ws, pre_normed=True, final_norm=t.norm)
         t.out_fnn(self.ws["xg"], out=self.logits, norm=(self.ws["sA"], t.eps))
+        if self.pen:
+            ops.penalty(self.logits, t.vocab + 4, self.ids, self.win, self.meta.step, self.pen[1], B=self.B)
         ops.sample_embed(self.logits, self.V_sample, self.ids, t.embedding, self.x, t.main.layers[0].ln1, t.eps,
                          self.ws["h"], top_k=self.topk, seed=self.seed, step=self.meta.step, B=self.B,
                          key=self.meta.key, hist_ptr=self.hist.dev, hist_row=self.meta.hist_row, hist_ld=self.B)
@@ -188,6 +203,8 @@ class DecodeGraph:
     def adopt(self, other):
         """Continue another graph's batch (same sessions, other sampler bound): take its ids and input rows."""
         self.ids.copy_(other.ids)
+        if self.pen:
+            self.win.copy_(other.win)
         self.x.copy_(other.x)
         self.ws["h"].copy_(other.ws["h"])
 
@@ -202,6 +219,12 @@ class DecodeGraph:
             ex = ctypes.c_void_p()
             _lib.call("fo_graph_end", s, ctypes.byref(ex))
         self.exec = ex
+
+    def set_window(self, generated_lists):
+        """Penalty rings of a new batch from the host-side id history ([SOS] + ids per session)."""
+        if self.pen:
+            rings = [penalty_ring(g, self.pen[0]) for g in generated_lists]
+            self.win.copy_(torch.tensor(rings, dtype=I32).to(self.win.device))
 
     def set_ids(self, ids_dev):
         self.ids.copy_(ids_dev[:self.B])

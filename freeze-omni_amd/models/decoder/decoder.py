@@ -2,6 +2,7 @@
 import torch
 
 from fo import ops
+from fo.tts import penalty_ring
 
 
 class LLM2TTSCodecAR:
@@ -10,8 +11,6 @@ class LLM2TTSCodecAR:
         self.vocab_size = tts_engine.vocab
 
     def infer(self, hidden, top_k, prefix, penalty_window_size=-1, penalty=1.1, max_tokens=1000):
-        if penalty_window_size > 0:
-            raise NotImplementedError("repetition penalty is not on the MI355X path")
         e = self.engine
         dev = e.device
         h = hidden.reshape(-1, hidden.shape[-1]).to(dev, torch.float32).contiguous()
@@ -20,13 +19,19 @@ class LLM2TTSCodecAR:
         cur = torch.full((1,), e.sos, dtype=torch.int32, device=dev)
         k = torch.tensor([top_k], dtype=torch.int32).to(dev)
         out = torch.empty(1, dtype=torch.int32, device=dev)
+        generated = [e.sos]
         try:
             for i in range(max_tokens):
-                ops.sample(e.step(seqs, cur), e.vocab + 4, out, k,
-                           step=torch.full((1,), i, dtype=torch.int32, device=dev))
+                step = torch.full((1,), i, dtype=torch.int32, device=dev)
+                lg = e.step(seqs, cur)
+                if penalty_window_size > 0:   # decoder.py:348-351
+                    win = torch.tensor([penalty_ring(generated, penalty_window_size)], dtype=torch.int32).to(dev)
+                    ops.penalty(lg, e.vocab + 4, cur, win, step, penalty)
+                ops.sample(lg, e.vocab + 4, out, k, step=step)
                 t = int(out.item())
                 if t == e.eos:
                     break
+                generated.append(t)
                 yield torch.tensor([[t]], device=dev)
                 cur = out.clone()
         finally:

@@ -44,9 +44,6 @@ class llm2TTS:
 
     def run_batch(self, items, top_k, codec_chunk_size=40, codec_padding_size=10, penalty_window_size=-1,
                   penalty=1.1, N=2401, seg_threshold=0.01, max_tokens=1000, min_tokens=0):
-        if penalty_window_size > 0:
-            raise NotImplementedError("repetition penalty (penalty_window_size > 0) is not on the MI355X path; "
-                                      "the reference drivers run with it off (bin/inference.py:89)")
         prepared = []
         for hidden, prefix in items:
             h = torch.as_tensor(hidden).reshape(-1, torch.as_tensor(hidden).shape[-1])
@@ -55,4 +52,5 @@ class llm2TTS:
                              None if p is None else p.to(self.engine.device, torch.float32).contiguous()))
         yield from speak(self.engine, prepared, top_k=top_k, codec_chunk_size=codec_chunk_size,
                          codec_padding_size=codec_padding_size, N=N, seg_threshold=seg_threshold,
-                         max_tokens=max_tokens, min_tokens=min_tokens)
+                         max_tokens=max_tokens, min_tokens=min_tokens, penalty_window_size=penalty_window_size,
+                         penalty=penalty)

@@ -200,6 +200,11 @@ int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
                     int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
                     int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, hipStream_t s);
+/* Repetition penalty of the AR decode loop (models/decoder/decoder.py:348-351), applied before the
+ * draw: win[row][step[row] % W] = ids[row], then logits[row][t] /= penalty for every entry t of the
+ * last min(step+1, W) ids -- once per occurrence, as the reference's set() of 0-d tensors does. */
+int fo_penalty(float* logits, int ld, int B, int V, const int* ids, int* win, int W, const int* step, float penalty,
+               hipStream_t s);
 
 #ifdef __cplusplus
 }

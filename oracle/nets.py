@@ -358,12 +358,14 @@ class TTSDecoder:
         x = rmsnorm(x, self.W["tts.norm.weight"], self.eps)
         return linear(x, self.W["tts.out_fnn.weight"], self.W["tts.out_fnn.bias"])[0]
 
-    def infer_greedy(self, hidden, prefix, max_tokens=1000, return_logits=0):
+    def infer_greedy(self, hidden, prefix, max_tokens=1000, return_logits=0, penalty_window_size=-1, penalty=1.1):
         kv, P = self.prefill(hidden, prefix)
         cur = self.vocab + 1
         ids, lgs = [], []
         for _ in range(max_tokens):
             lg = self.step(cur, kv, P)
+            if penalty_window_size > 0:
+                apply_penalty(lg, [self.vocab + 1] + ids, penalty_window_size, penalty)
             if len(lgs) < return_logits:
                 lgs.append(lg)
             nxt = int(np.argmax(lg))  # top_k=1: softmax/topk/multinomial collapse to argmax
@@ -372,6 +374,16 @@ class TTSDecoder:
             ids.append(nxt)
             cur = nxt
         return (ids, lgs) if return_logits else ids
+
+
+def apply_penalty(lg, generated, W, penalty):
+    """models/decoder/decoder.py:348-351: `for token in set(generated_tokens[0][-W:])` iterates 0-d tensors,
+    whose hash is their identity, so the set keeps duplicates and a token seen k times in the window has
+    its logit divided k times (in place, x / penalty each time, fp32)."""
+    p = np.float32(penalty)
+    for t in generated[-W:]:
+        lg[t] = np.float32(lg[t] / p)
+    return lg
 
 
 # ============================================================ codec (models/decoder/ticodec/*)

@@ -376,6 +376,27 @@ def gold_tts(cfg):
     return m
 
 
+def gold_tts_penalty(cfg):
+    """LLM2TTSCodecAR.infer with the repetition penalty on (decoder.py:348-351), greedy, same inputs as
+    gold_tts: pins the per-occurrence division of set(generated_tokens[0][-W:]) over 0-d tensors."""
+    import argparse
+    from models.decoder.decoder import LLM2TTSCodecAR
+    idim, odim, args = cfg["decoder_json"]
+    m = LLM2TTSCodecAR(idim, odim, argparse.Namespace(**args))
+    init_module(m, cfg["seed"], "tts.", cfg["overrides"])
+    m.eval()
+    rng = np.random.default_rng(5)
+    T1, T2 = 9, 24
+    hidden = torch.from_numpy(rng.standard_normal((1, T1, idim)).astype(np.float32) * 0.5)
+    prefix = torch.from_numpy(rng.standard_normal((1, T2, idim)).astype(np.float32) * 0.5)
+    out = {}
+    for name, W, pen in (("w20_p1.5", 20, 1.5), ("w3_p1.1", 3, 1.1)):
+        ids = [int(t) for t in m.infer(hidden, 1, prefix, W, pen, max_tokens=120)]
+        out["ids_" + name] = np.array(ids, dtype=np.int64)
+        print("tts penalty", name, len(ids), ids[:12])
+    np.savez_compressed(os.path.join(HERE, "tts_penalty_tiny.npz"), **out)
+
+
 def gold_codec(cfg, tts_model):
     from models.decoder.ticodec.models import Generator, Quantizer
     from models.decoder.ticodec.vqvae import VQVAE, AttrDict
@@ -461,6 +482,7 @@ def main():
     gold_audiollm(cfg, fb["A_feats"])
     m = gold_tts(cfg)
     gold_codec(cfg, m)
+    gold_tts_penalty(cfg)
     gold_text()
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
         json.dump(SHAPES, f)
@@ -469,4 +491,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["tts_penalty"]:   # regenerate only that fixture
+        install_shims()
+        gold_tts_penalty(C.get("tiny"))
+    else:
+        main()

@@ -273,3 +273,68 @@ def test_codec_mfma_matches_direct_at_real_geometry(dev):
     b = eng.forward_ncl(ids).view(3, -1)
     assert a.shape == b.shape and a.shape[1] >= 50 * 600  # odd (k - u) stages add a few samples, as upstream
     close(a, b.cpu().numpy(), rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("name,window,penalty", [("w20_p1.5", 20, 1.5), ("w3_p1.1", 3, 1.1)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_speak_penalty_ids_match_golden(dev, speech_engine, name, window, penalty, graph):
+    """fo_penalty in the eager loop and inside the captured decode graph: greedy ids equal the reference
+    run with the repetition penalty on (tests/golden/tts_penalty_tiny.npz, bit-exact)."""
+    t = np.load(os.path.join(G, "tts_tiny.npz"))
+    p = np.load(os.path.join(G, "tts_penalty_tiny.npz"))
+    items = [(torch.from_numpy(t["hidden"]).to(dev), torch.from_numpy(t["prefix"]).to(dev))]
+    ids, _ = _speak_all(speech_engine, items, graph, top_k=1, max_tokens=120, penalty_window_size=window,
+                        penalty=penalty)
+    assert ids[0] == p["ids_" + name].tolist()
+
+
+def test_speak_penalty_graph_matches_eager_on_shrink(dev, speech_engine):
+    """Penalty rings survive the batch shrinking at EOS (rings rebuilt from the host history) and the
+    sampler-bound switch at min_tokens (rings adopted on the device): graph == eager, token for token."""
+    tts = speech_engine.tts
+    saved = tts.out_fnn.bias.clone()
+    try:
+        tts.out_fnn.bias[tts.eos] += 3.0
+        items = _items(dev, 4, 9)
+        kw = dict(top_k=8, max_tokens=200, min_tokens=20, seed=11, penalty_window_size=7, penalty=1.3)
+        ids_e, segs_e = _speak_all(speech_engine, items, False, **kw)
+        ids_g, segs_g = _speak_all(speech_engine, items, True, **kw)
+    finally:
+        tts.out_fnn.bias.copy_(saved)
+    lens = [len(x) for x in ids_e]
+    assert len(set(lens)) > 1
+    assert ids_g == ids_e
+    for (_, a), (_, b) in zip(segs_g, segs_e):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_penalty_kernel_multiplicity(dev):
+    """fo_penalty divides once per window occurrence, ring slot = step % W, ids outside [0, V) ignored."""
+    from fo import ops
+    V, W = 50, 4
+    lg = torch.full((2, V), 2.0, device=dev)
+    lg[1] = -2.0
+    win = torch.tensor([[7, 7, -1, -1], [3, 9, 9, 9]], dtype=torch.int32, device=dev)
+    ids = torch.tensor([7, 3], dtype=torch.int32, device=dev)
+    step = torch.tensor([2, 4], dtype=torch.int32, device=dev)
+    ops.penalty(lg, V, ids, win, step, 1.25)
+    out = lg.cpu()
+    assert torch.equal(win.cpu(), torch.tensor([[7, 7, 7, -1], [3, 9, 9, 9]], dtype=torch.int32))
+    assert float(out[0, 7]) == np.float32(np.float32(np.float32(2.0) / np.float32(1.25)) / np.float32(1.25)) / np.float32(1.25)
+    assert float(out[1, 9]) == np.float32(np.float32(np.float32(-2.0) / np.float32(1.25)) / np.float32(1.25)) / np.float32(1.25)
+    assert float(out[1, 3]) == np.float32(-2.0) / np.float32(1.25)
+    assert float(out[0, 0]) == 2.0 and float(out[1, 0]) == -2.0
+
+
+@pytest.mark.parametrize("window,penalty,key", [(-1, 1.1, None), (3, 1.1, "ids_w3_p1.1")])
+def test_codec_ar_facade_infer_matches_golden(dev, speech_engine, window, penalty, key):
+    """models.decoder.decoder.LLM2TTSCodecAR.infer (the reference's generator form, decoder.py:314-367)
+    yields the reference's greedy ids, with and without the repetition penalty."""
+    from models.decoder.decoder import LLM2TTSCodecAR
+    t = np.load(os.path.join(G, "tts_tiny.npz"))
+    want = t["ids"][:120] if key is None else np.load(os.path.join(G, "tts_penalty_tiny.npz"))[key]
+    m = LLM2TTSCodecAR(speech_engine.tts)
+    h = torch.from_numpy(t["hidden"]).unsqueeze(0).to(dev)
+    p = torch.from_numpy(t["prefix"]).unsqueeze(0).to(dev)
+    ids = [int(x) for x in m.infer(h, 1, p, window, penalty, max_tokens=120)]
+    assert ids == want.tolist()

@@ -124,6 +124,17 @@ def test_tts_greedy_ids_match_golden(W):
     np.testing.assert_allclose(np.stack(lgs), g["logits"], atol=2e-4, rtol=1e-3)
 
 
+@pytest.mark.parametrize("name,window,penalty", [("w20_p1.5", 20, 1.5), ("w3_p1.1", 3, 1.1)])
+def test_tts_penalty_ids_match_golden(W, name, window, penalty):
+    """Repetition penalty (decoder.py:348-351) vs the reference run with it on; w3_p1.1 diverges if the
+    window is de-duplicated, so it pins the per-occurrence division."""
+    g = load("tts_tiny.npz")
+    p = load("tts_penalty_tiny.npz")
+    dec = nets.TTSDecoder(W, CFG)
+    ids = dec.infer_greedy(g["hidden"], g["prefix"], max_tokens=120, penalty_window_size=window, penalty=penalty)
+    assert ids == p["ids_" + name].tolist()
+
+
 def test_codec_matches_golden(W):
     g = load("codec_tiny.npz")
     pcm = nets.Codec(W, CFG)(g["ids"])
