@@ -143,7 +143,7 @@ __device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
 }
 
 // NT packed 16-column tiles per workgroup (SW: NT/2 interleaved gate/up pairs -> NT/2 output tiles)
-template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false>
+template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false, bool PIPE = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
   static_assert(!LN || XF32, "LayerNorm on load needs fp32 X");
@@ -248,6 +248,59 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   // together); the < U leftover steps go one per wave, so no wave runs a serial tail.
   const int G = len / U, rem = len - G * U;
   const int gb = G * wave / NW, ge = G * (wave + 1) / NW;
+  if constexpr (PIPE && XF32 && !LN) {
+    // Software-pipelined weight stream: group g + 1's weight fragments AND raw X rows are issued
+    // before group g's MFMAs, so a wave always has one group of loads in flight while it computes
+    // (the loads of g are older than those of g + 1, so the in-order vmcnt wait for g leaves g + 1
+    // in flight).  Two register buffers, ping-ponged by unrolling the loop by two groups.
+    bf16x8 w0[U][NT], w1[U][NT];
+    float4 x0[U][RB][2], x1[U][RB][2];
+    auto issue = [&](bf16x8 (&wv)[U][NT], float4 (&xv)[U][RB][2], int ks) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) wv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)(ks + u) * 64);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)(ks + u) * 32);
+          xv[u][r][0] = q[0];
+          xv[u][r][1] = q[1];
+        }
+    };
+    auto compute = [&](bf16x8 (&wv)[U][NT], float4 (&xv)[U][RB][2]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          if (r >= rbeff) continue;
+          const float f[8] = {xv[u][r][0].x, xv[u][r][0].y, xv[u][r][0].z, xv[u][r][0].w,
+                              xv[u][r][1].x, xv[u][r][1].y, xv[u][r][1].z, xv[u][r][1].w};
+          bf16x8 hi, lo;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const __bf16 h = (__bf16)f[j];
+            hi[j] = h;
+            lo[j] = (__bf16)(f[j] - (float)h);
+          }
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hi, wv[u][t], acc[t][r], 0, 0, 0);
+            acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lo, wv[u][t], acc[t][r], 0, 0, 0);
+          }
+        }
+    };
+    int g = gb;
+    if (g < ge) issue(w0, x0, kb + g * U);
+    for (; g + 1 < ge; g += 2) {
+      issue(w1, x1, kb + (g + 1) * U);
+      compute(w0, x0);
+      if (g + 2 < ge) issue(w0, x0, kb + (g + 2) * U);
+      compute(w1, x1);
+    }
+    if (g < ge) compute(w0, x0);
+  } else
   for (int g = gb; g < ge; ++g) {
     const int ks = kb + g * U;
     bf16x8 bv[U][NT];
@@ -435,6 +488,24 @@ template <int NT, int RB, bool XF32, int NW, int U, bool SW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
   gemm_body<NT, RB, XF32, NW, U, SW>(a);
 }
+template <int NT, int RB, int NW, int U, bool SW>
+__global__ __launch_bounds__(NW * 64) void k_gemm_wpipe(GemmArgs a) {
+  gemm_body<NT, RB, true, NW, U, SW, false, true>(a);
+}
+
+// Software-pipelined one-row-tile fp32-X weight stream (k_gemm_wpipe).  Mode: 0 = plain loops
+// everywhere; 1 / 2 = every such GEMM pipelined with U / 2 k-steps per group (sweeps); 3 = the
+// measured policy in fo_gemm (default).  -1 = not set yet: FO_GEMM_PIPE (0-3) decides at first use.
+int g_pipe = -1;
+inline int pipe_mode() {
+  if (g_pipe < 0) {
+    const char* e = getenv("FO_GEMM_PIPE");
+    g_pipe = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
+  }
+  return g_pipe;
+}
+// the pipelining fo_gemm chose for the launch it is issuing (0 none, 1 U-step, 2 two-step groups)
+thread_local int g_launch_pipe = 0;
 template <int NT, int RB, int NW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
   gemm_body<NT, RB, true, NW, 4, false, true>(a);
@@ -443,6 +514,13 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
 template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
   const size_t shm = 0;
+  if constexpr (RB == 1) {
+    if (wstream && x_f32 && g_launch_pipe) {
+      if (g_launch_pipe == 2) hipLaunchKernelGGL((k_gemm_wpipe<NT, RB, NW, 2, SW>), grid, dim3(NW * 64), shm, s, a);
+      else hipLaunchKernelGGL((k_gemm_wpipe<NT, RB, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
+      return;
+    }
+  }
   if (wstream) {
     if (x_f32) hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
     else hipLaunchKernelGGL((k_gemm_wstream<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
@@ -457,8 +535,13 @@ thread_local int g_force_nw = 0, g_force_nt = 0;
 
 template <int NT, int RB, bool SW>
 void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
-  if (nw == 16) launch_gemm<NT, RB, 16, 4, SW>(wstream, x_f32, grid, a, s);
-  else if (nw == 8) launch_gemm<NT, RB, 8, 4, SW>(wstream, x_f32, grid, a, s);
+  if constexpr (NT == 8) {  // 8 tiles x 16 waves exceeds the 128-VGPR budget of a 1024-thread group
+    if (nw == 16) nw = 8;
+  } else if (nw == 16) {
+    launch_gemm<NT, RB, 16, 4, SW>(wstream, x_f32, grid, a, s);
+    return;
+  }
+  if (nw == 8) launch_gemm<NT, RB, 8, 4, SW>(wstream, x_f32, grid, a, s);
   else launch_gemm<NT, RB, 4, 4, SW>(wstream, x_f32, grid, a, s);
 }
 
@@ -606,6 +689,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   // cover more output columns read X fewer times per weight byte (measured, gemm_sweep.py)
   int NT = swiglu ? 2 : 1;
   int S_auto = 0;
+  int launch_pipe = 0, nw_pref = 0;
   const int KS = K >> 5;
   if (mid) {
     NT = big_w ? (a.ntiles % 4 == 0 ? 4 : 2) : (swiglu ? 2 : 1);
@@ -617,8 +701,23 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     else if (KS >= 256 && a.ntiles >= 128) { NT = 4; S_auto = 4; }
     else if (KS >= 128 && a.ntiles <= 64) S_auto = 4;  // narrow long-K (TTS down): 10.9 -> 8.2 us in a graph
     else if (a.ntiles > 256) NT = 2;
+    // Pipelined weight stream, 2-step groups (policy measured in the turn bench, A/B twice in one
+    // call: 388-390 -> 383-386 ms/turn, p50 first PCM 50 -> 48.5 ms).  Isolated (scripts/
+    // gemm_gu_sweep.py, gemm_pipe_ab.py; two alternating weight copies): gate/up at <= 8 rows on 2
+    // tiles x 8 waves 50.5 -> 44.4 us, down 32.0 -> 29.5 us, lm_head 177 -> 172 us.  Gate/up at 9-16
+    // rows keeps the plain 4-tile loop: pipelined with a 2-way K split it is faster alone (53.8 ->
+    // 51.2 us) but made the pipelined listen stage slower (turn 388 -> 408 ms).
+    const int pm = pipe_mode();
+    if (x_f32 && (long long)a.ntiles * 16 * K >= (32ll << 20) && pm != 0) {
+      if (pm != 3) launch_pipe = pm;
+      else if (!swiglu || M <= 8) launch_pipe = 2;
+      if (pm == 3 && swiglu && M <= 8 && !g_force_nt && !g_force_nw) {
+        NT = 2;
+        nw_pref = 8;
+      }
+    }
     if (g_force_nt) NT = g_force_nt;
-    FO_REQUIRE(NT == 1 || NT == 2 || NT == 4, "fo_gemm: tiles per workgroup %d", NT);
+    FO_REQUIRE(NT == 1 || NT == 2 || NT == 4 || NT == 8, "fo_gemm: tiles per workgroup %d", NT);
     FO_REQUIRE(!swiglu || NT >= 2, "fo_gemm: swiglu needs tile pairs");
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   } else if (RB == 2) {
@@ -685,9 +784,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     // measured (scripts/gemm_sweep.py, MI355X): one workgroup per CU wants 16 waves, a couple per
     // CU 8, many 4; 4 k-steps in flight per wave is the sweet spot everywhere on the hot path
     int nw = wgs <= 160 ? 16 : (wgs <= 256 ? (NT == 1 ? 16 : 8) : ((NT == 4 || wgs >= 1024) ? 4 : 8));
+    if (nw_pref) nw = nw_pref;
     if (g_force_nw) nw = g_force_nw;
+    g_launch_pipe = wstream ? launch_pipe : 0;
     if (swiglu) {
-      if (NT == 4) launch_nw<4, 1, true>(nw, wstream, x_f32, grid, a, stream);
+      if (NT == 8) launch_nw<8, 1, true>(nw, wstream, x_f32, grid, a, stream);
+      else if (NT == 4) launch_nw<4, 1, true>(nw, wstream, x_f32, grid, a, stream);
       else launch_nw<2, 1, true>(nw, wstream, x_f32, grid, a, stream);
     } else {
       if (NT == 4) launch_nw<4, 1, false>(nw, wstream, x_f32, grid, a, stream);
@@ -713,6 +815,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       else launch_gemm<1, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
     }
   }
+  g_launch_pipe = 0;
   if (S > 1) {
     int rc = fo::check_launch("fo_gemm/split");
     if (rc) return rc;
@@ -777,9 +880,15 @@ int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void
 }
 
 // Force (waves, tiles per workgroup) of the M <= 16 kernels on this thread (0 = automatic); sweeps.
+int fo_gemm_set_pipe(int on) {
+  FO_REQUIRE(on >= 0 && on <= 3, "fo_gemm_set_pipe: 0 (off), 1 (U k-steps), 2 (2 k-steps) or 3 (policy)");
+  g_pipe = on;
+  return 0;
+}
+
 int fo_gemm_tune(int nw, int nt) {
   FO_REQUIRE(nw == 0 || nw == 4 || nw == 8 || nw == 16, "fo_gemm_tune: nw must be 0/4/8/16");
-  FO_REQUIRE(nt == 0 || nt == 1 || nt == 2 || nt == 4, "fo_gemm_tune: nt must be 0/1/2/4");
+  FO_REQUIRE(nt == 0 || nt == 1 || nt == 2 || nt == 4 || nt == 8, "fo_gemm_tune: nt must be 0/1/2/4/8");
   g_force_nw = nw;
   g_force_nt = nt;
   return 0;

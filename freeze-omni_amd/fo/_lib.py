@@ -102,6 +102,7 @@ _SIGS = {
     "fo_sample_embed": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int,
                                 c_vp, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp, c_float, c_vp, c_int,
                                 c_vp]),
+    "fo_gemm_set_pipe": (c_int, [c_int]),
     "fo_penalty": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_float, c_vp]),
 }
 

@@ -77,6 +77,11 @@ int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void
                      float* rsum, float* rsumsq, int* sgroups, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
+/* Software-pipelined one-row-tile fp32-X weight-stream GEMMs (M <= 16, >= 32 MB of weights: the next
+ * k-group's weights + X in flight during this group's MFMAs).  3 (default): the measured policy; 0: plain
+ * loops; 1 / 2: every such GEMM pipelined with 4 / 2 k-steps per group (sweeps).  Unset, the
+ * FO_GEMM_PIPE environment variable (0-3) decides. */
+int fo_gemm_set_pipe(int on);
 long long fo_pack_weight_elems(int N, int K);
 int fo_pack_weight(const void* W, int src_bf16, int N, int K, int ldw, void* out, int tile_base, int tile_stride,
                    hipStream_t stream);

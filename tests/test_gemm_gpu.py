@@ -224,3 +224,27 @@ def test_gemm_layernorm_on_load(dev, M, N, K, act, splitk, psplit):
     if act == "relu":
         ref = torch.relu(ref)
     torch.testing.assert_close(y.double(), ref, rtol=5e-5, atol=5e-5)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K,sw", [(8, 18944, 3584, True), (16, 18944, 3584, True), (16, 3584, 18944, False),
+                                      (5, 4608, 3584, False)])
+def test_gemm_pipelined_weight_stream(dev, mode, M, N, K, sw):
+    """k_gemm_wpipe (software-pipelined weight stream, fo_gemm_set_pipe modes 1-3) vs an fp64 reference of
+    the fp32-X GEMM (+ SwiGLU), next to the plain loop (mode 0): same tolerance for every mode."""
+    from fo import _lib
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M + N + K)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    u = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16) if sw else None
+    x = torch.randn(M, K, generator=g)
+    lin = PackedLinear(w.to(dev), swiglu_up=None if u is None else u.to(dev))
+    lib = _lib.load()
+    try:
+        lib.fo_gemm_set_pipe(mode)
+        y = lin(x.to(dev)).cpu().double()
+    finally:
+        lib.fo_gemm_set_pipe(3)
+    a = x.double() @ w.double().t()
+    ref = torch.nn.functional.silu(a) * (x.double() @ u.double().t()) if sw else a
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
