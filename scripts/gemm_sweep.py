@@ -54,4 +54,4 @@ for name, N, K, M, sw in shapes:
     lib.fo_gemm_tune(0, 0)
     res.sort()
     print(f"{name:9s} M={M:2d} N={N:6d} K={K:5d} {lin.nbytes / 1e6:7.1f}MB auto {auto:6.1f}us "
-          f"({lin.nbytes / auto / 1e3:4.2f}TB/s) best: " + " ".join(r for _, r in res[:6]), flush=True)
+          f"({lin.nbytes / auto / 1e6:4.2f} TB/s) best: " + " ".join(r for _, r in res[:6]), flush=True)
