@@ -515,7 +515,7 @@ template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
   const size_t shm = 0;
   if constexpr (RB == 1) {
-    if (wstream && x_f32 && g_launch_pipe) {
+    if (x_f32 && g_launch_pipe) {
       if (g_launch_pipe == 2) hipLaunchKernelGGL((k_gemm_wpipe<NT, RB, NW, 2, SW>), grid, dim3(NW * 64), shm, s, a);
       else hipLaunchKernelGGL((k_gemm_wpipe<NT, RB, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
       return;
@@ -708,7 +708,9 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     // rows keeps the plain 4-tile loop: pipelined with a 2-way K split it is faster alone (53.8 ->
     // 51.2 us) but made the pipelined listen stage slower (turn 388 -> 408 ms).
     const int pm = pipe_mode();
-    if (x_f32 && (long long)a.ntiles * 16 * K >= (32ll << 20) && pm != 0) {
+    if (x_f32 && pm != 0 && pm != 3) {
+      launch_pipe = pm;   // sweeps: every one-row-tile fp32-X GEMM
+    } else if (x_f32 && (long long)a.ntiles * 16 * K >= (32ll << 20) && pm != 0) {
       if (pm != 3) launch_pipe = pm;
       else if (!swiglu || M <= 8) launch_pipe = 2;
       if (pm == 3 && swiglu && M <= 8 && !g_force_nt && !g_force_nw) {
@@ -786,7 +788,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     int nw = wgs <= 160 ? 16 : (wgs <= 256 ? (NT == 1 ? 16 : 8) : ((NT == 4 || wgs >= 1024) ? 4 : 8));
     if (nw_pref) nw = nw_pref;
     if (g_force_nw) nw = g_force_nw;
-    g_launch_pipe = wstream ? launch_pipe : 0;
+    g_launch_pipe = launch_pipe;
     if (swiglu) {
       if (NT == 8) launch_nw<8, 1, true>(nw, wstream, x_f32, grid, a, stream);
       else if (NT == 4) launch_nw<4, 1, true>(nw, wstream, x_f32, grid, a, stream);
