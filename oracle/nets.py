@@ -387,15 +387,15 @@ def apply_penalty(lg, generated, W, penalty):
 
 
 # ============================================================ codec (models/decoder/ticodec/*)
-def conv1d(x, w, b, dilation=1, padding=0):
-    """x [Cin, T], w [Cout, Cin, k] -> [Cout, T']."""
+def conv1d(x, w, b, dilation=1, padding=0, stride=1):
+    """x [Cin, T], w [Cout, Cin, k] -> [Cout, T'] (b may be None)."""
     Cin, T = x.shape
     Cout, _, k = w.shape
     xp = np.pad(x, ((0, 0), (padding, padding)))
-    To = xp.shape[1] - dilation * (k - 1)
-    cols = np.stack([xp[:, j * dilation:j * dilation + To] for j in range(k)], axis=1)  # [Cin, k, To]
+    To = (xp.shape[1] - dilation * (k - 1) - 1) // stride + 1
+    cols = np.stack([xp[:, j * dilation:j * dilation + (To - 1) * stride + 1:stride] for j in range(k)], axis=1)
     y = w.reshape(Cout, Cin * k) @ cols.reshape(Cin * k, To)
-    return (y + b[:, None]).astype(F32)
+    return (y if b is None else y + b[:, None]).astype(F32)
 
 
 def conv_transpose1d(x, w, b, stride, padding):
@@ -451,3 +451,105 @@ class Codec:
 
     def __call__(self, ids, gt=None):
         return self.generate(self.embed(ids), self.global_features(gt))
+
+
+# ============================================================ codec encoder (VQVAE.encode)
+def group_norm(x, G, w, b, eps=1e-6):
+    """torch GroupNorm over x [C, T]: statistics per group of C/G channels x T, then the affine."""
+    C, T = x.shape
+    g = x.reshape(G, -1).astype(np.float64)
+    mu = g.mean(1, keepdims=True)
+    var = g.var(1, keepdims=True)
+    y = ((g - mu) / np.sqrt(var + eps)).reshape(C, T)
+    return (y * w[:, None] + b[:, None]).astype(F32)
+
+
+def vq_nearest(x, E):
+    """Quantizer_module.forward (models/decoder/ticodec/models.py:531-537): rows of x [N, D] to the
+    nearest codebook row by d = |x|^2 + |e|^2 - 2 x.e (argmin, first on ties) -> (ids, E[ids])."""
+    d = (x * x).sum(1, keepdims=True) + (E * E).sum(1)[None] - 2 * (x @ E.T)
+    ids = np.argmin(d, 1)
+    return ids, E[ids]
+
+
+class CodecEncoder:
+    """VQVAE.encode (models/decoder/ticodec/vqvae.py:44-57) = Encoder.forward (models.py:429-522, weight
+    norm removed) + Quantizer.forward (models.py:639-659: residual VQ over `residul_layer` layers of
+    `n_code_groups` groups, then the global-token VQ).  Returns (local ids [T', layers*groups],
+    global ids [global_code_num]) for one waveform [T]."""
+
+    def __init__(self, W, h):
+        self.W, self.h = W, h
+
+    def resblock(self, x, r, k, dil):
+        """ResBlock1 (models.py:59-131): y = conv2(leaky(conv1(leaky(y)))) + y per dilation."""
+        W = self.W
+        for m, d in enumerate(dil):
+            t = conv1d(leaky(x), W[r + f"convs1.{m}.weight"], W[r + f"convs1.{m}.bias"], d, (k * d - d) // 2)
+            t = conv1d(leaky(t), W[r + f"convs2.{m}.weight"], W[r + f"convs2.{m}.bias"], 1, (k - 1) // 2)
+            x = (t + x).astype(F32)
+        return x
+
+    def gte(self, x):
+        """GlobalTokenEncoder (models.py:22-57): 3 x (conv, stride s, no bias, leaky 0.1), mean over
+        time, Linear + leaky 0.1, BatchNorm1d (eval)."""
+        W, p = self.W, "codec.encoder.GlobalTokenEncoder."
+        _, _, _, k, st = self.h["global_feature_conv"]
+        for i in (0, 2, 4):
+            x = leaky(conv1d(x, W[p + f"conv.{i}.weight"], None, 1, (k - st) // 2, st))
+        v = x.mean(1).astype(F32)
+        v = leaky(linear(v[None], W[p + "fn.0.weight"], W[p + "fn.0.bias"])[0])
+        rm, rv = W[p + "fn.2.running_mean"], W[p + "fn.2.running_var"]
+        return ((v - rm) / np.sqrt(rv + F32(1e-5)) * W[p + "fn.2.weight"] + W[p + "fn.2.bias"]).astype(F32)
+
+    def encoder(self, wav):
+        h, W, p = self.h, self.W, "codec.encoder."
+        x = conv1d(np.asarray(wav, F32)[None], W[p + "conv_pre.weight"], W[p + "conv_pre.bias"], 1, 3)
+        nk = len(h["resblock_kernel_sizes"])
+        stages = list(reversed(list(zip(h["upsample_rates"], h["upsample_kernel_sizes"]))))
+        ks = list(reversed(h["resblock_kernel_sizes"]))
+        ds = list(reversed(h["resblock_dilation_sizes"]))
+        gfeat = None
+        for i, (u, k) in enumerate(stages):
+            x = leaky(x)
+            x = conv1d(x, W[p + f"ups.{i}.weight"], W[p + f"ups.{i}.bias"], 1, (k - u) // 2, u)
+            C = x.shape[0]
+            xs = None
+            for j in range(nk):
+                r = f"{p}resblocks.{i * nk + j}."
+                y = self.resblock(x, r, ks[j], ds[j])
+                xs = y if xs is None else (xs + y).astype(F32)
+                n = f"{p}normalize.{i * nk + j}."
+                xs = group_norm(xs, C // 16, W[n + "weight"], W[n + "bias"])
+            x = (xs / F32(nk)).astype(F32)
+            if i == len(stages) // 2 - 1:
+                gfeat = self.gte(x)
+        x = leaky(x, 0.01)   # F.leaky_relu default slope (models.py:496)
+        return conv1d(x, W[p + "conv_post.weight"], W[p + "conv_post.bias"], 1, 1), gfeat
+
+    def quantize(self, c, gfeat):
+        h, W, q = self.h, self.W, "codec.quantizer."
+        G = h["n_code_groups"]
+        names = ["quantizer_modules", "quantizer_modules2", "quantizer_modules3", "quantizer_modules4"]
+        res = c.T.astype(F32)                     # [T', 512]
+        local = []
+        for li in range(h["residul_layer"]):
+            parts = np.split(res, G, axis=1)
+            zq = []
+            for g, xg in enumerate(parts):
+                ids, z = vq_nearest(xg, W[q + f"{names[li]}.{g}.embedding.weight"])
+                local.append(ids)
+                zq.append(z)
+            z = np.concatenate(zq, 1)
+            quant = (res + (z - res)).astype(F32)  # straight-through form, rounded as the reference's
+            res = (res - quant).astype(F32)
+        gn = h["global_code_num"]
+        gids = []
+        for g, xg in enumerate(np.split(gfeat[None], gn, axis=1)):
+            ids, _ = vq_nearest(xg, W[q + f"quantizer_modules_globaltokens.{g}.embedding.weight"])
+            gids.append(int(ids[0]))
+        return np.stack(local, -1), np.array(gids)
+
+    def __call__(self, wav):
+        c, g = self.encoder(wav)
+        return self.quantize(c, g)

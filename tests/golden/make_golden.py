@@ -397,6 +397,48 @@ def gold_tts_penalty(cfg):
     np.savez_compressed(os.path.join(HERE, "tts_penalty_tiny.npz"), **out)
 
 
+CODEC_ENC_JSON = {"resblock": "1", "upsample_rates": [5, 3, 2, 2], "upsample_kernel_sizes": [10, 6, 4, 4],
+                  "upsample_initial_channel": 256, "resblock_kernel_sizes": [3, 5],
+                  "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5]], "n_codes": 60, "n_code_groups": 1,
+                  "residul_layer": 2, "global_code_num": 8, "codebook_loss_lambda": 1.0,
+                  "commitment_loss_lambda": 0.25, "global_feature_conv": [128, 64, 128, 3, 2]}
+
+
+def gold_codec_encoder(seed):
+    """VQVAE.encode (models/decoder/ticodec/vqvae.py:44-57): Encoder (models.py:429-522, weight norm
+    removed) + Quantizer.forward (models.py:531-659, residual VQ over 2 layers + global tokens) on
+    2400 samples of synthetic 24 kHz audio.  The Encoder's 32*2^i channel ladder ends in conv_post(512,
+    512), so it needs 4 stages; this config (60x down, GlobalTokenEncoder after stage 1) provides them."""
+    from models.decoder.ticodec.models import Encoder, Quantizer
+    from models.decoder.ticodec.vqvae import VQVAE, AttrDict
+    h = AttrDict(CODEC_ENC_JSON)
+    vq = VQVAE.__new__(VQVAE)
+    torch.nn.Module.__init__(vq)
+    vq.h = h
+    vq.quantizer = Quantizer(h)
+    vq.encoder = Encoder(h)
+    vq.encoder.remove_weight_norm()
+    init_module(vq.quantizer, seed, "codec.quantizer.")
+    init_module(vq.encoder, seed, "codec.encoder.")
+    vq.eval()
+    shapes = {**{"codec.quantizer." + k: list(v.shape) for k, v in vq.quantizer.state_dict().items()},
+              **{"codec.encoder." + k: list(v.shape) for k, v in vq.encoder.state_dict().items()}}
+    r = np.random.default_rng(21)
+    n = np.arange(2 * 2400)
+    wav = (0.3 * np.sin(2 * np.pi * 180 * n / 24000) * (1 + 0.5 * np.sin(2 * np.pi * 3 * n / 24000))
+           + 0.05 * r.standard_normal(n.size)).astype(np.float32).reshape(2, 2400)
+    wav[1] *= 0.5
+    with torch.no_grad():
+        c, gfeat = vq.encoder(torch.from_numpy(wav).unsqueeze(1))
+        local, gst = vq.encode(torch.from_numpy(wav))
+    np.savez_compressed(os.path.join(HERE, "codec_encoder_tiny.npz"), wav=wav, enc_out=c.numpy(),
+                        global_features=gfeat.numpy(), local_tokens=local.numpy(), global_tokens=gst.numpy())
+    with open(os.path.join(HERE, "codec_encoder_tiny.json"), "w") as f:
+        json.dump({"codec_json": CODEC_ENC_JSON, "seed": seed, "shapes": shapes}, f)
+    print("codec encoder: c", tuple(c.shape), "local", tuple(local.shape), local[0, :8, :].tolist(),
+          "global", gst.tolist())
+
+
 def gold_codec(cfg, tts_model):
     from models.decoder.ticodec.models import Generator, Quantizer
     from models.decoder.ticodec.vqvae import VQVAE, AttrDict
@@ -483,6 +525,7 @@ def main():
     m = gold_tts(cfg)
     gold_codec(cfg, m)
     gold_tts_penalty(cfg)
+    gold_codec_encoder(cfg["seed"])
     gold_text()
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
         json.dump(SHAPES, f)
@@ -494,5 +537,8 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["tts_penalty"]:   # regenerate only that fixture
         install_shims()
         gold_tts_penalty(C.get("tiny"))
+    elif sys.argv[1:] == ["codec_encoder"]:
+        install_shims()
+        gold_codec_encoder(C.get("tiny")["seed"])
     else:
         main()

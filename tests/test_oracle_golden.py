@@ -161,3 +161,20 @@ def test_llm2tts_run_matches_golden(W):
     assert len(segs) == int(g["n"])
     for i, s in enumerate(segs):
         np.testing.assert_allclose(s, g[f"seg{i}"], atol=3e-5, rtol=1e-3)
+
+
+def test_codec_encoder_matches_golden():
+    """VQVAE.encode (Encoder + residual/global VQ) restated in numpy vs the reference run on the same
+    counter-hash weights (tests/golden/codec_encoder_tiny.*): encoder output, global features, ids."""
+    import json
+    from oracle.weights import SynthCheckpoint
+    meta = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "codec_encoder_tiny.json")))
+    g = load("codec_encoder_tiny.npz")
+    enc = nets.CodecEncoder(SynthCheckpoint(meta["seed"], meta["shapes"]), meta["codec_json"])
+    for b in range(g["wav"].shape[0]):
+        c, gf = enc.encoder(g["wav"][b])
+        np.testing.assert_allclose(c, g["enc_out"][b], atol=1e-5, rtol=1e-4)
+        np.testing.assert_allclose(gf, g["global_features"][b], atol=1e-5, rtol=1e-4)
+        loc, gids = enc.quantize(c, gf)
+        np.testing.assert_array_equal(loc, g["local_tokens"][b])
+        np.testing.assert_array_equal(gids, g["global_tokens"][b, 0])
