@@ -103,6 +103,11 @@ _SIGS = {
                                 c_vp, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp, c_float, c_vp, c_int,
                                 c_vp]),
     "fo_gemm_set_pipe": (c_int, [c_int]),
+    "fo_conv1d_ex": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                             c_vp, c_int, c_vp]),
+    "fo_group_norm": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_float, c_float, c_vp, c_vp]),
+    "fo_gte_head": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
+    "fo_vq_nearest": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp]),
     "fo_penalty": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_float, c_vp]),
 }
 

@@ -157,3 +157,103 @@ class CodecEngine:
         out = torch.empty(B, 1, L, dtype=F32, device=dev)
         ops.conv1d(x, B, C, L, w, b, 1, 7, 1, 3, out, pre_leaky=0.1, post_tanh=True)
         return out.view(B, L)
+
+
+class CodecEncoderEngine:
+    """VQVAE.encode (models/decoder/ticodec/vqvae.py:44-57) on fo_codec_enc.hip: Encoder.forward
+    (models/decoder/ticodec/models.py:429-522; weight norm removed at load, as Encoder.remove_weight_norm)
+    then Quantizer.forward (models.py:639-659).  wav [B, T] fp32 (24 kHz) -> (local ids [B, T', L*G] int32,
+    global ids [B, 1, global_code_num] int32), the reference's encode() layout."""
+
+    def __init__(self, src, codec_json, device):
+        self.h, self.device = codec_json, torch.device(device)
+        self.src = src
+        self.p = "codec.encoder."
+        rates, ks = codec_json["upsample_rates"], codec_json["upsample_kernel_sizes"]
+        self.stages = list(reversed(list(zip(rates, ks))))
+        self.rk = list(reversed(codec_json["resblock_kernel_sizes"]))
+        self.rd = list(reversed(codec_json["resblock_dilation_sizes"]))
+        assert codec_json["resblock"] == "1", "ResBlock1 encoders only (the TiCodec configs use resblock '1')"
+        assert 32 * 2 ** len(self.stages) == 512, "Encoder channel ladder must end at conv_post's 512"
+        self._w = {}
+
+    def w(self, name):
+        if name not in self._w:
+            self._w[name] = self.src.get(self.p + name if not name.startswith("codec.") else name).contiguous()
+        return self._w[name]
+
+    def _conv(self, x, B, Cin, T, name, stride=1, dil=1, pad=0, pre=None, out=None, residual=False, bias=True):
+        wt = self.w(name + ".weight")
+        Cout, _, K = wt.shape
+        To = (T + 2 * pad - dil * (K - 1) - 1) // stride + 1
+        if out is None:
+            out = torch.empty(B, Cout, To, dtype=F32, device=self.device)
+        ops.conv1d_ex(x, B, Cin, T, wt, self.w(name + ".bias") if bias else None, Cout, K, stride, dil, pad, pre, out,
+                      residual)
+        return out, Cout, To
+
+    def encoder(self, wav):
+        B, T = wav.shape
+        x, C, L = self._conv(wav.contiguous(), B, 1, T, "conv_pre", pad=3)
+        nk = len(self.rk)
+        gfeat = None
+        for i, (u, k) in enumerate(self.stages):
+            x, C, L = self._conv(x, B, C, L, f"ups.{i}", stride=u, pad=(k - u) // 2, pre=0.1)
+            xs = torch.empty_like(x) if nk > 0 else None
+            for j in range(nk):
+                y = x.clone()
+                r = f"resblocks.{i * nk + j}."
+                kk = self.rk[j]
+                t1 = torch.empty_like(x)
+                for m, d in enumerate(self.rd[j]):
+                    self._conv(y, B, C, L, r + f"convs1.{m}", dil=d, pad=(kk * d - d) // 2, pre=0.1, out=t1)
+                    self._conv(t1, B, C, L, r + f"convs2.{m}", pad=(kk - 1) // 2, pre=0.1, out=y, residual=True)
+                if j == 0:
+                    xs.copy_(y)
+                else:
+                    ops.axpy_(xs, y)
+                n = f"normalize.{i * nk + j}."
+                ops.group_norm(xs, B, C, L, C // 16, self.w(n + "weight"), self.w(n + "bias"), 1e-6,
+                               1.0 / nk if j == nk - 1 else 1.0, xs)
+            x = xs
+            if i == len(self.stages) // 2 - 1:
+                gfeat = self.gte(x, B, C, L)
+        out, C, L = self._conv(x, B, C, L, "conv_post", pad=1, pre=0.01)   # F.leaky_relu default slope
+        return out, gfeat, L
+
+    def gte(self, x, B, C, L):
+        _, _, _, k, st = self.h["global_feature_conv"]
+        g = "GlobalTokenEncoder."
+        for i in (0, 2, 4):
+            # leaky 0.1 after each conv = pre-activation of the next consumer (the last one: fo_gte_head)
+            x, C, L = self._conv(x, B, C, L, g + f"conv.{i}", stride=st, pad=(k - st) // 2, bias=False,
+                                 pre=None if i == 0 else 0.1)
+        out = torch.empty(B, C, dtype=F32, device=self.device)
+        ops.gte_head(x, B, C, L, self.w(g + "fn.0.weight"), self.w(g + "fn.0.bias"), self.w(g + "fn.2.running_mean"),
+                     self.w(g + "fn.2.running_var"), self.w(g + "fn.2.weight"), self.w(g + "fn.2.bias"), 1e-5, out)
+        return out
+
+    def encode(self, wav):
+        wav = torch.as_tensor(wav)
+        if wav.dim() == 3 and wav.shape[-1] == 1:
+            wav = wav.squeeze(-1)
+        wav = wav.to(self.device, F32).contiguous()
+        B = wav.shape[0]
+        c, gfeat, L = self.encoder(wav)
+        h = self.h
+        G, layers = h["n_code_groups"], h["residul_layer"]
+        D = 512 // G
+        names = ["quantizer_modules", "quantizer_modules2", "quantizer_modules3", "quantizer_modules4"]
+        local = torch.empty(B, L, layers * G, dtype=I32, device=self.device)
+        res = c   # residual, updated in place
+        for li in range(layers):
+            for g in range(G):
+                cb = self.w(f"codec.quantizer.{names[li]}.{g}.embedding.weight")
+                ops.vq_nearest(res, B, 512, L, g * D, D, cb, local, layers * G, li * G + g, residual=True)
+        gn = h["global_code_num"]
+        gids = torch.empty(B, 1, gn, dtype=I32, device=self.device)
+        for g in range(gn):
+            cb = self.w(f"codec.quantizer.quantizer_modules_globaltokens.{g}.embedding.weight")
+            ops.vq_nearest(gfeat, B, gfeat.shape[1], 1, g * (gfeat.shape[1] // gn), gfeat.shape[1] // gn, cb, gids, gn,
+                           g, residual=False)
+        return local, gids

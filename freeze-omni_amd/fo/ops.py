@@ -495,6 +495,32 @@ def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0,
     return out_ids
 
 
+def conv1d_ex(x, B, Cin, Tin, w, bias, Cout, K, stride, dil, pad, pre_leaky, out, residual=False):
+    """Channel-first conv [B][Cin][Tin] -> out [B][Cout][Tout] (fp32 weights [Cout][Cin][K])."""
+    _lib.call("fo_conv1d_ex", x.data_ptr(), B, Cin, Tin, w.data_ptr(), ptr(bias), Cout, K, stride, dil, pad,
+              0 if pre_leaky is None else 1, 0.0 if pre_leaky is None else float(pre_leaky), out.data_ptr(),
+              1 if residual else 0, stream(x.device))
+    return out
+
+
+def group_norm(x, B, C, T, G, w, b, eps, scale, out):
+    _lib.call("fo_group_norm", x.data_ptr(), B, C, T, G, w.data_ptr(), b.data_ptr(), float(eps), float(scale),
+              out.data_ptr(), stream(x.device))
+    return out
+
+
+def gte_head(x, B, C, T, lw, lb, rm, rv, bw, bb, eps, out):
+    _lib.call("fo_gte_head", x.data_ptr(), B, C, T, lw.data_ptr(), lb.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+              bw.data_ptr(), bb.data_ptr(), float(eps), out.data_ptr(), stream(x.device))
+    return out
+
+
+def vq_nearest(x, B, Ctot, T, ch0, D, codebook, ids, ids_ld, ids_col, residual=False):
+    _lib.call("fo_vq_nearest", x.data_ptr(), B, Ctot, T, ch0, D, codebook.data_ptr(), codebook.shape[0],
+              ids.data_ptr(), ids_ld, ids_col, 1 if residual else 0, stream(x.device))
+    return ids
+
+
 def penalty(logits, V, ids, win, step, penalty, B=None):
     """Repetition penalty (models/decoder/decoder.py:348-351) in place on logits [B, >=V]: stores this
     step's input ids into the ring win [B, W] at step % W, then divides each windowed id's logit."""

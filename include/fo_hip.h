@@ -192,6 +192,24 @@ int fo_conv_post_cl(const float* x, int B, int T, int C, const void* w, const fl
 /* llm2TTS.find_min_sum_index window search (models/decoder/llm2tts.py:70-112): res = {min_sum, cut} */
 int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s);
 
+/* ---------------------------------------------------------------- codec encoder (fo_codec_enc.hip)
+ * VQVAE.encode (models/decoder/ticodec/vqvae.py:44-57).  Channel-first fp32 [B][C][T], fp32 weights. */
+/* Conv1d with stride / dilation / zero padding, optional leaky pre-activation (slope) and += into out
+ * (Encoder.conv_pre / ups / ResBlock1 convs / conv_post, GlobalTokenEncoder convs; models.py:22-166,429-498) */
+int fo_conv1d_ex(const float* x, int B, int Cin, int Tin, const float* w, const float* bias, int Cout, int K,
+                 int stride, int dil, int pad, int pre_act, float slope, float* out, int residual, hipStream_t s);
+/* torch.nn.GroupNorm(G, C, eps) with affine, then * scale (Encoder.normalize, models.py:466-467,483-489) */
+int fo_group_norm(const float* x, int B, int C, int T, int G, const float* w, const float* bias, float eps,
+                  float scale, float* out, hipStream_t s);
+/* GlobalTokenEncoder tail (models.py:32-57): leaky 0.1 of the last conv's output, mean over T, Linear + leaky 0.1, BatchNorm1d eval -> out [B][C] */
+int fo_gte_head(const float* x, int B, int C, int T, const float* lw, const float* lb, const float* rm,
+                const float* rv, const float* bw, const float* bb, float bn_eps, float* out, hipStream_t s);
+/* Quantizer_module.forward (models.py:531-537) on channels [ch0, ch0+D) of every (b, t):
+ * argmin_j (|x|^2 + |e_j|^2) - 2 x.e_j -> ids[(b*T+t)*ids_ld + ids_col]; residual: x -= x + (e - x)
+ * (Quantizer.for_one_step / forward, models.py:583-645) */
+int fo_vq_nearest(float* x, int B, int Ctot, int T, int ch0, int D, const float* codebook, int n_codes, int* ids,
+                  int ids_ld, int ids_col, int residual, hipStream_t s);
+
 /* ---------------------------------------------------------------- sampling (fo_sample.hip) */
 /* AudioLLM._post_decode (models/audioLLM.py:431-477) / decoder top-k (models/decoder/decoder.py:353-359).
  * Draws come from a counter stream keyed by (seed, key[row] or row, step[row]). */
