@@ -185,6 +185,9 @@ def reference_state(model_path, llm_path=None, cfg=None):
             raise KeyError(f"codec/final.pt has no '{part}' entry")
         for k, v in _fold_weight_norm(ck[part]).items():
             state[f"codec.{part}.{k}"] = v
+    if "encoder" in ck:  # VQVAE(with_encoder=True) (vqvae.py:33-35): weight norm folded as the generator's
+        for k, v in _fold_weight_norm(ck["encoder"]).items():
+            state[f"codec.encoder.{k}"] = v
     return state
 
 
