@@ -99,6 +99,8 @@ _SIGS = {
     "fo_silence_cut": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int, c_vp,
                           c_vp, c_vp]),
+    "fo_sample_probs": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int,
+                                c_vp, c_vp, c_int, c_vp]),
     "fo_sample_embed": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int,
                                 c_vp, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp, c_float, c_vp, c_int,
                                 c_vp]),

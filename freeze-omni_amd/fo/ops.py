@@ -495,6 +495,18 @@ def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0,
     return out_ids
 
 
+def sample_probs(logits, V, out_ids, probs, top_k=None, temperature=None, top_p=None, seed=0, step=None, B=None,
+                 ban_id=-1, key=None):
+    """sample() that also writes each row's sampling distribution (the reference's pre-multinomial probs)
+    into probs [B, >=V] fp32."""
+    B = logits.shape[0] if B is None else B
+    assert probs.dtype == F32 and probs.is_contiguous() and probs.shape[0] >= B and probs.shape[1] >= V
+    _lib.call("fo_sample_probs", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), probs.data_ptr(),
+              probs.stride(0), stream(logits.device))
+    return out_ids
+
+
 def conv1d_ex(x, B, Cin, Tin, w, bias, Cout, K, stride, dil, pad, pre_leaky, out, residual=False):
     """Channel-first conv [B][Cin][Tin] -> out [B][Cout][Tout] (fp32 weights [Cout][Cin][K])."""
     _lib.call("fo_conv1d_ex", x.data_ptr(), B, Cin, Tin, w.data_ptr(), ptr(bias), Cout, K, stride, dil, pad,

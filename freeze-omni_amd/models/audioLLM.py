@@ -129,16 +129,20 @@ class AudioLLM:
         return out
 
     # ------------------------------------------------------------------ models/audioLLM.py:431-477
-    def _post_decode(self, output, temperature=1.0, top_k=0, top_p=0.0):
-        """Sample one token id from logits [1, 1, V] with the reference's temperature / top-k /
-        top-p rule (fo_sample kernel; top_k in 1..64 on this path, 0 means argmax)."""
+    def _post_decode(self, output, temperature=1.0, top_k=0, top_p=0.0, seed=None):
+        """Sample one token id from logits [1, 1, V] with the reference's rule (models/audioLLM.py:
+        431-477): temperature, top_k > 0 keeps the k largest (0 = no top-k filtering: the whole
+        vocabulary), top_p > 0 the nucleus, then one draw (fo_sample).  The draw comes from the
+        kernel's counter stream: `seed` pins it, otherwise each call takes the next stream."""
         lg = torch.as_tensor(output).reshape(1, -1).to(self.device, F32).contiguous()
         V = lg.shape[1]
-        k = top_k if top_k > 0 else 1
+        if seed is None:
+            self._draws = getattr(self, "_draws", 0) + 1
+            seed = self._draws
         out = torch.empty(1, dtype=I32, device=self.device)
-        ops.sample(lg, V, out, torch.tensor([k], dtype=I32).to(self.device),
+        ops.sample(lg, V, out, torch.tensor([int(top_k)], dtype=I32).to(self.device),
                    torch.tensor([temperature], dtype=F32).to(self.device),
-                   torch.tensor([top_p], dtype=F32).to(self.device))
+                   torch.tensor([top_p], dtype=F32).to(self.device), seed=seed)
         return out.view(1, 1).long()
 
     # ------------------------------------------------------------------ A17: text decode step

@@ -216,6 +216,12 @@ int fo_vq_nearest(float* x, int B, int Ctot, int T, int ch0, int D, const float*
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
               const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
               int* out_ids, float* out_maxlogit, hipStream_t s);
+/* fo_sample that also writes each row's sampling distribution -- the `probs` _post_decode hands to
+ * torch.multinomial (models/audioLLM.py:455-476) -- to probs[row * ldp + i] (ldp >= V).  top_k 0 (no
+ * top-k, the reference default) and top_k > 64 take a whole-vocabulary radix-select path. */
+int fo_sample_probs(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
+                    const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
+                    int* out_ids, float* probs, int ldp, hipStream_t s);
 /* fo_sample fused with the next AR decode step's input (models/decoder/decoder.py:341-346: embed(id) ->
  * first LlamaRMSNorm): hist[hist_row[0] * hist_ld + row] = id (hist nullable), x[row] = emb[id] (bf16
  * table -> fp32), h[row] = RMSNorm(x[row]) * gamma. */

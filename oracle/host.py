@@ -28,6 +28,35 @@ def find_min_sum_index(buffer, syn, N=2401, threshold=0.01):
     return np.concatenate([buffer, arr]).astype(F32), None
 
 
+def post_decode_probs(logits, temperature=1.0, top_k=0, top_p=0.0):
+    """The distribution AudioLLM._post_decode draws its token from (models/audioLLM.py:431-477), i.e. the
+    `probs` handed to torch.multinomial: softmax(logits / T); top_k > 0 keeps the k largest and
+    renormalises; top_p > 0 sorts descending, removes entries whose inclusive cumsum exceeds top_p -- but
+    shifts that mask right by one (always keeping the first) only when the first entry alone exceeds
+    top_p -- and renormalises.  float32 like the reference; ties keep the lower index."""
+    x = np.asarray(logits, F32).reshape(-1)
+    if temperature != 1.0:
+        x = (x / F32(temperature)).astype(F32)
+    e = np.exp((x - x.max()).astype(F32)).astype(F32)
+    p = (e / e.sum(dtype=F32)).astype(F32)
+    if top_k > 0:
+        keep = np.argsort(-p, kind="stable")[:top_k]
+        q = np.zeros_like(p)
+        q[keep] = p[keep]
+        p = (q / q.sum(dtype=F32)).astype(F32)
+    if top_p > 0.0:
+        order = np.argsort(-p, kind="stable")
+        cs = np.cumsum(p[order], dtype=F32)
+        remove = cs > F32(top_p)
+        if remove[0]:
+            remove[1:] = remove[:-1].copy()
+            remove[0] = False
+        p = p.copy()
+        p[order[remove]] = 0
+        p = (p / p.sum(dtype=F32)).astype(F32)
+    return p
+
+
 def run_chunking(token_ids, vocoder, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
                  upsample=600):
     """Yield the PCM segments llm2TTS.run emits for a fixed AR token stream; vocoder(ids)->pcm 1-D."""

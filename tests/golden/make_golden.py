@@ -346,6 +346,275 @@ def gold_audiollm(cfg, feats_a):
                         pe0=np.array(pe0), max_len=np.array(enc.enc[1].pe.max_len))
 
 
+def build_audiollm(cfg):
+    """The reference AudioLLM (models/utils.py:init_encoder_llm) on a tiny local Qwen2, every parameter
+    from the counter hash (keyed by the canonical state_dict names), chat-prefix embeds initialised."""
+    import tempfile
+    sys.argv = ["golden"]
+    from models.utils import init_encoder_llm
+    from models.encoder.cmvn import GlobalCMVN
+    llm_dir = tiny_llm_dir(cfg, tempfile.mkdtemp())
+    ty = copy.deepcopy(cfg["train_yaml"])
+    ty["cmvn_file"] = None
+    ty["model_conf"]["llm_path"] = llm_dir
+    model = init_encoder_llm(ty, device="cpu")
+    for enc in (model.encoder_user, model.encoder_system):
+        enc.global_cmvn = GlobalCMVN(torch.zeros(80), torch.ones(80))
+    sd = model.state_dict()
+    model.load_state_dict({k: v if v.dtype == torch.long else
+                           torch.from_numpy(synth_param(cfg["seed"], canonical_llm_name(k), tuple(v.shape),
+                                                        cfg["overrides"])) for k, v in sd.items()})
+    model.eval()
+    model.init_template_compilation = lambda: None
+    model.system_chat_prefix_embeds, model.system_chat_prefix_mask = model.initialize_chat_template_embeds("system")
+    model.user_chat_prefix_embeds, model.user_chat_prefix_mask = model.initialize_chat_template_embeds("user")
+    return model
+
+
+def _capture_hooks(model, cap):
+    """Record the LLM input embeds / last hidden and the encoder output of every recognize call."""
+    orig_core = model._llm_forward_core
+
+    def core(inputs):
+        cap["embeds"] = inputs["inputs_embeds"].float().numpy().copy()
+        h, pkv = orig_core(inputs)
+        cap["hidden"] = h.float().numpy().copy()
+        return h, pkv
+
+    model._llm_forward_core = core
+    for ident in ("user", "system"):
+        enc = getattr(model, f"encoder_{ident}")
+
+        def infer(*a, _o=enc.infer, **k):
+            r = _o(*a, **k)
+            cap["enc"] = r[0].float().numpy().copy()
+            return r
+
+        enc.infer = infer
+
+
+def framing_b_feats(n, seed):
+    """n consecutive [32, 80] framing-B features from the reference AudioFeatureGating
+    (models/AudioFeatureGating.py:54-75, configs/dialog_state_pred_config.yaml) on synthetic PCM."""
+    import yaml
+    from models.AudioFeatureGating import AudioFeatureGating
+    ycfg = yaml.safe_load(open(os.path.join(REF, "configs/dialog_state_pred_config.yaml")))
+    g = AudioFeatureGating(16000, 10, 0, ycfg["audio_feature_gating"]["fbank"])
+    CB = g.expected_frames_per_audio_chunk
+    pcm = synth_pcm(CB * n, seed)
+    feats = [g._extract_fbank(pcm[i * CB:(i + 1) * CB].astype(np.float32)).numpy()[0].copy() for i in range(n)]
+    return pcm.astype(np.float32), np.stack(feats).astype(np.float32)
+
+
+def gold_audiollm_b(cfg):
+    """AudioLLM.recognize on FRAMING-B features ([1, 32, 80], the duplex path of config 5:
+    bin/dialog_state_pred.py:777-844 -> models/pipeline.py:36-88): 7 encoder frames per chunk, the
+    odd-length adapter step, 'ipu_sl' chat prefixes on both identities, system audio prefilled without
+    prediction.  Captures encoder output, LLM input embeds, hidden, probs, pe_index and kv_len."""
+    model = build_audiollm(cfg)
+    cap = {}
+    _capture_hooks(model, cap)
+    pcm, feats = framing_b_feats(10, 123)
+    extra = {"identity": "", "status": "pre", "past_key_values": None, "adapter_cache": None,
+             "encoder_cache": None, "pe_index": 0, "role_prompt": "<|im_start|>system\nYou are a helpful assistant."}
+    pkv = model.set_system_role(extra)
+    script = [("user", "ipu_sl"), ("user", "ipu_cl"), ("user", "ipu_cl"), ("system", "ipu_sl"), ("system", "ipu_cl"),
+              ("user", "ipu_sl"), ("system", "ipu_cl"), ("user", "ipu_cl"), ("user", "ipu_cl"), ("user", "ipu_el")]
+    caches = {i: {"encoder_cache": None, "adapter_cache": None, "pe_index": 0} for i in ("user", "system")}
+    res = {"role_prompt": extra["role_prompt"], "steps": []}
+    arrays = {"feats": feats, "pcm": pcm}
+    for si, (ident, status) in enumerate(script):
+        x = torch.from_numpy(feats[si]).unsqueeze(0)
+        e = {"identity": ident, "status": status, "past_key_values": pkv, **caches[ident]}
+        probs, pkv, ac, ec, pe = model.recognize(x, e)
+        caches[ident] = {"encoder_cache": ec, "adapter_cache": ac, "pe_index": pe}
+        res["steps"].append({"identity": ident, "status": status, "probs": probs, "pe_index": pe,
+                             "kv_len": int(pkv.get_seq_length()), "enc_frames": int(cap["enc"].shape[1]),
+                             "llm_rows": int(cap["embeds"].shape[1])})
+        arrays[f"s{si}_enc"] = cap["enc"][0]
+        arrays[f"s{si}_embeds"] = cap["embeds"][0]
+        arrays[f"s{si}_hidden"] = cap["hidden"][0]
+    np.savez_compressed(os.path.join(HERE, "audiollm_b_tiny.npz"), **arrays)
+    with open(os.path.join(HERE, "audiollm_b_tiny.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("audiollm framing B: steps", len(script), "enc frames", res["steps"][0]["enc_frames"],
+          "kv_len", res["steps"][-1]["kv_len"])
+
+
+SAMPLER_SETTINGS = [  # (temperature, top_k, top_p) of AudioLLM._post_decode (models/audioLLM.py:431-477)
+    (1.0, 1, 0.0), (1.0, 0, 0.0), (0.7, 0, 0.0), (1.0, 0, 0.9), (1.3, 0, 0.5), (0.6, 0, 0.3), (0.8, 5, 0.0),
+    (1.0, 100, 0.0), (1.2, 100, 0.8), (1.0, 20, 0.95), (1.0, 3, 0.05), (0.9, 64, 0.7), (1.0, 65, 0.0)]
+
+
+def gold_llm_text(cfg):
+    """LLM logits and the text decode, assembled from reference pieces on the tiny
+    AudioLLM: lm_head (Qwen2ForCausalLM.lm_head, models/audioLLM.py:70-74,104-109) on the hidden rows of
+    the audiollm_tiny session; then, from the end of that session, the reconstructed dialog_ss / dialog_cs
+    steps of bin/inference.py:138-179: prefill prefix_for_system_utterance (.half(), full past mask),
+    lm_head on the last row, _post_decode(top_k=1), feed that token's embedding, repeat.  Plus the
+    pre-multinomial `probs` of _post_decode for SAMPLER_SETTINGS on those logits and on synthetic rows."""
+    from models.audioLLM import AudioLLM
+    model = build_audiollm(cfg)
+    g = np.load(os.path.join(HERE, "audiollm_tiny.npz"))
+    meta = json.load(open(os.path.join(HERE, "audiollm_tiny.json")))
+    lm_head = model.llm_decoder.lm_head
+    arrays = {"pre_logits": lm_head(torch.from_numpy(g["pre_hidden"])).numpy()}
+    for si in range(len(meta["steps"])):
+        arrays[f"s{si}_logits"] = lm_head(torch.from_numpy(g[f"s{si}_hidden"])).numpy()
+    # replay the session's context through the reference (embeds from the golden = its own inputs)
+    extra = {"identity": "", "status": "pre", "past_key_values": None, "adapter_cache": None,
+             "encoder_cache": None, "pe_index": 0, "role_prompt": "<|im_start|>system\nYou are a helpful assistant."}
+    pkv = model.set_system_role(extra)
+
+    def forward(embeds, pkv):
+        mask = torch.full([1, pkv.get_seq_length() + embeds.shape[1]], True)
+        h, pkv = model._llm_forward_core({"inputs_embeds": embeds.half(), "attention_mask": mask,
+                                          "past_key_values": pkv})
+        return h, pkv
+
+    for si in range(len(meta["steps"])):
+        h, pkv = forward(torch.from_numpy(g[f"s{si}_embeds"]).unsqueeze(0), pkv)
+        np.testing.assert_allclose(h[0].numpy(), g[f"s{si}_hidden"], atol=1e-5)
+    assert pkv.get_seq_length() == meta["steps"][-1]["kv_len"]
+    wte = model.llm_decoder.transformer.wte
+    ids = model.chat_template["prefix_for_system_utterance"]
+    text_ids, text_logits, text_hidden = [], [], []
+    for step in range(10):
+        h, pkv = forward(wte(ids), pkv)
+        last = h[:, -1:]
+        lg = lm_head(last)
+        tok = int(model._post_decode(lg, temperature=1.0, top_k=1, top_p=0.0).reshape(-1)[0])
+        text_ids.append(tok)
+        text_logits.append(lg[0, 0].numpy().copy())
+        text_hidden.append(last[0, 0].numpy().copy())
+        ids = torch.tensor([[tok]])
+    arrays.update(text_ids=np.array(text_ids, np.int64), text_logits=np.stack(text_logits),
+                  text_hidden=np.stack(text_hidden), kv_len_after=np.array(pkv.get_seq_length()))
+    np.savez_compressed(os.path.join(HERE, "llm_text_tiny.npz"), **arrays)
+    print("llm text: greedy ids", text_ids, "kv", pkv.get_seq_length())
+
+    # _post_decode probability vectors (the distribution torch.multinomial draws from)
+    rng = np.random.default_rng(17)
+    rows = [arrays["text_logits"][0], arrays["text_logits"][3], arrays["s0_logits"][-1],
+            (rng.standard_normal(4096) * 3.0).astype(np.float32),
+            (rng.standard_normal(4096) * 0.7).astype(np.float32)]
+    orig = torch.multinomial
+    probs = np.zeros((len(rows), len(SAMPLER_SETTINGS), 4096), np.float32)
+    toks = np.zeros((len(rows), len(SAMPLER_SETTINGS)), np.int64)
+    try:
+        for ri, lg in enumerate(rows):
+            for si, (T, k, p) in enumerate(SAMPLER_SETTINGS):
+                cap = {}
+
+                def mn(pr, n, **kw):
+                    cap["p"] = pr.detach().clone()
+                    return torch.argmax(pr).view(1)
+
+                torch.multinomial = mn
+                t = AudioLLM._post_decode(None, torch.from_numpy(np.ascontiguousarray(lg)).view(1, 1, -1),
+                                          temperature=T, top_k=k, top_p=p)
+                probs[ri, si, :lg.size] = cap["p"].numpy()
+                toks[ri, si] = int(t.reshape(-1)[0])
+    finally:
+        torch.multinomial = orig
+    np.savez_compressed(os.path.join(HERE, "sampler_tiny.npz"), rows_384=np.stack(rows[:3]),
+                        rows_4096=np.stack(rows[3:]), settings=np.array(SAMPLER_SETTINGS, np.float64),
+                        probs=probs, argmax_of_probs=toks)
+    print("sampler: kept counts", [[int((probs[r, s] > 0).sum()) for s in range(len(SAMPLER_SETTINGS))]
+                                   for r in range(len(rows))])
+
+
+def gold_real_t2(seed=7):
+    """Real-geometry (T2) reference runs with counter-hash weights (configs 'real'), one component at a
+    time so the CPU time stays bounded; only I/O is committed and every consumer regenerates the weights:
+      * speechEncoder.infer (models/encoder/encoder.py:149-155) with 2 of the 24 blocks at d=1024,
+        16 heads, ff 4096, chunk 4 / left 16, framing A (20 chunks: the 64-frame ring fills and trims)
+        and framing B (8 chunks starting 3 chunks before the RelPE wrap at max_len);
+      * CNNSubsampling 1024 -> 3584 (models/adapter.py:112-157) streaming on those encoder outputs;
+      * LLM2TTSCodecAR.infer (models/decoder/decoder.py:314-367): all 4 layers at 896 / 14 heads / 4864,
+        pre_nn + layers_prefix, greedy (top_k=1) 48 tokens, first logits rows;
+      * VQVAE.forward (vqvae.py:37-42): Quantizer.embed + Generator at upsample_initial_channel 512 on
+        one 60-token call (36000 samples)."""
+    import argparse
+    sys.argv = ["golden"]
+    from models.adapter import CNNSubsampling
+    from models.decoder.decoder import LLM2TTSCodecAR
+    from models.decoder.ticodec.models import Generator, Quantizer
+    from models.decoder.ticodec.vqvae import VQVAE, AttrDict
+    from models.encoder.cmvn import GlobalCMVN
+    from models.encoder.encoder import speechEncoder
+    cfg = C.get("real")
+    assert cfg["seed"] == seed
+    ec = cfg["train_yaml"]["encoder_conf"]
+    ec["para_conf"]["transformer"]["transformer-num-blocks"] = 2
+    enc = speechEncoder(80, ec["overview_conf"], ec["para_conf"], GlobalCMVN(torch.zeros(80), torch.ones(80)))
+    init_module(enc, seed, "encoder_user.", cfg["overrides"])
+    enc.eval()
+    mc = cfg["train_yaml"]["model_conf"]
+    ada = CNNSubsampling(mc["enc_out_dim"], mc["llm_embed_dim"], mc["kernel_size"], mc["activation_func"], mc["norm"])
+    init_module(ada, seed, "adpter_user.", cfg["overrides"])
+    ada.eval()
+    fb = np.load(os.path.join(HERE, "fbank.npz"))
+    out = {}
+    tr = enc.enc[1]
+    for kind, n, pe0 in (("A", 20, 0), ("B", 8, tr.pe.max_len - 3 * tr.chunk_size + 1)):
+        feats = fb["A_feats"][np.arange(n) % len(fb["A_feats"])] if kind == "A" else framing_b_feats(n, 321)[1]
+        buf, pe, cc = [None] * tr.num_blocks, pe0, None
+        eo, ao, pes = [], [], []
+        for i in range(n):
+            o, buf, _, _, pe = enc.infer(torch.from_numpy(feats[i]).unsqueeze(0), buf, 0, None, pe)
+            a, _, cc = ada(o, torch.full(o.shape[:2], True).unsqueeze(1), cache=cc, return_cache=True)
+            eo.append(o[0].numpy().copy())
+            ao.append(a[0].numpy().copy())
+            pes.append(pe)
+        out[f"{kind}_feats"] = feats
+        out[f"{kind}_enc"] = np.stack(eo)
+        out[f"{kind}_ada"] = np.stack(ao)
+        out[f"{kind}_pe"] = np.array(pes)
+        out[f"{kind}_pe0"] = np.array(pe0)
+        print(f"T2 encoder {kind}: {n} chunks, enc {out[kind + '_enc'].shape}, adapter {out[kind + '_ada'].shape}")
+    np.savez_compressed(os.path.join(HERE, "real_encoder_t2.npz"), **out)
+
+    idim, odim, args = cfg["decoder_json"]
+    m = LLM2TTSCodecAR(idim, odim, argparse.Namespace(**args))
+    init_module(m, seed, "tts.", cfg["overrides"])
+    m.eval()
+    rng = np.random.default_rng(55)
+    hidden = torch.from_numpy(rng.standard_normal((1, 12, idim)).astype(np.float32) * 0.5)
+    prefix = torch.from_numpy(rng.standard_normal((1, 24, idim)).astype(np.float32) * 0.5)
+    logits = []
+    orig = m.out_fnn.forward
+
+    def hook(x):
+        y = orig(x)
+        if len(logits) < 4:
+            logits.append(y[0, -1].numpy().copy())
+        return y
+
+    m.out_fnn.forward = hook
+    ids = [int(t) for t in m.infer(hidden, 1, prefix, -1, 1.1, max_tokens=48)]
+    m.out_fnn.forward = orig
+    np.savez_compressed(os.path.join(HERE, "real_tts_t2.npz"), hidden=hidden[0].numpy(), prefix=prefix[0].numpy(),
+                        ids=np.array(ids, np.int64), logits=np.stack(logits))
+    print("T2 tts: ids", len(ids), ids[:12])
+
+    h = AttrDict(cfg["codec_json"])
+    vq = VQVAE.__new__(VQVAE)
+    torch.nn.Module.__init__(vq)
+    vq.h = h
+    vq.quantizer = Quantizer(h)
+    vq.generator = Generator(h)
+    vq.generator.remove_weight_norm()
+    init_module(vq.quantizer, seed, "codec.quantizer.")
+    init_module(vq.generator, seed, "codec.generator.")
+    vq.eval()
+    cids = torch.from_numpy(np.random.default_rng(66).integers(0, h.n_codes, size=(1, 60, 1)))
+    gt = torch.tensor(h.global_tokens).unsqueeze(0).unsqueeze(0)
+    pcm = vq(cids, gt)
+    np.savez_compressed(os.path.join(HERE, "real_codec_t2.npz"), ids=cids[0, :, 0].numpy(), pcm=pcm[0, 0].numpy())
+    print("T2 codec: pcm", tuple(pcm.shape))
+
+
 def gold_tts(cfg):
     import argparse
     from models.decoder.decoder import LLM2TTSCodecAR
@@ -527,6 +796,9 @@ def main():
     gold_tts_penalty(cfg)
     gold_codec_encoder(cfg["seed"])
     gold_text()
+    gold_audiollm_b(cfg)
+    gold_llm_text(cfg)
+    gold_real_t2()
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
         json.dump(SHAPES, f)
     total = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith((".npz", ".json")))
@@ -540,5 +812,14 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["codec_encoder"]:
         install_shims()
         gold_codec_encoder(C.get("tiny")["seed"])
+    elif sys.argv[1:] == ["framing_b"]:
+        install_shims()
+        gold_audiollm_b(C.get("tiny"))
+    elif sys.argv[1:] == ["llm_text"]:
+        install_shims()
+        gold_llm_text(C.get("tiny"))
+    elif sys.argv[1:] == ["real_t2"]:
+        install_shims()
+        gold_real_t2()
     else:
         main()

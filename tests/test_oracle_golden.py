@@ -178,3 +178,125 @@ def test_codec_encoder_matches_golden():
         loc, gids = enc.quantize(c, gf)
         np.testing.assert_array_equal(loc, g["local_tokens"][b])
         np.testing.assert_array_equal(gids, g["global_tokens"][b, 0])
+
+
+# ------------------------------------------------------------------ round 2 fixtures
+def _prefix_ids(ident):
+    meta = json.load(open(os.path.join(G, "audiollm_tiny.json")))
+    return meta["user_prefix_ids"] if ident == "user" else meta["system_prefix_ids"]
+
+
+def test_audiollm_framing_b_matches_golden(W):
+    """The duplex (config 5) model path at framing B: [32, 80] features -> 7 encoder frames -> 4 adapter
+    rows (odd-length conv step), 'ipu_sl' prefixes on both identities (tests/golden/audiollm_b_tiny.*)."""
+    meta = json.load(open(os.path.join(G, "audiollm_b_tiny.json")))
+    g = load("audiollm_b_tiny.npz")
+    roles = json.load(open(os.path.join(G, "audiollm_tiny.json")))["role_ids"]
+    llm = nets.Qwen2(W, CFG)
+    kv = nets.KV(CFG["llm"]["num_hidden_layers"])
+    llm.forward(llm.embed(roles), kv)
+    enc = {i: nets.Encoder(W, CFG, i) for i in ("user", "system")}
+    ada = {i: nets.Adapter(W, CFG, i) for i in ("user", "system")}
+    st = {i: {"enc": nets.new_encoder_state(enc[i].nb), "ada": None} for i in ("user", "system")}
+    for si, step in enumerate(meta["steps"]):
+        ident = step["identity"]
+        e = enc[ident].infer(g["feats"][si], st[ident]["enc"])
+        assert e.shape[0] == step["enc_frames"] == 7
+        np.testing.assert_allclose(e, g[f"s{si}_enc"], atol=2e-4, rtol=1e-3)
+        a, st[ident]["ada"] = ada[ident](e, st[ident]["ada"])
+        if step["status"] == "ipu_sl":
+            a = np.concatenate([llm.embed(_prefix_ids(ident)), a], axis=0)
+        assert a.shape[0] == step["llm_rows"]
+        np.testing.assert_allclose(a, g[f"s{si}_embeds"], atol=2e-3, rtol=2e-3)
+        hid = llm.forward(a, kv)
+        np.testing.assert_allclose(hid, g[f"s{si}_hidden"], atol=5e-4, rtol=2e-3)
+        assert st[ident]["enc"]["pe"] == step["pe_index"] and kv.length() == step["kv_len"]
+        if step["probs"] is not None:
+            s1, s2 = nets.state_probs(W, hid)
+            assert abs(s1 - step["probs"]["state_1"]) < 1e-4 and abs(s2 - step["probs"]["state_2"]) < 1e-4
+
+
+def test_llm_logits_and_greedy_text_match_golden(W):
+    """lm_head logits on the reference's hidden rows, and the reconstructed text decode (assistant prefix
+    prefill + greedy tokens) against the reference pieces run end to end (tests/golden/llm_text_tiny.npz)."""
+    g = load("audiollm_tiny.npz")
+    t = load("llm_text_tiny.npz")
+    meta = json.load(open(os.path.join(G, "audiollm_tiny.json")))
+    llm = nets.Qwen2(W, CFG)
+    np.testing.assert_allclose(llm.logits(g["pre_hidden"][0]), t["pre_logits"][0], atol=1e-4, rtol=1e-4)
+    for si in range(len(meta["steps"])):
+        np.testing.assert_allclose(llm.logits(g[f"s{si}_hidden"]), t[f"s{si}_logits"], atol=1e-4, rtol=1e-4)
+    kv = nets.KV(CFG["llm"]["num_hidden_layers"])
+    llm.forward(llm.embed(meta["role_ids"]), kv)
+    for si in range(len(meta["steps"])):
+        llm.forward(g[f"s{si}_embeds"], kv)
+    ids = meta["system_prefix_ids"]
+    for step, want in enumerate(t["text_ids"].tolist()):
+        h = llm.forward(llm.embed(ids), kv)[-1:]
+        lg = llm.logits(h)[0]
+        np.testing.assert_allclose(h[0], t["text_hidden"][step], atol=5e-4, rtol=2e-3)
+        np.testing.assert_allclose(lg, t["text_logits"][step], atol=1e-3, rtol=1e-3)
+        tok = int(np.argmax(host.post_decode_probs(lg, 1.0, 1, 0.0)))
+        assert tok == want
+        ids = [tok]
+    assert kv.length() == int(t["kv_len_after"])
+
+
+def test_post_decode_probs_match_golden():
+    """The pre-multinomial distribution of AudioLLM._post_decode for temperature / top_k (0 = off,
+    k > 64) / top_p (incl. the first-entry-exceeds-top_p shift) against the reference."""
+    s = load("sampler_tiny.npz")
+    rows = list(s["rows_384"]) + list(s["rows_4096"])
+    for ri, lg in enumerate(rows):
+        for si, (T, k, p) in enumerate(s["settings"]):
+            want = s["probs"][ri, si, :lg.size]
+            got = host.post_decode_probs(lg, float(T), int(k), float(p))
+            np.testing.assert_array_equal(got > 0, want > 0)
+            np.testing.assert_allclose(got, want, atol=1e-6, rtol=1e-4)
+
+
+T2 = configs.get("real")
+T2["train_yaml"]["encoder_conf"]["para_conf"]["transformer"]["transformer-num-blocks"] = 2
+
+
+@pytest.fixture(scope="module")
+def W2():
+    shapes = {}
+    shapes.update(audiollm_shapes(T2))
+    shapes.update(tts_shapes(T2))
+    shapes.update(codec_shapes(T2))
+    return SynthCheckpoint(T2["seed"], shapes, T2["overrides"])
+
+
+def test_real_geometry_encoder_adapter_match_golden(W2):
+    """T2: 2 blocks at d=1024 / 16 heads / left 16 + the 1024 -> 3584 adapter, framing A past the ring trim
+    and framing B across the RelPE wrap, against the reference (tests/golden/real_encoder_t2.npz)."""
+    g = load("real_encoder_t2.npz")
+    for kind in ("A", "B"):
+        enc, ada = nets.Encoder(W2, T2, "user"), nets.Adapter(W2, T2, "user")
+        st, ac = nets.new_encoder_state(enc.nb), None
+        st["pe"] = int(g[f"{kind}_pe0"])
+        for i in range(g[f"{kind}_feats"].shape[0]):
+            e = enc.infer(g[f"{kind}_feats"][i], st)
+            a, ac = ada(e, ac)
+            np.testing.assert_allclose(e, g[f"{kind}_enc"][i], atol=5e-4, rtol=1e-3)
+            scale = float(np.abs(g[f"{kind}_ada"][i]).max())
+            np.testing.assert_allclose(a, g[f"{kind}_ada"][i], atol=1e-3 * scale, rtol=1e-3)
+            assert st["pe"] == int(g[f"{kind}_pe"][i])
+
+
+def test_real_geometry_tts_matches_golden(W2):
+    """T2: LLM2TTSCodecAR at 896 / 14 heads / 4864 with all 4 layers + pre_nn + prefix layers, greedy ids
+    exact and first logits rows, against the reference (tests/golden/real_tts_t2.npz)."""
+    g = load("real_tts_t2.npz")
+    dec = nets.TTSDecoder(W2, T2)
+    ids, lgs = dec.infer_greedy(g["hidden"], g["prefix"], max_tokens=48, return_logits=4)
+    assert ids == g["ids"].tolist()
+    np.testing.assert_allclose(np.stack(lgs), g["logits"], atol=2e-4, rtol=1e-3)
+
+
+def test_real_geometry_codec_matches_golden(W2):
+    """T2: one 60-token vocoder call at upsample_initial_channel 512 (36146 samples) vs the reference."""
+    g = load("real_codec_t2.npz")
+    pcm = nets.Codec(W2, T2)(g["ids"])
+    np.testing.assert_allclose(pcm, g["pcm"], atol=2e-5, rtol=1e-3)
