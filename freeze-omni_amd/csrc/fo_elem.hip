@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm(const float* x, int ldx, int D,
 }
 
 __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, int D, const float* w, const float* b,
-                                                   float eps, float* out, int ldo, int relu) {
+                                                   float eps, float* out, int ldo, int act) {
   __shared__ float red[4];
   const float* xr = x + (size_t)blockIdx.x * ldx;
   float* o = out + (size_t)blockIdx.x * ldo;
@@ -70,9 +70,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, int 
   const float var = block_sum<4>(q, red) / (float)D;
   const float r = 1.0f / sqrtf(var + eps);
   for (int i = threadIdx.x; i < D; i += 256) {
-    float v = (xr[i] - mean) * r * w[i] + b[i];
-    if (relu) v = fmaxf(v, 0.f);
-    o[i] = v;
+    o[i] = apply_act((xr[i] - mean) * r * w[i] + b[i], act);
   }
 }
 
@@ -226,9 +224,10 @@ int fo_rmsnorm(const float* x, int ldx, int M, int D, const float* w, float eps,
 }
 
 int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const float* b, float eps, float* out, int ldo,
-                 int relu, hipStream_t s) {
+                 int act, hipStream_t s) {
   FO_REQUIRE(M > 0 && D > 0, "fo_layernorm: bad shape");
-  hipLaunchKernelGGL(k_layernorm, dim3(M), dim3(256), 0, s, x, ldx, D, w, b, eps, out, ldo, relu);
+  FO_REQUIRE(act == FO_ACT_NONE || act == FO_ACT_RELU || act == FO_ACT_GELU, "fo_layernorm: act %d", act);
+  hipLaunchKernelGGL(k_layernorm, dim3(M), dim3(256), 0, s, x, ldx, D, w, b, eps, out, ldo, act);
   return fo::check_launch("fo_layernorm");
 }
 

@@ -144,6 +144,28 @@ def _fold_weight_norm(sd):
     return out
 
 
+def audiollm_state(path):
+    """audiollm/final.pt (models/utils.py:11-20) under the engine's names: 'llm_decoder.*' -> the Qwen2
+    names, upstream 'encoder.*' / 'adpter.*' -> both identities unless the fork's own key is present."""
+    sd = _torch_load(path)
+    if isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
+        sd = sd["model"]
+    fork = {k for k in sd if k.startswith(("encoder_user.", "encoder_system.", "adpter_user.", "adpter_system."))}
+    state = {}
+    for k, v in sd.items():
+        if k.startswith("llm_decoder."):
+            state[k[len("llm_decoder."):]] = v
+        elif k.startswith(("encoder.", "adpter.")):
+            head, rest = k.split(".", 1)
+            for ident in ("user", "system"):
+                nk = f"{head}_{ident}.{rest}"
+                if nk not in fork:
+                    state[nk] = v
+        else:
+            state[k] = v
+    return state
+
+
 def reference_state(model_path, llm_path=None, cfg=None):
     """All tensors under the engine's names (lazy for the LLM shards)."""
     llm_path = llm_path or os.path.join(model_path, "llm")
@@ -157,21 +179,8 @@ def reference_state(model_path, llm_path=None, cfg=None):
         for ident in ("user", "system"):
             state[f"encoder_{ident}.global_cmvn.mean"] = mean
             state[f"encoder_{ident}.global_cmvn.istd"] = istd
-    sd = _torch_load(os.path.join(model_path, "audiollm", "final.pt"))
-    if isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
-        sd = sd["model"]
-    fork = {k for k in sd if k.startswith(("encoder_user.", "encoder_system.", "adpter_user.", "adpter_system."))}
-    for k, v in sd.items():
-        if k.startswith("llm_decoder."):
-            state[k[len("llm_decoder."):]] = v
-        elif k.startswith(("encoder.", "adpter.")):
-            head, rest = k.split(".", 1)
-            for ident in ("user", "system"):
-                nk = f"{head}_{ident}.{rest}"
-                if nk not in fork:
-                    state[nk] = v
-        else:
-            state[k] = v
+    for k, v in audiollm_state(os.path.join(model_path, "audiollm", "final.pt")).items():
+        state[k] = v
     # ---- decoder/final.pt
     snap = _torch_load(os.path.join(model_path, "decoder", "final.pt"))
     if isinstance(snap, dict) and "model" in snap:

@@ -69,6 +69,7 @@ class FreezeOmniEngine:
         self.cfg, self.synth, self.llm_path = load_model_dir(model_path, llm_path)
         src = source or make_source(self.cfg, self.synth, self.device, model_path, self.llm_path)
         self.src = src
+        self.max_sessions = max_sessions
         ty = self.cfg["train_yaml"]
         self.enc = {i: SpeechEncoderEngine(src, self.cfg, i, self.device, max_sessions) for i in ("user", "system")}
         self.ada = {i: AdapterEngine(src, self.cfg, i, self.device, max_sessions) for i in ("user", "system")}
@@ -87,6 +88,39 @@ class FreezeOmniEngine:
         self.use_graphs = True
         self.predict_usr_state = ty["model_conf"].get("predict_usr_state", 0)
         self._chat_template(ty["model_conf"].get("chat_template"))
+
+    # ------------------------------------------------------------------ models/utils.py:11-28
+    def rebind_audiollm(self, state):
+        """Load an audiollm/final.pt state (fo.checkpoint.audiollm_state) over this engine, as the
+        reference's load_checkpoint does after the model is built: the speech encoders, adapters and
+        state head are rebuilt from it; 'llm_decoder.*' entries rebuild the Qwen2 weights too (the KV
+        pool with them, so no session may be open).  Unknown keys are ignored (strict=False, utils.py:20);
+        a key the path reads with the wrong shape raises."""
+        from .checkpoint import CheckpointSource
+        from .weights import OverlaySource
+        need = all_shapes(self.cfg)
+        bad = [f"{k}: {tuple(v.shape)} != {tuple(need[k])}" for k, v in state.items()
+               if k in need and tuple(v.shape) != tuple(need[k])]
+        if bad:
+            raise RuntimeError("load_checkpoint: shape mismatch: " + "; ".join(bad[:20]))
+        state = {k: v for k, v in state.items() if k in need}
+        src = OverlaySource(CheckpointSource(state, self.device), self.src)
+        for g in list(self._lgraphs.values()) + list(self._tgraphs.values()):
+            g.destroy()
+        self._lgraphs, self._tgraphs = {}, {}
+        self.enc = {i: SpeechEncoderEngine(src, self.cfg, i, self.device, self.max_sessions) for i in ("user", "system")}
+        self.ada = {i: AdapterEngine(src, self.cfg, i, self.device, self.max_sessions) for i in ("user", "system")}
+        if any(k.startswith(("model.", "lm_head.")) for k in state):
+            if self.llm.pool.pages_in_use():
+                raise RuntimeError("load_checkpoint: Qwen2 weights cannot be replaced while sessions hold KV pages")
+            kv_tokens = self.llm.pool.n_pages * self.llm.pool.PS
+            self.llm = None   # release the old weights and pool first (15 GB at Qwen2-7B size)
+            torch.cuda.empty_cache()
+            self.llm = LLMEngine(src, self.cfg["llm"], self.device, kv_tokens=kv_tokens)
+        elif "predictor_head.weight" in src:
+            self.llm.head_w, self.llm.head_b = src.get("predictor_head.weight"), src.get("predictor_head.bias")
+        self.src = src
+        return sorted(state)
 
     # ------------------------------------------------------------------ chat template (audioLLM.py:112-126)
     def _ids(self, text):

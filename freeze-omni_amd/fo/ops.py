@@ -267,11 +267,13 @@ def rmsnorm(x, w, eps, out=None, round_fp16=False, M=None):
     return out
 
 
-def layernorm(x, w, b, eps=1e-5, out=None, relu=False, M=None):
+def layernorm(x, w, b, eps=1e-5, out=None, relu=False, M=None, act=None):
+    """Row LayerNorm; act ('relu' | 'gelu', or relu=True) applied after the affine."""
     M = x.shape[0] if M is None else M
     out = torch.empty_like(x) if out is None else out
+    a = ACT[act] if act is not None else (ACT["relu"] if relu else 0)
     _lib.call("fo_layernorm", x.data_ptr(), x.stride(0), M, x.shape[1], w.data_ptr(), b.data_ptr(), float(eps),
-              out.data_ptr(), out.stride(0), 1 if relu else 0, stream(x.device))
+              out.data_ptr(), out.stride(0), a, stream(x.device))
     return out
 
 

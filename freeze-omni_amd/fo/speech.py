@@ -9,8 +9,8 @@
   Conv2dSubsampling4 (im2col + MFMA GEMMs) + rel-pos Transformer with a left-chunk KV ring per user
   (models/encoder/transformer.py:266-285, attention.py:407-459).  linear_pos(sinusoid(p)) is
   precomputed for every position at load (memory for compute: ~0.5 GB per encoder at REAL size).
-* AdapterEngine: CNNSubsampling single-conv branch with carried frames (models/adapter.py:112-157),
-  eval BatchNorm as a per-column affine GEMM epilogue.
+* AdapterEngine: CNNSubsampling with carried frames (models/adapter.py:72-157), both conv branches,
+  eval BatchNorm as a per-column affine GEMM epilogue, or LayerNorm; ReLU or GELU.
 Batched: one launch sequence serves all users of a replica; per-user state lives in slot pools.
 """
 import math
@@ -269,7 +269,8 @@ class AdapterCache:
 
     def __init__(self, engine):
         self.engine, self.slot = engine, engine.slots.get()
-        engine.cache[self.slot].zero_()
+        for c in engine.caches:
+            c[self.slot].zero_()
 
     def __del__(self):
         try:
@@ -279,24 +280,60 @@ class AdapterCache:
 
 
 class AdapterEngine:
+    """CNNSubsampling (models/adapter.py:72-157), every branch the reference builds:
+    cnn_num == 1 (4*d >= L): causal conv1d(d -> 2d, k, stride 2) + eval BatchNorm (a per-column affine
+    in the GEMM epilogue) or LayerNorm(2d, eps 1e-3) + ReLU / exact GELU, then Linear(2d -> L);
+    cnn_num == 2 (4*d < L): conv1d(d -> 2d, k, stride 1) + BN + ReLU first, then the stride-2 conv
+    2d -> 4d + BN + ReLU and Linear(4d -> L), each conv with its own carried k-1 input frames.
+    adpter_type 'cnn' / 'linear' (CNNAdapter / LinearAdapter) are rejected at load: their forward takes no
+    cache, so the reference's recognize (models/audioLLM.py:386-387) cannot call them either."""
+
     def __init__(self, src, cfg, ident, device, max_sessions=64):
         mc = cfg["train_yaml"]["model_conf"]
+        atype = mc.get("adpter_type", "subsampling")
+        if atype != "subsampling":
+            raise ValueError(f"adpter_type {atype!r}: only 'subsampling' (CNNSubsampling) streams with a cache "
+                             "(models/audioLLM.py:159-165,386-387)")
         self.d, self.L, self.k = mc["enc_out_dim"], mc["llm_embed_dim"], mc["kernel_size"]
+        self.cnn_num = 2 if 4 * self.d < self.L else 1
+        self.norm = mc.get("norm", "batch") if self.cnn_num == 1 else "batch"
+        if self.norm not in ("batch", "layer"):
+            raise ValueError(f"adapter norm {self.norm!r}: CNNSubsampling builds bn2 only for 'batch' or 'layer' "
+                             "(models/adapter.py:100-103)")
+        self.act = "gelu" if (self.cnn_num == 1 and mc.get("activation_func", "relu") == "gelu") else "relu"
         p = f"adpter_{ident}."
         self.device = torch.device(device)
-        w = src.get(p + "conv1d2.weight", torch.bfloat16)  # [2d, d, k] -> [2d, d*k] (col = c*k + j)
-        self.conv = PackedLinear(w.reshape(2 * self.d, self.d * self.k), src.get(p + "conv1d2.bias"))
-        g, b = src.get(p + "bn2.weight"), src.get(p + "bn2.bias")
-        rm, rv = src.get(p + "bn2.running_mean"), src.get(p + "bn2.running_var")
-        sc = g / torch.sqrt(rv + 1e-3)
-        self.conv.set_affine(sc, b - rm * sc)
+        d, k = self.d, self.k
+
+        def bn_affine(lin, name):
+            g, b = src.get(p + name + ".weight"), src.get(p + name + ".bias")
+            rm, rv = src.get(p + name + ".running_mean"), src.get(p + name + ".running_var")
+            sc = g / torch.sqrt(rv + 1e-3)
+            lin.set_affine(sc, b - rm * sc)
+
+        self.conv1 = None
+        if self.cnn_num == 2:
+            w1 = src.get(p + "conv1d1.weight", torch.bfloat16)  # [2d, d, k] -> [2d, d*k] (col = c*k + j)
+            self.conv1 = PackedLinear(w1.reshape(2 * d, d * k), src.get(p + "conv1d1.bias"))
+            bn_affine(self.conv1, "bn1")
+        cin = d if self.cnn_num == 1 else 2 * d
+        w = src.get(p + "conv1d2.weight", torch.bfloat16)
+        self.conv = PackedLinear(w.reshape(w.shape[0], cin * k), src.get(p + "conv1d2.bias"))
+        self.ln = None
+        if self.norm == "batch":
+            bn_affine(self.conv, "bn2")
+        else:
+            self.ln = (src.get(p + "bn2.weight"), src.get(p + "bn2.bias"))
         self.project = PackedLinear(src.get(p + "project.weight", torch.bfloat16), src.get(p + "project.bias"))
-        self.cache = torch.zeros(max_sessions, self.k - 1, self.d, dtype=F32, device=self.device)
+        # cache[0]: inputs of the stride-2 conv; cache[1] (cnn_num 2): inputs of the stride-1 conv
+        self.cache = torch.zeros(max_sessions, k - 1, cin, dtype=F32, device=self.device)
+        self.cache1 = torch.zeros(max_sessions, k - 1, d, dtype=F32, device=self.device) if self.conv1 else None
+        self.caches = [c for c in (self.cache, self.cache1) if c is not None]
         self.slots = SlotPool(max_sessions)
 
     @property
     def weight_bytes(self):
-        return self.conv.nbytes + self.project.nbytes
+        return self.conv.nbytes + self.project.nbytes + (self.conv1.nbytes if self.conv1 else 0)
 
     def new_cache(self):
         return AdapterCache(self)
@@ -306,18 +343,30 @@ class AdapterEngine:
 
     def buffers(self, B, T):
         To, dev = self.out_len(T), self.device
-        return {"cols": torch.empty(B * To, self.conv.Kp, dtype=F32, device=dev),
-                "y": torch.empty(B * To, self.conv.N, dtype=F32, device=dev),
-                "out": torch.empty(B * To, self.project.N, dtype=F32, device=dev),
+        e = lambda *shape: torch.empty(*shape, dtype=F32, device=dev)  # noqa: E731
+        bufs = {"cols": e(B * To, self.conv.Kp), "y": e(B * To, self.conv.N), "out": e(B * To, self.project.N),
                 "slots": torch.empty(B, dtype=I32, device=dev)}
+        if self.conv1 is not None:
+            bufs["cols1"] = e(B * T, self.conv1.Kp)
+            bufs["y1"] = e(B * T, self.conv1.N)
+        return bufs
 
     def run(self, x, B, T, bufs):
         """Device part of __call__ with bufs['slots'] uploaded."""
         KC = self.k - 1
         slots = bufs["slots"]
-        ops.im2col_conv1d(self.cache, slots, x, B, KC, T, self.d, self.k, 2, bufs["cols"])
-        ops.conv_cache_update(self.cache, slots, x, B, KC, T, self.d)
-        self.conv(bufs["cols"], out=bufs["y"], act="relu")
+        if self.conv1 is not None:  # models/adapter.py:123-134
+            ops.im2col_conv1d(self.cache1, slots, x, B, KC, T, self.d, self.k, 1, bufs["cols1"])
+            ops.conv_cache_update(self.cache1, slots, x, B, KC, T, self.d)
+            x = self.conv1(bufs["cols1"], out=bufs["y1"], act="relu")
+        cin = self.cache.shape[2]
+        ops.im2col_conv1d(self.cache, slots, x, B, KC, T, cin, self.k, 2, bufs["cols"])
+        ops.conv_cache_update(self.cache, slots, x, B, KC, T, cin)
+        if self.ln is None:
+            self.conv(bufs["cols"], out=bufs["y"], act=self.act)
+        else:  # LayerNorm over the 2d channels of each frame (models/adapter.py:145-149)
+            self.conv(bufs["cols"], out=bufs["y"])
+            ops.layernorm(bufs["y"], *self.ln, eps=1e-3, out=bufs["y"], act=self.act)
         return self.project(bufs["y"], out=bufs["out"]), self.out_len(T)
 
     def __call__(self, x, T, caches):

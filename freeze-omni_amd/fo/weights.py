@@ -89,3 +89,17 @@ class CheckpointSource:
 
     def get(self, name, dtype=torch.float32):
         return self.state[name].to(device=self.device, dtype=dtype)
+
+
+class OverlaySource:
+    """`primary` wins where it has the name, `fallback` serves the rest (a checkpoint loaded over an
+    engine that was built from another source: models/utils.py:load_checkpoint)."""
+
+    def __init__(self, primary, fallback):
+        self.primary, self.fallback = primary, fallback
+
+    def __contains__(self, name):
+        return name in self.primary or name in self.fallback
+
+    def get(self, name, dtype=torch.float32):
+        return (self.primary if name in self.primary else self.fallback).get(name, dtype)

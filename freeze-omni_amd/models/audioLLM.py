@@ -84,6 +84,15 @@ class AudioLLM:
         self.top_k, self.top_p, self.temperature = top_k, top_p, temperature
         self.logger = None
 
+    def rebind(self, loaded=None):
+        """Refresh the views on the engine after models.utils.load_checkpoint re-packed weights."""
+        eng = self.engine
+        self.encoder_user = _Encoder(eng.enc["user"])
+        self.encoder_system = _Encoder(eng.enc["system"])
+        self.predictor_head = eng.llm.head_w
+        self.llm_decoder = _LLMDecoder(eng)
+        return loaded
+
     @classmethod
     def from_model_dir(cls, model_path, llm_path=None, device="cuda:0", **kw):
         return cls(FreezeOmniEngine(model_path, llm_path, device=device), **kw)

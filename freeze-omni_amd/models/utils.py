@@ -16,6 +16,22 @@ def init_encoder_llm(configs, device="cuda:0", model_path=None, llm_path=None):
 
 
 def load_checkpoint(model, path):
-    """Weights are bound when the engine is built from the model directory (synthetic.json or the
-    reference checkpoint files); kept for API parity with models/utils.py:11-28."""
+    """models/utils.py:11-28: load an audiollm final.pt into the model (strict=False: unknown keys are
+    ignored; the fork's 'encoder_*' / 'adpter_*' names and the upstream 'encoder.' / 'adpter.' names
+    both bind, see fo.checkpoint.audiollm_state) and return the configs of a sibling final.yaml, or {}.
+    The encoders, adapters and state head (and the Qwen2 weights for 'llm_decoder.*' entries) are
+    re-packed on the device from the file; a tensor of the wrong shape raises."""
+    import re
+
+    import yaml
+
+    from fo.checkpoint import audiollm_state
+    if not isinstance(model, AudioLLM):
+        raise TypeError(f"load_checkpoint: expected models.audioLLM.AudioLLM, got {type(model).__name__}")
+    print(f"Checkpoint: loading from checkpoint {path} for GPU")
+    model.rebind(model.engine.rebind_audiollm(audiollm_state(path)))
+    info_path = re.sub(r"\.pt$", ".yaml", path)
+    if os.path.exists(info_path):
+        with open(info_path) as f:
+            return yaml.safe_load(f)
     return {}

@@ -101,9 +101,10 @@ int fo_fill_hash(void* out, int out_bf16, long long n, unsigned long long key, f
  * models/decoder/decoder.py:299-311,343); round_fp16 mirrors the cast back to an fp16 input dtype. */
 int fo_rmsnorm(const float* x, int ldx, int M, int D, const float* w, float eps, float* out, int ldo, int round_fp16,
                hipStream_t s);
-/* torch.nn.LayerNorm (+ReLU) of the speech encoder (models/encoder/transformer.py:343-346,261,278,287) */
+/* torch.nn.LayerNorm of the speech encoder (models/encoder/transformer.py:343-346,261,278,287) and of the
+ * adapter's norm: layer branch (models/adapter.py:102-103,145-149); act 0 none, 1 ReLU, 3 exact GELU. */
 int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const float* b, float eps, float* out, int ldo,
-                 int relu, hipStream_t s);
+                 int act, hipStream_t s);
 /* embedding / row gather (wte at models/audioLLM.py:303,330; decoder embedding decoder.py:318,336) */
 int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,
                    int ldo, const int* out_rows, int round_fp16, hipStream_t s);

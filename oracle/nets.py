@@ -157,30 +157,59 @@ def new_encoder_state(nb):
 
 
 class Adapter:
-    """CNNSubsampling.forward(x, mask, cache, return_cache=True), single-conv branch
-    (models/adapter.py:84-110,112-157): causal conv1d(d->2d, k, stride 2) + BN(eval, eps 1e-3) + ReLU + Linear."""
+    """CNNSubsampling.forward(x, mask, cache, return_cache=True) (models/adapter.py:72-157):
+    cnn_num == 1 (4*d >= L): causal conv1d(d->2d, k, stride 2) + BatchNorm(eval, eps 1e-3) or
+    LayerNorm(2d, eps 1e-3) over channels + ReLU or exact GELU + Linear(2d -> L);
+    cnn_num == 2 (4*d < L): causal conv1d(d->2d, k, stride 1) + BN + ReLU, then conv1d(2d->4d, k,
+    stride 2) + BN + ReLU + Linear(4d -> L).  cache = [last k-1 inputs of the stride-2 conv,
+    last k-1 inputs of the stride-1 conv] (zeros on the first call, :124-143)."""
 
     def __init__(self, W, cfg, ident="user"):
+        mc = cfg["train_yaml"]["model_conf"]
         self.W = W
         self.p = f"adpter_{ident}."
-        self.k = cfg["train_yaml"]["model_conf"]["kernel_size"]
+        self.k = mc["kernel_size"]
+        self.cnn_num = 2 if 4 * mc["enc_out_dim"] < mc["llm_embed_dim"] else 1
+        self.norm = "batch" if self.cnn_num == 2 else mc.get("norm", "batch")
+        self.act = "relu" if self.cnn_num == 2 else mc.get("activation_func", "relu")
 
-    def __call__(self, x, cache):
-        """x [T, d]; cache None or [d, k-1] array.  Returns (out [T', L], new_cache)."""
-        xt = x.T
+    def _conv(self, xt, cache, name, stride):
+        """xt [C, T] -> (y [T', Cout] incl. bias, new cache [C, k-1])."""
         left = np.zeros((xt.shape[0], self.k - 1), F32) if cache is None else cache
         xt = np.concatenate([left, xt], axis=1)
         new_cache = xt[:, 1 - self.k:].copy()
-        w = self.W[self.p + "conv1d2.weight"]
-        Tin = xt.shape[1]
-        To = (Tin - self.k) // 2 + 1
-        cols = np.stack([xt[:, t * 2:t * 2 + self.k].reshape(-1) for t in range(To)])
-        y = linear(cols, w.reshape(w.shape[0], -1), self.W[self.p + "conv1d2.bias"])
-        g, b = self.W[self.p + "bn2.weight"], self.W[self.p + "bn2.bias"]
-        rm, rv = self.W[self.p + "bn2.running_mean"], self.W[self.p + "bn2.running_var"]
-        y = ((y - rm) / np.sqrt(rv + F32(1e-3)) * g + b).astype(F32)
-        y = np.maximum(y, 0)
-        return linear(y, self.W[self.p + "project.weight"], self.W[self.p + "project.bias"]), new_cache
+        w = self.W[self.p + name + ".weight"]
+        To = (xt.shape[1] - self.k) // stride + 1
+        cols = np.stack([xt[:, t * stride:t * stride + self.k].reshape(-1) for t in range(To)])
+        return linear(cols, w.reshape(w.shape[0], -1), self.W[self.p + name + ".bias"]), new_cache
+
+    def _bn(self, y, name):
+        g, b = self.W[self.p + name + ".weight"], self.W[self.p + name + ".bias"]
+        rm, rv = self.W[self.p + name + ".running_mean"], self.W[self.p + name + ".running_var"]
+        return ((y - rm) / np.sqrt(rv + F32(1e-3)) * g + b).astype(F32)
+
+    def __call__(self, x, cache):
+        """x [T, d]; cache None or the list above.  Returns (out [T', L], new_cache)."""
+        xt = x.T
+        c0 = c1 = None
+        if cache is not None:
+            c0 = cache[0]
+            c1 = cache[1] if len(cache) > 1 else None
+        if self.cnn_num == 2:
+            y1, c1 = self._conv(xt, c1, "conv1d1", 1)
+            xt = np.maximum(self._bn(y1, "bn1"), 0).T
+        y, c0 = self._conv(xt, c0, "conv1d2", 2)
+        if self.norm == "batch":
+            y = self._bn(y, "bn2")
+        else:
+            y = layernorm(y, self.W[self.p + "bn2.weight"], self.W[self.p + "bn2.bias"], eps=1e-3)
+        if self.act == "gelu":
+            from scipy.special import erf
+            y = (0.5 * y * (1.0 + erf(y.astype(np.float64) / np.sqrt(2.0)))).astype(F32)
+        else:
+            y = np.maximum(y, 0)
+        out = linear(y, self.W[self.p + "project.weight"], self.W[self.p + "project.bias"])
+        return out, ([c0, c1] if self.cnn_num == 2 else [c0])
 
 
 # ============================================================ decoder-only transformers

@@ -44,13 +44,24 @@ def encoder_shapes(cfg, ident):
 
 
 def adapter_shapes(cfg, ident):
+    """CNNSubsampling (models/adapter.py:72-110): one stride-2 conv when 4*d >= L (BatchNorm or
+    LayerNorm(2d) per `norm`), else a stride-1 conv d->2d + BatchNorm first and the stride-2 conv
+    2d->4d + BatchNorm (cnn_num == 2)."""
     mc = cfg["train_yaml"]["model_conf"]
     d, L, k = mc["enc_out_dim"], mc["llm_embed_dim"], mc["kernel_size"]
-    assert 4 * d >= L, "only the single-conv CNNSubsampling branch (models/adapter.py:84-110) is on the path"
     p = f"adpter_{ident}."
+    bn = ("weight", "bias", "running_mean", "running_var")
+    if 4 * d < L:
+        s = {p + "conv1d1.weight": [2 * d, d, k], p + "conv1d1.bias": [2 * d],
+             p + "conv1d2.weight": [4 * d, 2 * d, k], p + "conv1d2.bias": [4 * d],
+             p + "project.weight": [L, 4 * d], p + "project.bias": [L]}
+        for n in bn:
+            s[p + f"bn1.{n}"] = [2 * d]
+            s[p + f"bn2.{n}"] = [4 * d]
+        return s
     s = {p + "conv1d2.weight": [2 * d, d, k], p + "conv1d2.bias": [2 * d], p + "project.weight": [L, 2 * d],
          p + "project.bias": [L]}
-    for n in ("weight", "bias", "running_mean", "running_var"):
+    for n in (bn if mc.get("norm", "batch") == "batch" else ("weight", "bias")):
         s[p + f"bn2.{n}"] = [2 * d]
     return s
 

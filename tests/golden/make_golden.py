@@ -615,6 +615,39 @@ def gold_real_t2(seed=7):
     print("T2 codec: pcm", tuple(pcm.shape))
 
 
+ADAPTER_VARIANTS = [  # CNNSubsampling(enc_out_dim, llm_embed_dim, kernel_size, activation_func, norm)
+    {"enc_out_dim": 16, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "relu", "norm": "batch"},
+    {"enc_out_dim": 32, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "gelu", "norm": "layer"},
+    {"enc_out_dim": 32, "llm_embed_dim": 96, "kernel_size": 3, "activation_func": "relu", "norm": "layer"},
+    {"enc_out_dim": 32, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "gelu", "norm": "batch"}]
+
+
+def gold_adapter_variants(seed):
+    """CNNSubsampling's other branches (models/adapter.py:84-110,123-150): cnn_num == 2 (4*d < L: a
+    stride-1 conv + BN + ReLU before the stride-2 conv, two caches), LayerNorm(2d, eps 1e-3) over
+    channels, exact GELU; streamed over chunks of 4 and 7 encoder frames (framings A and B) with the
+    returned cache fed back, as AudioLLM.recognize does (models/audioLLM.py:386-387)."""
+    from models.adapter import CNNSubsampling
+    out = {}
+    rng = np.random.default_rng(31)
+    for vi, v in enumerate(ADAPTER_VARIANTS):
+        m = CNNSubsampling(v["enc_out_dim"], v["llm_embed_dim"], v["kernel_size"], v["activation_func"], v["norm"])
+        init_module(m, seed, "adpter_user.")
+        m.eval()
+        cache = None
+        for c in range(6):
+            T = 4 if c % 2 == 0 else 7
+            x = torch.from_numpy(rng.standard_normal((1, T, v["enc_out_dim"])).astype(np.float32))
+            y, _, cache = m(x, torch.full((1, 1, T), True), cache=cache, return_cache=True)
+            out[f"v{vi}_c{c}_x"] = x[0].numpy()
+            out[f"v{vi}_c{c}_y"] = y[0].detach().numpy().copy()
+        out[f"v{vi}_cnn_num"] = np.array(m.cnn_num)
+    np.savez_compressed(os.path.join(HERE, "adapter_variants_tiny.npz"), **out)
+    with open(os.path.join(HERE, "adapter_variants_tiny.json"), "w") as f:
+        json.dump({"seed": seed, "variants": ADAPTER_VARIANTS}, f, indent=1)
+    print("adapter variants: cnn_num", [int(out[f"v{i}_cnn_num"]) for i in range(len(ADAPTER_VARIANTS))])
+
+
 def gold_tts(cfg):
     import argparse
     from models.decoder.decoder import LLM2TTSCodecAR
@@ -799,6 +832,7 @@ def main():
     gold_audiollm_b(cfg)
     gold_llm_text(cfg)
     gold_real_t2()
+    gold_adapter_variants(cfg["seed"])
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
         json.dump(SHAPES, f)
     total = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith((".npz", ".json")))
@@ -818,6 +852,9 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["llm_text"]:
         install_shims()
         gold_llm_text(C.get("tiny"))
+    elif sys.argv[1:] == ["adapter_variants"]:
+        install_shims()
+        gold_adapter_variants(C.get("tiny")["seed"])
     elif sys.argv[1:] == ["real_t2"]:
         install_shims()
         gold_real_t2()

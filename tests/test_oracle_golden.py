@@ -300,3 +300,26 @@ def test_real_geometry_codec_matches_golden(W2):
     g = load("real_codec_t2.npz")
     pcm = nets.Codec(W2, T2)(g["ids"])
     np.testing.assert_allclose(pcm, g["pcm"], atol=2e-5, rtol=1e-3)
+
+
+def _variant_cfg(v):
+    c = configs.get("tiny")
+    c["train_yaml"]["model_conf"].update(v)
+    return c
+
+
+def test_adapter_variants_match_golden():
+    """CNNSubsampling's cnn_num == 2 branch, LayerNorm and GELU (models/adapter.py:84-150), streamed over
+    chunks of 4 and 7 frames with the cache fed back, against the reference (adapter_variants_tiny.*)."""
+    from oracle.params import adapter_shapes
+    meta = json.load(open(os.path.join(G, "adapter_variants_tiny.json")))
+    g = load("adapter_variants_tiny.npz")
+    for vi, v in enumerate(meta["variants"]):
+        c = _variant_cfg(v)
+        Wv = SynthCheckpoint(meta["seed"], adapter_shapes(c, "user"))
+        ada = nets.Adapter(Wv, c, "user")
+        assert ada.cnn_num == int(g[f"v{vi}_cnn_num"])
+        cache = None
+        for ci in range(6):
+            y, cache = ada(g[f"v{vi}_c{ci}_x"], cache)
+            np.testing.assert_allclose(y, g[f"v{vi}_c{ci}_y"], atol=1e-5, rtol=1e-4)

@@ -267,3 +267,58 @@ def test_real_geometry_vocoder_matches_reference(dev):
     pcm = eng(torch.from_numpy(g["ids"][None]).to(dev, torch.int32))[0]
     assert pcm.numel() == g["pcm"].size
     close(pcm, g["pcm"], rtol=1e-3, atol=1e-4)
+
+
+# ------------------------------------------------------------------ adapter branches
+def test_adapter_variants_match_reference(dev):
+    """CNNSubsampling's cnn_num == 2 branch (stride-1 conv + BN + ReLU first, two caches), LayerNorm(2d)
+    and exact GELU (models/adapter.py:84-150) on the GPU, streamed over 4- and 7-frame chunks, against
+    the reference (adapter_variants_tiny.*; 5e-4 abs)."""
+    from fo.speech import AdapterEngine
+    from fo.weights import SynthSource
+    meta = json.load(open(os.path.join(G, "adapter_variants_tiny.json")))
+    g = load("adapter_variants_tiny.npz")
+    for vi, v in enumerate(meta["variants"]):
+        c = configs.get("tiny")
+        c["train_yaml"]["model_conf"].update(v)
+        ada = AdapterEngine(SynthSource(meta["seed"], adapter_shapes(c, "user"), dev), c, "user", dev, 2)
+        assert ada.cnn_num == int(g[f"v{vi}_cnn_num"])
+        other = ada.new_cache()   # a second session's slot must stay independent
+        ac = ada.new_cache()
+        for ci in range(6):
+            x = g[f"v{vi}_c{ci}_x"]
+            xx = torch.from_numpy(np.concatenate([x, x[::-1].copy()])).to(dev)
+            y, To = ada(xx, x.shape[0], [ac, other])
+            close(y[:To], g[f"v{vi}_c{ci}_y"], atol=5e-4)
+
+
+def test_load_checkpoint_binds_final_pt(pipe, tmp_path):
+    """models.utils.load_checkpoint re-packs the encoder / adapter / state-head weights from a final.pt
+    (upstream 'encoder.' names included) and returns final.yaml's configs: a state head of zeros with
+    bias (0, 5, 0, 0) must give state_1 = e^5 / (2 + e^5) on any chunk afterwards."""
+    import yaml
+    from models.utils import load_checkpoint
+    D = pipe.model.engine.llm.D
+    sd = {"predictor_head.weight": torch.zeros(4, D), "predictor_head.bias": torch.tensor([0.0, 5.0, 0.0, 0.0]),
+          "encoder.global_cmvn.mean": torch.zeros(80), "unrelated.key": torch.ones(3)}
+    path = str(tmp_path / "final.pt")
+    torch.save(sd, path)
+    orig_src = pipe.model.engine.src
+    with open(str(tmp_path / "final.yaml"), "w") as f:
+        yaml.safe_dump({"note": "sidecar"}, f)
+    try:
+        assert load_checkpoint(pipe.model, path) == {"note": "sidecar"}
+        assert torch.equal(pipe.model.engine.enc["system"].mean.cpu(), torch.zeros(80))
+        g = load("audiollm_tiny.npz")
+        _, pkv, _, _, _ = pipe.speech_dialogue(None, identity="", status="pre", role="hi")
+        probs = pipe.speech_dialogue(torch.from_numpy(g["feats"][0]).unsqueeze(0), identity="user",
+                                     status="ipu_sl", past_key_values=pkv)[0]
+        want = np.exp(5.0) / (2.0 + np.exp(5.0))
+        assert abs(probs["state_1"] - want) < 1e-5 and abs(probs["state_2"] - 1.0 / (2.0 + np.exp(5.0))) < 1e-5
+        torch.save({"predictor_head.weight": torch.zeros(3, D)}, path)
+        with pytest.raises(RuntimeError):
+            load_checkpoint(pipe.model, path)
+    finally:   # restore the synthetic weights for later tests of this module
+        pipe.model.engine.src = orig_src
+        pipe.model.engine.rebind_audiollm({})
+        pipe.model.rebind()
