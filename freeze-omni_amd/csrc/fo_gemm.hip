@@ -881,11 +881,14 @@ int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void
                    splitk, rstats, rgroups, eps, nullptr, nullptr, nullptr, nullptr, &r, stream);
 }
 
-// Force (waves, tiles per workgroup) of the M <= 16 kernels on this thread (0 = automatic); sweeps.
+// Software-pipelining mode of the one-row-tile weight-stream GEMMs (k_gemm_wpipe): 0 off, 1 U k-steps,
+// 2 two k-steps, 3 the default policy.  PROCESS-GLOBAL library state (not per thread or per stream):
+// meant for sweeps and tests, which restore the previous mode.  Returns the previous mode (>= 0).
 int fo_gemm_set_pipe(int on) {
   FO_REQUIRE(on >= 0 && on <= 3, "fo_gemm_set_pipe: 0 (off), 1 (U k-steps), 2 (2 k-steps) or 3 (policy)");
+  const int prev = g_pipe;
   g_pipe = on;
-  return 0;
+  return prev;
 }
 
 int fo_gemm_tune(int nw, int nt) {

@@ -539,6 +539,10 @@ def penalty(logits, V, ids, win, step, penalty, B=None):
     """Repetition penalty (models/decoder/decoder.py:348-351) in place on logits [B, >=V]: stores this
     step's input ids into the ring win [B, W] at step % W, then divides each windowed id's logit."""
     B = logits.shape[0] if B is None else B
+    assert logits.dtype == F32 and logits.stride(-1) == 1 and logits.shape[0] >= B and logits.shape[1] >= V
+    assert win.dtype == I32 and win.is_contiguous() and win.dim() == 2 and win.shape[0] >= B
+    assert ids.dtype == I32 and ids.is_contiguous() and ids.numel() >= B
+    assert step.dtype == I32 and step.is_contiguous() and step.numel() >= B
     _lib.call("fo_penalty", logits.data_ptr(), logits.stride(0), B, V, ids.data_ptr(), win.data_ptr(), win.shape[1],
               step.data_ptr(), float(penalty), stream(logits.device))
     return logits

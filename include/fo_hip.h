@@ -80,7 +80,8 @@ int fo_gemm_tune(int nw, int nt);
 /* Software-pipelined one-row-tile fp32-X weight-stream GEMMs (M <= 16, >= 32 MB of weights: the next
  * k-group's weights + X in flight during this group's MFMAs).  3 (default): the measured policy; 0: plain
  * loops; 1 / 2: every such GEMM pipelined with 4 / 2 k-steps per group (sweeps).  Unset, the
- * FO_GEMM_PIPE environment variable (0-3) decides. */
+ * FO_GEMM_PIPE environment variable (0-3) decides.  Process-global state (for sweeps and tests); returns the
+ * previous mode (>= 0) so callers can restore it. */
 int fo_gemm_set_pipe(int on);
 long long fo_pack_weight_elems(int N, int K);
 int fo_pack_weight(const void* W, int src_bf16, int N, int K, int ldw, void* out, int tile_base, int tile_stride,

@@ -240,11 +240,12 @@ def test_gemm_pipelined_weight_stream(dev, mode, M, N, K, sw):
     x = torch.randn(M, K, generator=g)
     lin = PackedLinear(w.to(dev), swiglu_up=None if u is None else u.to(dev))
     lib = _lib.load()
+    prev = lib.fo_gemm_set_pipe(mode)
+    assert prev >= 0
     try:
-        lib.fo_gemm_set_pipe(mode)
         y = lin(x.to(dev)).cpu().double()
     finally:
-        lib.fo_gemm_set_pipe(3)
+        lib.fo_gemm_set_pipe(prev)
     a = x.double() @ w.double().t()
     ref = torch.nn.functional.silu(a) * (x.double() @ u.double().t()) if sw else a
     torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
