@@ -545,6 +545,175 @@ void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, h
   else launch_gemm<NT, RB, 4, 4, SW>(wstream, x_f32, grid, a, s);
 }
 
+// X-stationary weight stream for M <= 16 fp32 rows and K = NW * KPW * 32 (Qwen2: K = 3584 = 16 x 7 x 32).
+// One workgroup per CU (the LDS footprint admits one), persistent over a contiguous, balanced range of
+// column units (2 packed tiles: a gate/up pair, a RoPE (i, i + hd/2) pair, or two plain tiles).
+//  * prologue: wave w loads ITS K slice of X once, split into bf16 hi (kept in VGPRs) and lo (kept in
+//    the wave's private LDS region) -- X never goes through the vector-memory path again, so the weight
+//    stream is the only VMEM traffic (the fo_gemm grid re-reads X from L2 once per column group);
+//  * steady state: per unit, two tiles' weight fragments (KPW x 1 KiB per wave each) are double
+//    buffered -- the next unit's loads are issued right after the MFMAs that free a buffer;
+//  * per unit the NW partial tiles are reduced through LDS (two barriers), then the epilogue of the
+//    row-major output (bias, SwiGLU, RoPE + KV append, residual, RMSNorm statistics) as in gemm_body.
+constexpr int XS_NW = 8, XS_KPW = 14;
+template <int NW, int KPW, int MODE>  // MODE 0: plain (+stats), 1: SwiGLU pair, 2: RoPE pair
+__global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
+  __shared__ bf16x8 xlo[NW][KPW][64];
+  __shared__ float part[NW][2][16][17];
+  __shared__ float ybuf[2][16][17];
+  __shared__ float rstd_s[16];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int KS = NW * KPW;
+  const int ub = (int)((long)units * blockIdx.x / gridDim.x);
+  const int ue = (int)((long)units * (blockIdx.x + 1) / gridDim.x);
+  // weights of this wave's K slice, tile t, k-step j: byte (t * KS + j) * 1024 (SGPR offset) + this lane's
+  // (wave * KPW * 64 + lane) * 16 (one VGPR) through a buffer descriptor (no 64-bit address per load)
+  const unsigned long long wbase = (unsigned long long)a.Wp;
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(wbase >> 32)) << 32) |
+                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)wbase)),
+      (short)0, __builtin_amdgcn_readfirstlane(a.ntiles * KS * 1024), 0x00020000);
+  const int voff = (wave * KPW * 64 + lane) * 16;
+  bf16x8 w0[KPW], w1[KPW];
+  auto issue = [&](bf16x8 (&w)[KPW], int tile) {
+#pragma unroll
+    for (int j = 0; j < KPW; ++j)
+      w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024, 2));
+  };
+  issue(w0, ub < ue ? 2 * ub : a.ntiles);
+  issue(w1, ub < ue ? 2 * ub + 1 : a.ntiles);
+  // X slice (hi in registers, lo in LDS); rows >= M clamp to the last row (computed, never stored)
+  bf16x8 xh[KPW];
+  {
+    const int row = min(lane & 15, a.M - 1);
+    const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4) +
+                      (size_t)wave * KPW * 32;
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      const float4 p0 = reinterpret_cast<const float4*>(xp + j * 32)[0];
+      const float4 p1 = reinterpret_cast<const float4*>(xp + j * 32)[1];
+      const float f[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+      bf16x8 lo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const __bf16 h = (__bf16)f[i];
+        xh[j][i] = h;
+        lo[i] = (__bf16)(f[i] - (float)h);
+      }
+      xlo[wave][j][lane] = lo;
+    }
+  }
+  if (a.rstats) {  // RMSNorm consumer: rstd of each row from the producer's partial sums
+    for (int rr = wave; rr < 16; rr += NW) {
+      const int m = min(rr, a.M - 1);
+      float v = 0.f;
+      for (int j = lane; j < a.rgroups; j += 64) v += a.rstats[(size_t)m * a.rgroups + j];
+      v = wave_sum(v);
+      if (lane == 0) rstd_s[rr] = rsqrtf(v / (float)a.K + a.reps);
+    }
+  }
+  auto compute = [&](bf16x8 (&w)[KPW]) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[j], w[j], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xlo[wave][j][lane], w[j], acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  for (int u = ub; u < ue; ++u) {
+    // the next unit's loads are issued unconditionally (the compiler's in-order vmcnt accounting then
+    // waits only for the buffer it consumes); past the last unit they address tile `ntiles`, beyond the
+    // descriptor's range, which the hardware drops without touching memory
+    const int nxt = u + 1 < ue ? 2 * (u + 1) : a.ntiles;
+    const f32x4 c0 = compute(w0);
+    issue(w0, nxt);
+    const f32x4 c1 = compute(w1);
+    issue(w1, nxt + (u + 1 < ue ? 1 : 0));
+    __syncthreads();  // the previous unit's epilogue has read part[]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      part[wave][0][4 * (lane >> 4) + i][lane & 15] = c0[i];
+      part[wave][1][4 * (lane >> 4) + i][lane & 15] = c1[i];
+    }
+    __syncthreads();
+    const int e = threadIdx.x;
+    if constexpr (MODE != 0) {
+      if (e < 256) {
+        const int rr = e >> 4, c = e & 15;
+        float x1 = 0.f, x2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          x1 += part[w][0][rr][c];
+          x2 += part[w][1][rr][c];
+        }
+        if (a.rstats) {
+          x1 *= rstd_s[rr];
+          x2 *= rstd_s[rr];
+        }
+        if (rr < a.M) {
+          if constexpr (MODE == 1) {
+            const int n = u * 16 + c;
+            if (n < a.N) epilogue_store(a, true, rr, n, x1, x2);
+          } else {
+            rope_store(a, rr, rope_col(a, u, c), x1, x2);
+          }
+        }
+      }
+    } else {
+      float y = 0.f;
+      const int t = e >> 8, rr = (e >> 4) & 15, c = e & 15;
+      const int n = (2 * u + t) * 16 + c;
+      if (e < 512) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) v += part[w][t][rr][c];
+        if (a.rstats) v *= rstd_s[rr];
+        if (rr < a.M && n < a.N) {
+          y = epilogue_store(a, false, rr, n, v, 0.f);
+          if (a.yg) a.yg[(size_t)rr * a.ldy + n] = y * a.gnext[n];
+        }
+      }
+      if (a.sout) {  // row partial sums of squares (and sums) of this unit's 32 columns
+        if (e < 512) ybuf[t][rr][c] = (rr < a.M && n < a.N) ? y : 0.f;
+        __syncthreads();
+        if (e < 16 && e < a.M) {
+          float ss = 0.f, s1 = 0.f;
+#pragma unroll
+          for (int q = 0; q < 32; ++q) {
+            const float v = ybuf[q >> 4][e][q & 15];
+            ss += v * v;
+            s1 += v;
+          }
+          a.sout[(size_t)e * units + u] = ss;
+          if (a.sout1) a.sout1[(size_t)e * units + u] = s1;
+        }
+      }
+    }
+  }
+}
+
+int g_xs = -1;  // X-stationary kernel for eligible M <= 16 GEMMs: -1 = FO_GEMM_XS (default on), 0 off, 1 on
+inline bool xs_mode() {
+  if (g_xs < 0) {
+    const char* e = getenv("FO_GEMM_XS");
+    g_xs = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_xs == 1;
+}
+int g_num_cus = 0;
+inline int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+        hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
 // Pack W[N][K] (row-major, f32 or bf16, row stride ldw) into fragment order, writing tile t
 // of the source to destination tile (tile_base + t * tile_stride).
 __global__ void k_pack(const void* W, int src_bf16, int N, int K, int ldw, bf16_t* out, int KSp,
@@ -674,6 +843,28 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.rKVH = rope->rKVH;
     a.rhd = rope->rhd;
     a.rPS = rope->rPS;
+  }
+  // X-stationary persistent weight stream (k_gemm_xs) for the M <= 16 rows of a listen chunk / text step on
+  // K = 3584 layers (Qwen2 q|k|v, o, gate/up, lm_head): no split, no LayerNorm-on-load
+  // Measured (scripts/gemm_xs_ab.py, graph-replayed over weight copies beyond the Infinity Cache): gate/up
+  // + SwiGLU 56.1 -> 48.4 us at 16 rows, 47.4 -> 45.5 us at 8; lm_head equal (169.5 vs 169.9 us); the
+  // 26-33 MB o and q|k|v projections slower (one unit per workgroup: 12.3 -> 15.1, 18.7 -> 20.4 us), so
+  // only the SwiGLU pair takes this path.
+  if (x_f32 && M <= 16 && !lnw && K == XS_NW * XS_KPW * 32 && (a.ntiles % 2) == 0 && splitk <= 1 && xs_mode() &&
+      !g_force_nt && !g_force_nw && swiglu && (long long)a.ntiles * 16 * K >= (64ll << 20) && ldx % 4 == 0) {
+    const int units = a.ntiles / 2;
+    // as many workgroups as it takes for every one to get the same (ceil) number of units: 1184 gate/up
+    // pairs -> 237 x 5 (not 256 with 4 or 5: the 5-unit CUs would set the time); a CU can pull more than
+    // its 1/256 share of the HBM stream, so the idle CUs cost nothing
+    const int per = (units + num_cus() - 1) / num_cus();
+    const int G = (units + per - 1) / per;
+    a.S = 1;
+    if (sgroups) *sgroups = units;
+    if (sout) FO_REQUIRE(!swiglu && !rope, "fo_gemm: statistics with a paired epilogue");
+    if (swiglu) hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 1>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    else if (rope) hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 2>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    else hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 0>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    return fo::check_launch("fo_gemm/xs");
   }
   // mid-size row counts on large weights (the Qwen2 prefills of a turn: assistant prefix, the first
   // chunk with its chat prefix, the system prompt; 17..64 rows): one row tile of ceil(M/16) row blocks
@@ -888,6 +1079,15 @@ int fo_gemm_set_pipe(int on) {
   FO_REQUIRE(on >= 0 && on <= 3, "fo_gemm_set_pipe: 0 (off), 1 (U k-steps), 2 (2 k-steps) or 3 (policy)");
   const int prev = g_pipe;
   g_pipe = on;
+  return prev;
+}
+
+// X-stationary kernel switch for the eligible M <= 16 GEMMs (k_gemm_xs): 0 off, 1 on.  Process-global
+// (sweeps, A/B); returns the previous setting.  Unset, FO_GEMM_XS (default on) decides.
+int fo_gemm_set_xs(int on) {
+  FO_REQUIRE(on == 0 || on == 1, "fo_gemm_set_xs: 0 or 1");
+  const int prev = xs_mode() ? 1 : 0;
+  g_xs = on;
   return prev;
 }
 

@@ -41,6 +41,7 @@ _SIGS = {
     "fo_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
     "fo_event_destroy": (c_int, [c_vp]),
     "fo_gemm_tune": (c_int, [c_int, c_int]),
+    "fo_gemm_set_xs": (c_int, [c_int]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),

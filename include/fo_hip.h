@@ -77,6 +77,10 @@ int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void
                      float* rsum, float* rsumsq, int* sgroups, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
+/* X-stationary persistent weight stream (k_gemm_xs) for the M <= 16 fp32-X GEMMs with K = 3584 (Qwen2 q|k|v,
+ * o, gate/up, lm_head): 0 off, 1 on (default; FO_GEMM_XS=0 turns it off).  Process-global; returns the
+ * previous setting. */
+int fo_gemm_set_xs(int on);
 /* Software-pipelined one-row-tile fp32-X weight-stream GEMMs (M <= 16, >= 32 MB of weights: the next
  * k-group's weights + X in flight during this group's MFMAs).  3 (default): the measured policy; 0: plain
  * loops; 1 / 2: every such GEMM pipelined with 4 / 2 k-steps per group (sweeps).  Unset, the
