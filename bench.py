@@ -26,7 +26,22 @@ import os
 import sys
 import time
 
-import numpy as np
+
+def _blas_threads_from_argv(default=16):
+    """--cpu-threads, read before numpy is imported so the BLAS pool is created at that size."""
+    n = default
+    for i, a in enumerate(sys.argv):
+        if a == "--cpu-threads" and i + 1 < len(sys.argv):
+            n = int(sys.argv[i + 1])
+        elif a.startswith("--cpu-threads="):
+            n = int(a.split("=", 1)[1])
+    return n
+
+
+for _k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS", "BLIS_NUM_THREADS"):
+    os.environ[_k] = str(_blas_threads_from_argv())
+
+import numpy as np  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "freeze-omni_amd"))
@@ -49,7 +64,9 @@ def parse():
     ap.add_argument("--scenario", default="turn", choices=["turn", "duplex"],
                     help="turn: config 3 (default, the headline line); duplex: config 5 sessions")
     ap.add_argument("--duplex-sec", type=float, default=60.0, help="duplex: seconds of audio per session")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="BLAS threads of the cpu_baseline leg (set before numpy is imported)")
+    ap.add_argument("--no-single-user", action="store_true", help="skip the config-2 (1 user) leg")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
 
@@ -154,89 +171,108 @@ def run_turn(engine, base_kv, pcms, args, sync):
     return dict(t_ss=t_ss, first=first, last=last, samples=samples, first_pcm=[s.t_first_pcm for s in states])
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(cfg_name, threads, seconds_audio, n_chunks, text_tokens, codec_tokens):
-    """Oracle (numpy port) timed on host cores on a bounded sample at REAL geometry, scaled to the
-    metric: per-unit costs U1 (chunk step), U2 (text token), U3 (codec token), U4 (vocoder call)
-    measured on a subset of layers and extrapolated linearly in layer count."""
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    """Oracle (numpy fp32 port of the reference path, oracle/nets.py) timed on host cores at REAL geometry,
+    one unit of each kind at FULL depth: U1 = one 160 ms chunk through the 24-block encoder, the adapter
+    and all 28 Qwen2 layers + state head; U2 = one text token through the 28 layers + lm_head; U3 = one
+    codec token through the 4 AR layers + out_fnn; U4 = one 60-token vocoder call.  Only chunk / token /
+    call COUNTS are extrapolated to the turn (no layer extrapolation).  Weights: one random array per
+    parameter shape, shared by every layer of that shape (the GEMMs still stream their operands from DRAM:
+    each shape's array is far beyond the last-level cache), so the sample needs ~3 GB of host RAM, not
+    the 30 GB of distinct fp32 Qwen2 weights.  BLAS threads are set before numpy is imported
+    (_blas_threads_from_argv) and verified with threadpoolctl."""
     sys.path.insert(0, ROOT)
     from oracle import configs, nets, params
     cfg = configs.get(cfg_name)
     rng = np.random.default_rng(0)
-    n_llm = cfg["llm"]["num_hidden_layers"]
-    n_enc = cfg["train_yaml"]["encoder_conf"]["para_conf"]["transformer"]["transformer-num-blocks"]
-    sub = {"llm": 2, "enc": 2}
-    c2 = configs.get(cfg_name)
-    c2["llm"]["num_hidden_layers"] = sub["llm"]
-    c2["train_yaml"]["encoder_conf"]["para_conf"]["transformer"]["transformer-num-blocks"] = sub["enc"]
 
-    class Rand(dict):
+    class Shared(dict):
         def __init__(self, shapes):
             super().__init__()
-            self.shapes = shapes
+            self.shapes, self.by_shape = shapes, {}
 
         def __missing__(self, k):
-            shp = self.shapes[k]
-            v = (rng.standard_normal(shp, dtype=np.float32) * (0.02 if len(shp) > 1 else 0.1)).astype(np.float32)
-            if k.endswith(("norm.weight", "norm1.weight", "norm2.weight", "layernorm.weight")) or "running_var" in k \
-                    or "istd" in k:
-                v = np.abs(v) + 1.0
-            self[k] = v
-            return v
+            shp = tuple(self.shapes[k])
+            pos = k.endswith(("norm.weight", "norm1.weight", "norm2.weight", "layernorm.weight")) or \
+                "running_var" in k or "istd" in k
+            key = (shp, pos)
+            if key not in self.by_shape:
+                v = (rng.standard_normal(shp, dtype=np.float32) * np.float32(0.02 if len(shp) > 1 else 0.1))
+                self.by_shape[key] = (np.abs(v) + np.float32(1.0)) if pos else v
+            self[k] = self.by_shape[key]
+            return self[k]
 
-    W = Rand(params.all_shapes(c2))
-    enc, ada = nets.Encoder(W, c2, "user"), nets.Adapter(W, c2, "user")
-    llm = nets.Qwen2(W, c2)
-    feats = rng.standard_normal((19, 80)).astype(np.float32) * 3 + 8
-    kv = nets.KV(sub["llm"])
-    llm.forward(rng.standard_normal((40, c2["llm"]["hidden_size"])).astype(np.float32), kv)
-    est = nets.new_encoder_state(sub["enc"])
-    ac = None
-    t = time.perf_counter()
-    reps = 2
-    for _ in range(reps):
+    W = Shared(params.all_shapes(cfg))
+    for k in W.shapes:   # generate (and first-touch) every shared array before anything is timed
+        W[k]
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+        limiter = threadpool_limits(limits=threads, user_api="blas")
+        blas = [d for d in threadpool_info() if d.get("user_api") == "blas"]
+        used = max((int(d.get("num_threads", 0)) for d in blas), default=threads)
+        blas_lib = ",".join(sorted({d.get("internal_api", "?") for d in blas}))
+    except Exception:   # threadpoolctl missing: the env vars set before the numpy import still hold
+        limiter, used, blas_lib = None, threads, "unknown"
+    try:
+        enc, ada = nets.Encoder(W, cfg, "user"), nets.Adapter(W, cfg, "user")
+        llm = nets.Qwen2(W, cfg)
+        D = cfg["llm"]["hidden_size"]
+        feats = rng.standard_normal((19, 80)).astype(np.float32) * 3 + 8
+        kv = nets.KV(cfg["llm"]["num_hidden_layers"])
+        llm.forward(rng.standard_normal((40, D)).astype(np.float32), kv)   # system prompt context
+        est = nets.new_encoder_state(enc.nb)
+        ac = None
+        enc.infer(feats, est)   # warm (first-touch page faults of the shared arrays)
+        t = time.perf_counter()
         e = enc.infer(feats, est)
         a, ac = ada(e, ac)
-        llm.forward(a, kv)
-    u1_sub = (time.perf_counter() - t) / reps
-    # split the measured sub-stack time into encoder and LLM parts to extrapolate each
-    t = time.perf_counter()
-    for _ in range(reps):
-        enc.infer(feats, est)
-    u1_enc = (time.perf_counter() - t) / reps
-    u1 = u1_enc * n_enc / sub["enc"] + (u1_sub - u1_enc) * n_llm / sub["llm"]
-    t = time.perf_counter()
-    for _ in range(reps):
-        h = llm.forward(rng.standard_normal((1, c2["llm"]["hidden_size"])).astype(np.float32), kv)
-    u2_layers = (time.perf_counter() - t) / reps
-    t = time.perf_counter()
-    llm.logits(h)
-    u2 = u2_layers * n_llm / sub["llm"] + (time.perf_counter() - t)
-    tts = nets.TTSDecoder(W, c2)
-    idim = c2["decoder_json"][0]
-    kvt, P = tts.prefill(rng.standard_normal((32, idim)).astype(np.float32),
-                         rng.standard_normal((32, idim)).astype(np.float32))
-    t = time.perf_counter()
-    n3 = 5
-    for i in range(n3):
-        tts.step(5 + i, kvt, P)
-    u3 = (time.perf_counter() - t) / n3
-    codec = nets.Codec(W, c2)
-    t = time.perf_counter()
-    codec(rng.integers(0, c2["codec_json"]["n_codes"], 60))
-    u4 = time.perf_counter() - t
+        h = llm.forward(a, kv)
+        nets.state_probs(W, h)
+        u1 = time.perf_counter() - t
+        t = time.perf_counter()
+        h = llm.forward(rng.standard_normal((1, D)).astype(np.float32), kv)
+        llm.logits(h)
+        u2 = time.perf_counter() - t
+        tts = nets.TTSDecoder(W, cfg)
+        idim = cfg["decoder_json"][0]
+        kvt, P = tts.prefill(rng.standard_normal((32, idim)).astype(np.float32),
+                             rng.standard_normal((32, idim)).astype(np.float32))
+        tts.step(4, kvt, P)
+        t = time.perf_counter()
+        n3 = 5
+        for i in range(n3):
+            tts.step(5 + i, kvt, P)
+        u3 = (time.perf_counter() - t) / n3
+        codec = nets.Codec(W, cfg)
+        t = time.perf_counter()
+        codec(rng.integers(0, cfg["codec_json"]["n_codes"], 60))
+        u4 = time.perf_counter() - t
+    finally:
+        if limiter is not None:
+            limiter.restore_original_limits()
     n_voc = 1 + max(0, (codec_tokens - 50 + 39) // 40)
     turn = n_chunks * u1 + text_tokens * u2 + codec_tokens * u3 + n_voc * u4
     speak = text_tokens * u2 + codec_tokens * u3 + n_voc * u4
-    return {"value": round(seconds_audio / turn, 4), "unit": "x real-time (1 user, 1 turn)", "cores": threads,
+    return {"value": round(seconds_audio / turn, 4), "unit": "x real-time (1 user, 1 turn)", "cores": used,
             "kind": "port",
-            "sample": (f"numpy fp32 oracle at REAL geometry on {threads} host threads; per-unit times measured on "
-                       f"{sub['llm']}/{n_llm} Qwen2 layers and {sub['enc']}/{n_enc} encoder blocks (extrapolated "
-                       f"linearly), full TTS layers and a full 60-token vocoder call: U1 chunk {u1 * 1e3:.1f} ms, "
-                       f"U2 text token {u2 * 1e3:.1f} ms, U3 codec token {u3 * 1e3:.2f} ms, U4 vocoder "
-                       f"{u4 * 1e3:.1f} ms; turn = {n_chunks} U1 + {text_tokens} U2 + {codec_tokens} U3 + "
-                       f"{n_voc} U4 for {seconds_audio:.0f} s of speech"),
+            "sample": (f"numpy fp32 oracle (oracle/nets.py) at REAL geometry, {used} BLAS threads ({blas_lib}) of "
+                       f"{os.cpu_count()} host CPUs ({cpu_model()}); one unit of each kind at full depth (24 encoder "
+                       f"blocks, 28 Qwen2 layers, 4 AR layers): U1 chunk {u1 * 1e3:.1f} ms, U2 text token "
+                       f"{u2 * 1e3:.1f} ms, U3 codec token {u3 * 1e3:.2f} ms, U4 vocoder {u4 * 1e3:.1f} ms; "
+                       f"turn = {n_chunks} U1 + {text_tokens} U2 + {codec_tokens} U3 + {n_voc} U4 for "
+                       f"{seconds_audio:.0f} s of speech (counts extrapolated, layers not)"),
             "speak_rtf_per_user": round(seconds_audio / speak, 4),
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "units_ms": {"U1": u1 * 1e3, "U2": u2 * 1e3, "U3": u3 * 1e3, "U4": u4 * 1e3}}
 
 
@@ -269,9 +305,24 @@ def recorded_traffic(kernel_regex):
     return g["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def recorded_kernel_avg_us(kernel_regex):
+    """Average duration of the dominant kernel in the newest committed rocprofv3 --kernel-trace --stats
+    summary (profiles/rNN_kernel_stats.csv, the same bench command under the profiler)."""
+    import csv
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.csv")))
+    for f in reversed(files):
+        rows = [r for r in csv.DictReader(open(f)) if re.search(kernel_regex, r["Name"])]
+        if rows:
+            r = max(rows, key=lambda r: int(r["Calls"]))
+            return float(r["AverageNs"]) / 1e3, int(r["Calls"]), os.path.relpath(f, ROOT)
+    return None, None, None
+
+
 def gemm_probe(engine, M, reps=2):
-    """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the
-    k_gemm_wstream<4,1,true,...,true> launch of every layer) with HIP events on the launching stream.
+    """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the X-stationary
+    k_gemm_xs<8,14,1> launch of every layer) with HIP events on the launching stream.
     The launches walk all layers' gate/up weights in order, as a chunk step does, so no launch finds
     its weights in the Infinity Cache from the previous one (273 MB per layer > 256 MB MALL)."""
     import torch
@@ -431,7 +482,9 @@ def main():
     from fo.engine import FreezeOmniEngine
     model_dir = os.path.join(ROOT, "configs", args.config)
     t0 = time.perf_counter()
-    eng = FreezeOmniEngine(model_dir, device=dev, max_sessions=max(8, args.users))
+    # ranks > 0 allocate the packed layouts without generating or reading weights: rank 0's broadcast fills them
+    eng = FreezeOmniEngine(model_dir, device=dev, max_sessions=max(8, args.users), receive_weights=dist is not None
+                           and rank > 0)
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     bcast_s = bcast_bytes = None
@@ -476,6 +529,21 @@ def main():
     lat = [(f - s["t_ss"]) * 1e3 for s in stats for f in s["first_pcm"] if f is not None]
     lat_gated = [(f - s["t_ss"]) * 1e3 for s in stats for f in s["first"] if f is not None]
     rtf_user = [(n / sr) / (l - s["t_ss"]) for s in stats for n, l in zip(s["samples"], s["last"]) if l is not None]
+    # config 2 from the same invocation: one user alone on the replica (1 warm-up turn + 1 timed turn)
+    single = None
+    if args.users > 1 and not args.no_single_user:
+        run_turn(eng, base_kv, pcms[:1], args, sync)
+        sync()
+        t1 = time.perf_counter()
+        s1 = run_turn(eng, base_kv, pcms[:1], args, sync)
+        sync()
+        w1 = time.perf_counter() - t1
+        a1 = s1["samples"][0] / 24000.0
+        single = {"workload": "config 2: 1 user on 1 GPU, 10 s input, same turn",
+                  "ms_per_turn": round(w1 * 1e3, 2), "value": round(a1 / w1, 3),
+                  "first_audio_ms": round((s1["first_pcm"][0] - s1["t_ss"]) * 1e3, 2),
+                  "first_emit_gated_ms": round((s1["first"][0] - s1["t_ss"]) * 1e3, 2),
+                  "rtf_per_user": round(a1 / (s1["last"][0] - s1["t_ss"]), 3)}
     probe = gemm_probe(eng, 2 * args.users)
     if dist is not None:
         t = torch.tensor([wall, audio], dtype=torch.float64, device=dev)
@@ -489,7 +557,9 @@ def main():
     if rank == 0:
         peak = 8000.0
         # the SwiGLU (last template flag true) M<=16 weight stream: Qwen2 gate/up of every layer
-        traffic, traffic_src = recorded_traffic(r"k_gemm_wstream<\d, 1, true, \d+, \d, true>")
+        kre = r"k_gemm_xs<\d+, \d+, 1>"
+        traffic, traffic_src = recorded_traffic(kre)
+        rp_us, rp_calls, rp_src = recorded_kernel_avg_us(kre)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -521,8 +591,16 @@ def main():
                          "frac": round(probe["gbps"] / peak, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
-                         "kernel": "k_gemm_wstream<4,1,true,4,4,true> (Qwen2 gate/up SwiGLU weight stream, M=16, all 28 layers in turn)",
-                         "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2)},
+                         "kernel": "k_gemm_xs<8,14,1> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all "
+                                   "28 layers in turn)",
+                         "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2),
+                         "frac_source": "live: HIP events around every layer's gate/up launch on the engine stream "
+                                        "(gemm_probe); rocprof_* = the committed rocprofv3 summary of this command",
+                         "rocprof_avg_launch_us": None if rp_us is None else round(rp_us, 2),
+                         "rocprof_calls": rp_calls,
+                         "rocprof_frac": None if rp_us is None else round(probe["bytes"] / (rp_us * 1e-6) / 1e9 / peak, 4),
+                         "rocprof_source": rp_src},
+            "single_user": single,
             "cpu_baseline": cpu,
         }
         s = json.dumps(line)

@@ -48,10 +48,14 @@ def load_model_dir(model_path, llm_path=None):
     return cfg, synth, llm_path
 
 
-def make_source(cfg, synth, device, model_path=None, llm_path=None):
+def make_source(cfg, synth, device, model_path=None, llm_path=None, receive=False):
     """synthetic.json in the model dir -> counter-hash weights generated on the device; otherwise the
     reference's checkpoint files (fo.checkpoint: audiollm/final.pt, the Qwen2 safetensors,
-    decoder/final.pt, codec/final.pt)."""
+    decoder/final.pt, codec/final.pt).  receive=True: a replica that gets its weights from rank 0's
+    broadcast (fo.replica) -- shapes only, nothing is read or generated."""
+    if receive:
+        from .weights import ReceiveSource
+        return ReceiveSource(all_shapes(cfg), device)
     if synth is not None:
         return SynthSource(synth["seed"], all_shapes(cfg), device, {k: tuple(v) for k, v in
                                                                    synth.get("overrides", {}).items()})
@@ -61,13 +65,16 @@ def make_source(cfg, synth, device, model_path=None, llm_path=None):
 
 class FreezeOmniEngine:
     def __init__(self, model_path, llm_path=None, device="cuda:0", max_sessions=64, llm_kv_tokens=None,
-                 tts_kv_tokens=None, source=None):
+                 tts_kv_tokens=None, source=None, receive_weights=False):
+        """receive_weights=True: allocate every packed layout without reading or generating weights; the
+        caller fills them with fo.replica.broadcast_frozen(engine, dist) from rank 0 before any use."""
         if not torch.cuda.is_available():
             raise RuntimeError("FreezeOmniEngine needs an MI355X (gfx950) device: there is no CPU fallback")
         self.device = torch.device(device)
         torch.cuda.set_device(self.device)
         self.cfg, self.synth, self.llm_path = load_model_dir(model_path, llm_path)
-        src = source or make_source(self.cfg, self.synth, self.device, model_path, self.llm_path)
+        src = source or make_source(self.cfg, self.synth, self.device, model_path, self.llm_path,
+                                    receive=receive_weights)
         self.src = src
         self.max_sessions = max_sessions
         ty = self.cfg["train_yaml"]

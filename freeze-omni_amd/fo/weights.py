@@ -103,3 +103,19 @@ class OverlaySource:
 
     def get(self, name, dtype=torch.float32):
         return (self.primary if name in self.primary else self.fallback).get(name, dtype)
+
+
+class ReceiveSource:
+    """Shapes only: every get() returns an UNINITIALISED tensor of the parameter's shape.  A replica that
+    receives its frozen weights from rank 0 (fo.replica.broadcast_frozen) builds its packed layouts from
+    this source: no checkpoint read, no hash fill -- the broadcast then overwrites every frozen tensor
+    (derived ones such as packed GEMM weights and folded BatchNorm affines included)."""
+
+    def __init__(self, shapes, device):
+        self.shapes, self.device = dict(shapes), torch.device(device)
+
+    def __contains__(self, name):
+        return name in self.shapes
+
+    def get(self, name, dtype=torch.float32):
+        return torch.empty(tuple(self.shapes[name]), dtype=dtype, device=self.device)

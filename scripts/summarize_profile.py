@@ -46,7 +46,7 @@ def main(r):
         for x in rows[:30]:
             f.write(f"| {float(x['Percentage']):.2f} | {x['Calls']} | {float(x['AverageNs']) / 1e3:.2f} | "
                     f"`{x['Name'][:100]}` |\n")
-        f.write("\n## FETCH_SIZE (separate --pmc pass, k_gemm_wstream only)\n\n| kernel | grid | n | MB/launch |\n"
+        f.write("\n## FETCH_SIZE (separate --pmc pass on the dominant kernel, scripts/gpu_profile.sh FETCH_RE)\n\n| kernel | grid | n | MB/launch |\n"
                 "|---|---|---|---|\n")
         for g in fetch:
             f.write(f"| `{g['kernel'][:70]}` | {g['grid']} | {g['dispatches']} | "
