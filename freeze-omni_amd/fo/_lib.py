@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfo_hip.so")
+LIB_PATH = os.environ.get("FO_LIB_PATH") or os.path.join(_HERE, "libfo_hip.so")   # override: A/B sweeps only
 
 c_int = ctypes.c_int
 c_ll = ctypes.c_longlong
