@@ -151,9 +151,13 @@ __global__ __launch_bounds__(1024) void k_silence_cut(const float* x, int L, int
   cs[threadIdx.x + 1] = loc;
   if (threadIdx.x == 0) cs[0] = 0.0;
   __syncthreads();
-  if (threadIdx.x == 0)
-    for (int i = 1; i <= 1024; ++i) cs[i] += cs[i - 1];
-  __syncthreads();
+  // inclusive scan of the 1024 chunk sums (log-step in LDS; a serial thread-0 loop cost ~40 us)
+  for (int off = 1; off < 1024; off <<= 1) {
+    const double v = threadIdx.x >= off ? cs[threadIdx.x + 1 - off] : 0.0;
+    __syncthreads();
+    cs[threadIdx.x + 1] += v;
+    __syncthreads();
+  }
   // window sum at w: S(w) = P(start + w + N) - P(start + w), P(k) = sum_{i<k} |x_i|
   auto P = [&](int k) -> double {
     const int c = k / per;

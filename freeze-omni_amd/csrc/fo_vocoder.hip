@@ -30,21 +30,34 @@ struct ConvArgs {
   int nks_c;           // k-steps per Cin chunk
   int pre_act;         // leaky ReLU on the input
   float slope;
-  int residual;        // out += conv
+  // epilogue: out = (conv + bias + res + res2) * oscale + gadd[b][co]; res / res2 are [B][Tout_total][Cout]
+  // like out and may alias it (each element is read and written by the same lane)
+  const float* res;
+  const float* res2;
+  float oscale;
+  const float* gadd;   // [B][Cout] or null
 };
+
+constexpr int CONV_KMAX = 11;
+// k-steps per Cin chunk, rounded up to even (padding k-steps carry zero weights)
+__host__ __device__ constexpr int nks_per_chunk(int K, int CK) { return ((K * CK + 31) / 32 + 1) & ~1; }
+__host__ __device__ constexpr int conv_wmax(int CK) { return nks_per_chunk(CONV_KMAX, CK); }
 
 template <int MTW, int NTW, int CK>
 __global__ __launch_bounds__(256) void k_conv_cl(ConvArgs a) {
   constexpr int TW = 64 * NTW;     // time steps per workgroup (4 waves x 16*NTW)
   constexpr int ROWS = TW + HALO;
-  constexpr int LP = CK + 4;       // padded row: 16 lanes of different rows hit distinct banks
-  __shared__ float xs[ROWS][LP];
+  constexpr int LP = CK + 8;       // padded bf16 row (16 B): 16 lanes of different rows hit distinct banks
+  // the window is split into bf16 hi + lo ONCE when staged; every k-step's B fragments are then two
+  // 16-B LDS reads with no conversion (the split in the k-loop made the kernel VALU-bound)
+  __shared__ __attribute__((aligned(16))) __bf16 xh[ROWS][LP];
+  __shared__ __attribute__((aligned(16))) __bf16 xl[ROWS][LP];
+  __shared__ __attribute__((aligned(16))) bf16_t wl[MTW * conv_wmax(CK) * 512];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t0 = blockIdx.x * TW;
   const int ct0 = blockIdx.y * MTW;  // first 16-channel output tile
   const int b = blockIdx.z;
-  const int nchunks = a.Cin / CK;
-  const int nks = nchunks * a.nks_c;
+  const int nks = (a.Cin / CK) * a.nks_c;
   const int span = TW + a.dil * (a.K - 1);
   const float* xb = a.x + (size_t)b * a.Tin * a.Cin;
 
@@ -54,78 +67,126 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvArgs a) {
 #pragma unroll
     for (int n = 0; n < NTW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bf16x8* wpl = reinterpret_cast<const bf16x8*>(a.wp) + lane;
   const int tl = wave * 16 * NTW + (lane & 15);  // this lane's time row (tile n adds 16 n)
   const int kq = 8 * (lane >> 4);                 // this lane's 8-wide K slice inside a step
 
-  for (int c = 0; c < nchunks; ++c) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < span * (CK / 4); e += 256) {
+  // A chunk's weight A-fragments (MTW tiles x nks_c k-steps, 1 KiB each) are copied global -> LDS
+  // with 16-B LDS-DMA loads (lane-linear, exactly one fragment per wave-instruction), issued with the
+  // activation loads: one memory latency per chunk, and the four waves share one copy.
+  // Staging: every thread issues all of its window loads for the chunk back to back (MAXL 16-B loads,
+  // one latency per chunk instead of one per loop trip), then splits them into LDS.
+  constexpr int MAXL = (ROWS * (CK / 4) + 255) / 256;
+  auto stage = [&](int c) {
+    __syncthreads();  // the previous chunk's reads are done
+    for (int f = wave; f < MTW * a.nks_c; f += 4) {
+      const int m = f / a.nks_c, st = f - m * a.nks_c;
+      const bf16_t* src = a.wp + ((size_t)(ct0 + m) * nks + c * a.nks_c + st) * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)&wl[f * 512], 16, 0, 0);
+    }
+    float4 v[MAXL];
+#pragma unroll
+    for (int i = 0; i < MAXL; ++i) {
+      const int e = threadIdx.x + 256 * i;
       const int row = e / (CK / 4), c4 = e % (CK / 4);
       const int ti = t0 - a.pad + row;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ti >= 0 && ti < a.Tin) {
-        v = *reinterpret_cast<const float4*>(xb + (size_t)ti * a.Cin + c * CK + c4 * 4);
-        if (a.pre_act) {
-          v.x = v.x < 0.f ? v.x * a.slope : v.x;
-          v.y = v.y < 0.f ? v.y * a.slope : v.y;
-          v.z = v.z < 0.f ? v.z * a.slope : v.z;
-          v.w = v.w < 0.f ? v.w * a.slope : v.w;
-        }
-      }
-      *reinterpret_cast<float4*>(&xs[row][c4 * 4]) = v;
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < span * (CK / 4) && ti >= 0 && ti < a.Tin)
+        v[i] = *reinterpret_cast<const float4*>(xb + (size_t)ti * a.Cin + c * CK + c4 * 4);
     }
+#pragma unroll
+    for (int i = 0; i < MAXL; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e >= span * (CK / 4)) break;
+      const int row = e / (CK / 4), c4 = e % (CK / 4);
+      float f[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+      __attribute__((ext_vector_type(4))) __bf16 h4, l4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (a.pre_act) f[q] = f[q] < 0.f ? f[q] * a.slope : f[q];
+        const __bf16 h = (__bf16)f[q];
+        h4[q] = h;
+        l4[q] = (__bf16)(f[q] - (float)h);
+      }
+      *reinterpret_cast<decltype(h4)*>(&xh[row][c4 * 4]) = h4;
+      *reinterpret_cast<decltype(l4)*>(&xl[row][c4 * 4]) = l4;
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the LDS-DMA copies (vmcnt) too
     __syncthreads();
-    for (int s = 0; s < a.nks_c; ++s) {
-      const int ks = c * a.nks_c + s;
-      bf16x8 av[MTW];
+  };
+  auto comp = [&](int s) {
+    const int kk = s * 32 + kq;
+    int j = kk / CK;
+    const int cil = kk - j * CK;
+    if (j > a.K - 1) j = a.K - 1;  // padded K: the packed weights are zero there
+    const int rb = tl + j * a.dil;
+    bf16x8 av[MTW];
 #pragma unroll
-      for (int m = 0; m < MTW; ++m) av[m] = wpl[((size_t)(ct0 + m) * nks + ks) * 64];
-      const int kk = s * 32 + kq;
-      int j = kk / CK;
-      const int cil = kk - j * CK;
-      if (j > a.K - 1) j = a.K - 1;  // padded K: the packed weights are zero there
-      const int rb = tl + j * a.dil;
+    for (int m = 0; m < MTW; ++m) av[m] = *reinterpret_cast<const bf16x8*>(&wl[(m * a.nks_c + s) * 512 + lane * 8]);
 #pragma unroll
-      for (int n = 0; n < NTW; ++n) {
-        const float4 p0 = *reinterpret_cast<const float4*>(&xs[rb + 16 * n][cil]);
-        const float4 p1 = *reinterpret_cast<const float4*>(&xs[rb + 16 * n][cil + 4]);
-        const float f[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-        bf16x8 hi, lo;
+    for (int n = 0; n < NTW; ++n) {
+      const bf16x8 hi = *reinterpret_cast<const bf16x8*>(&xh[rb + 16 * n][cil]);
+      const bf16x8 lo = *reinterpret_cast<const bf16x8*>(&xl[rb + 16 * n][cil]);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const __bf16 h = (__bf16)f[i];
-          hi[i] = h;
-          lo[i] = (__bf16)(f[i] - (float)h);
-        }
-#pragma unroll
-        for (int m = 0; m < MTW; ++m) {
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], hi, acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], lo, acc[m][n], 0, 0, 0);
-        }
+      for (int m = 0; m < MTW; ++m) {
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], hi, acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], lo, acc[m][n], 0, 0, 0);
       }
     }
+  };
+  const int nchunks = a.Cin / CK;
+  for (int c = 0; c < nchunks; ++c) {
+    stage(c);
+    for (int s = 0; s < a.nks_c; ++s) comp(s);
   }
-  // C layout: row (output channel) = 4*(lane>>4) + i, column (time) = lane & 15
+  // C layout: row (output channel) = 4*(lane>>4) + i, column (time) = lane & 15.  Every epilogue
+  // operand is loaded for all tiles first (one memory latency, not one per tile), rows past Tq read
+  // row Tq - 1 and are not stored.
+  float4 add[NTW][MTW];
+#pragma unroll
+  for (int n = 0; n < NTW; ++n)
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) add[n][m] = make_float4(0.f, 0.f, 0.f, 0.f);
+  size_t off[NTW];
 #pragma unroll
   for (int n = 0; n < NTW; ++n) {
-    const int q = t0 + tl + 16 * n;
-    if (q >= a.Tq) continue;
-    const int t = q * a.ostride + a.ooff;
+    const int q = min(t0 + tl + 16 * n, a.Tq - 1);
+    off[n] = ((size_t)b * a.Tout_total + (size_t)q * a.ostride + a.ooff) * a.Cout + (ct0 * 16 + kq / 2);
+  }
+  const float* rs[2] = {a.res, a.res2};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (!rs[r]) continue;
+    float4 v[NTW][MTW];
+#pragma unroll
+    for (int n = 0; n < NTW; ++n)
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) v[n][m] = *reinterpret_cast<const float4*>(rs[r] + off[n] + m * 16);
+#pragma unroll
+    for (int n = 0; n < NTW; ++n)
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        add[n][m].x += v[n][m].x; add[n][m].y += v[n][m].y; add[n][m].z += v[n][m].z; add[n][m].w += v[n][m].w;
+      }
+  }
+  float4 bb[MTW], gg[MTW];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) {
+    const int co = (ct0 + m) * 16 + kq / 2;
+    bb[m] = a.bias ? *reinterpret_cast<const float4*>(a.bias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gg[m] = a.gadd ? *reinterpret_cast<const float4*>(a.gadd + (size_t)b * a.Cout + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) {
+    if (t0 + tl + 16 * n >= a.Tq) continue;
 #pragma unroll
     for (int m = 0; m < MTW; ++m) {
-      const int co = (ct0 + m) * 16 + kq / 2;  // 4*(lane>>4)
-      float4 v = make_float4(acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]);
-      if (a.bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(a.bias + co);
-        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
-      }
-      float4* o = reinterpret_cast<float4*>(a.out + ((size_t)b * a.Tout_total + t) * a.Cout + co);
-      if (a.residual) {
-        const float4 r = *o;
-        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-      }
-      *o = v;
+      float4 v;
+      v.x = (acc[m][n][0] + bb[m].x + add[n][m].x) * a.oscale + gg[m].x;
+      v.y = (acc[m][n][1] + bb[m].y + add[n][m].y) * a.oscale + gg[m].y;
+      v.z = (acc[m][n][2] + bb[m].z + add[n][m].z) * a.oscale + gg[m].z;
+      v.w = (acc[m][n][3] + bb[m].w + add[n][m].w) * a.oscale + gg[m].w;
+      *reinterpret_cast<float4*>(a.out + off[n] + m * 16) = v;
     }
   }
 }
@@ -191,8 +252,14 @@ __global__ void k_scale_add_cl(float* y, int B, int T, int C, float s, const flo
 }
 
 // conv_post (Cout = 1) + tanh: out[b][t] = tanh(bias + sum_{j,ci} w[ci][j] leaky(x[t + j - pad][ci]))
-__global__ void k_conv_post_cl(const float* x, int B, int T, int C, const bf16_t* w, const float* bias, int K,
-                               int pad, float slope, float* out) {
+// One output per thread; the taps x channels weights sit in LDS as fp32, every input row is read as
+// float4s (neighbouring threads share K-1 of their K rows, served by L1/L2).
+constexpr int POST_MAXW = 4096;
+__global__ __launch_bounds__(256) void k_conv_post_cl(const float* x, int B, int T, int C, const bf16_t* w,
+                                                      const float* bias, int K, int pad, float slope, float* out) {
+  __shared__ float ws[POST_MAXW];  // [K][C]
+  for (int i = threadIdx.x; i < K * C; i += 256) ws[i] = bf2f(w[(size_t)(i % C) * K + i / C]);
+  __syncthreads();
   const long long total = (long long)B * T;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
@@ -201,11 +268,13 @@ __global__ void k_conv_post_cl(const float* x, int B, int T, int C, const bf16_t
     for (int j = 0; j < K; ++j) {
       const int ti = t + j - pad;
       if (ti < 0 || ti >= T) continue;
-      const float* xr = x + ((size_t)b * T + ti) * C;
-      for (int ci = 0; ci < C; ++ci) {
-        float v = xr[ci];
-        v = v < 0.f ? v * slope : v;
-        acc += v * bf2f(w[(size_t)ci * K + j]);
+      const float4* xr = reinterpret_cast<const float4*>(x + ((size_t)b * T + ti) * C);
+      const float* wj = ws + j * C;
+      for (int c4 = 0; c4 < C / 4; ++c4) {
+        const float4 v = xr[c4];
+        const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc += (f[i] < 0.f ? f[i] * slope : f[i]) * wj[c4 * 4 + i];
       }
     }
     out[e] = tanhf(acc);
@@ -219,13 +288,14 @@ inline int grid_for(long long n) {
 
 inline int pick_ck(int Cin) { return Cin >= 64 ? 64 : Cin; }
 
+
 }  // namespace
 
 extern "C" {
 
 long long fo_conv_pack_elems(int Cout, int Cin, int K) {
   const int CK = pick_ck(Cin);
-  const int nks_c = (K * CK + 31) / 32;
+  const int nks_c = nks_per_chunk(K, CK);
   return (long long)(Cout / 16) * (Cin / CK) * nks_c * 64 * 8;
 }
 
@@ -237,7 +307,7 @@ int fo_pack_conv(const void* W, int src_bf16, int Cout, int Cin, int K, int tran
              K);
   const int CK = pick_ck(Cin);
   FO_REQUIRE(Cin % CK == 0, "fo_pack_conv: Cin=%d not a multiple of %d", Cin, CK);
-  const int nks_c = (K * CK + 31) / 32;
+  const int nks_c = nks_per_chunk(K, CK);
   const long long total = (long long)(Cout / 16) * (Cin / CK) * nks_c * 64;
   hipLaunchKernelGGL(k_pack_conv, dim3(grid_for(total)), dim3(256), 0, s, W, src_bf16, Cout, Cin, K, CK, nks_c,
                      transposed, Ktot, j0, u, (bf16_t*)out);
@@ -245,28 +315,40 @@ int fo_pack_conv(const void* W, int src_bf16, int Cout, int Cin, int K, int tran
 }
 
 // Stride-1 conv on channel-last activations: x [B][Tin][Cin] -> out [B][Tout_total][Cout] at time
-// q * ostride + ooff for q < Tq (Tq = Tin + 2 pad - dil (K-1) for a plain conv).
+// q * ostride + ooff for q < Tq (Tq = Tin + 2 pad - dil (K-1) for a plain conv), with the fused
+// epilogue out = (conv + bias + res + res2) * oscale + gadd[b] (res, res2, gadd optional).
+// out must not alias x (other workgroups still read the input window).
 int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const float* bias, int Cout, int K, int dil,
                int pad, int Tq, int ostride, int ooff, int Tout_total, int pre_leaky, float slope, float* out,
-               int residual, hipStream_t s) {
+               const float* res, const float* res2, float oscale, const float* gadd, hipStream_t s) {
   FO_REQUIRE(Cout % 16 == 0 && Cin % 16 == 0 && Cin >= 16, "fo_conv_cl: Cout=%d Cin=%d", Cout, Cin);
-  FO_REQUIRE(K >= 1 && dil >= 1 && dil * (K - 1) <= HALO, "fo_conv_cl: K=%d dil=%d beyond the LDS halo", K, dil);
+  FO_REQUIRE(K >= 1 && K <= CONV_KMAX && dil >= 1 && dil * (K - 1) <= HALO,
+             "fo_conv_cl: K=%d dil=%d beyond the LDS halo / weight buffer", K, dil);
   FO_REQUIRE(Tq > 0 && (long long)(Tq - 1) * ostride + ooff < Tout_total, "fo_conv_cl: output range");
+  FO_REQUIRE((const void*)x != (const void*)out, "fo_conv_cl: out aliases the input");
   const int CK = pick_ck(Cin);
   ConvArgs a{x, (const bf16_t*)wp, bias, out, Cin, Tin, Cout, K, dil, pad, Tq, ostride, ooff, Tout_total,
-             (K * CK + 31) / 32, pre_leaky, slope, residual};
-  const int MTW = Cout >= 64 ? 4 : Cout / 16;
-  const int NTW = 8 / MTW;
+             nks_per_chunk(K, CK), pre_leaky, slope, res, res2, oscale, gadd};
+  int MTW = Cout >= 64 ? 4 : Cout / 16;
+  int NTW = 8 / MTW;
+  // short, wide stages (the first upsampling stages: Tq of a few hundred, 256-512 channels) would put
+  // only ~100 workgroups on 256 CUs: take 2 x 2 tiles per wave there (more workgroups, less reuse of
+  // the L2-resident weights, which costs little at these sizes)
+  if (MTW == 4 && (long long)((Tq + 127) / 128) * (Cout / 64) * B < 256) {
+    MTW = 2;
+    NTW = 2;
+  }
   dim3 grid((Tq + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B);
-  if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, a);
-  else if (MTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, a);
+  if (MTW == 2 && NTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 2, 64>), grid, dim3(256), 0, s, a);
+  else if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, a);
+  else if (MTW == 2 && NTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, a);
   else if (MTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 4, 32>), grid, dim3(256), 0, s, a);
   else if (MTW == 1 && CK == 32) hipLaunchKernelGGL((k_conv_cl<1, 8, 32>), grid, dim3(256), 0, s, a);
   else if (MTW == 1 && CK == 16) hipLaunchKernelGGL((k_conv_cl<1, 8, 16>), grid, dim3(256), 0, s, a);
   else if (MTW == 4 && CK == 32) hipLaunchKernelGGL((k_conv_cl<4, 2, 32>), grid, dim3(256), 0, s, a);
   else if (MTW == 4 && CK == 16) hipLaunchKernelGGL((k_conv_cl<4, 2, 16>), grid, dim3(256), 0, s, a);
   else if (MTW == 2 && CK == 16) hipLaunchKernelGGL((k_conv_cl<2, 4, 16>), grid, dim3(256), 0, s, a);
-  else if (MTW == 1 && CK == 64) hipLaunchKernelGGL((k_conv_cl<1, 8, 64>), grid, dim3(256), 0, s, a);
+  else if (MTW == 1 && CK == 64) hipLaunchKernelGGL((k_conv_cl<1, 4, 64>), dim3((Tq + 255) / 256, Cout / 16, B), dim3(256), 0, s, a);
   else FO_REQUIRE(false, "fo_conv_cl: no variant for Cout=%d Cin=%d", Cout, Cin);
   return fo::check_launch("fo_conv_cl");
 }
@@ -286,6 +368,7 @@ int fo_scale_add_cl(float* y, int B, int T, int C, float sc, const float* g, hip
 
 int fo_conv_post_cl(const float* x, int B, int T, int C, const void* w, const float* bias, int K, int pad, float slope,
                     float* out, hipStream_t s) {
+  FO_REQUIRE(C % 4 == 0 && K * C <= POST_MAXW, "fo_conv_post_cl: C=%d K=%d", C, K);
   const long long n = (long long)B * T;
   hipLaunchKernelGGL(k_conv_post_cl, dim3(grid_for(n)), dim3(256), 0, s, x, B, T, C, (const bf16_t*)w, bias, K, pad,
                      slope, out);

@@ -93,7 +93,7 @@ _SIGS = {
     "fo_conv_pack_elems": (c_ll, [c_int, c_int, c_int]),
     "fo_pack_conv": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "fo_conv_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                           c_int, c_int, c_float, c_vp, c_int, c_vp]),
+                           c_int, c_int, c_float, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
     "fo_codec_embed_cl": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp]),
     "fo_scale_add_cl": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_conv_post_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_float, c_vp, c_vp]),

@@ -3,13 +3,19 @@
 Reference: models/decoder/ticodec/vqvae.py:37-42 (quantizer.embed + embed_gst + generator),
 models/decoder/ticodec/models.py:59-166 (ResBlock1/2), :169-242 (Generator.forward).
 """
+import ctypes
+import os
+from types import SimpleNamespace
+
 import torch
 
-from . import ops
+from . import _lib, ops
 from .ops import F32, I32
 
 
 class CodecEngine:
+    MAX_GRAPHS = 16
+
     def __init__(self, src, codec_json, device):
         h = self.h = codec_json
         self.device = torch.device(device)
@@ -56,6 +62,8 @@ class CodecEngine:
                 off = (r + pad - j0) // u
                 phases.append((r, pc, pc.K - 1 - off))  # (phase, weights, pad of the equivalent conv)
             self.p_ups.append(phases)
+        self.use_graphs = os.environ.get("FO_CODEC_GRAPH", "1") != "0"
+        self._graphs = {}   # (B, T) -> static buffers (+ captured graph), least recently used first
         self.p_res = [[(k, [(ops.PackedConv(c1[0], c1[1]), c1[2], None if c2 is None else ops.PackedConv(c2[0], c2[1]))
                             for c1, c2 in convs]) for k, convs in stage] for stage in self.res]
 
@@ -73,47 +81,98 @@ class CodecEngine:
         f += 2 * C * 7 * L
         return f
 
+    def _buffers(self, B, T):
+        """Static activations of one (B, T) call: every conv reads and writes these, so the call can be
+        captured once as a hipGraph and replayed."""
+        dev, F = self.device, dict(dtype=F32, device=self.device)
+        E = self.codebook.shape[1]
+        bufs = SimpleNamespace(B=B, T=T, exec=None, ids=torch.empty(B, T, dtype=I32, device=dev),
+                               x0=torch.empty(B, T, E, **F), y0=torch.empty(B, T, self.U, **F),
+                               g=self.gfeat.view(1, -1).expand(B, -1).contiguous(), stages=[])
+        C, L = self.U, T
+        for w, b, u, k in self.ups:
+            C, L = C // 2, (L - 1) * u - 2 * ((k - u) // 2) + k
+            bufs.stages.append(SimpleNamespace(C=C, L=L, up=torch.empty(B, L, C, **F), t1=torch.empty(B, L, C, **F),
+                                               ya=torch.empty(B, L, C, **F), yb=torch.empty(B, L, C, **F),
+                                               xs=torch.empty(B, L, C, **F)))
+        bufs.out = torch.empty(B, L, **F)
+        return bufs
+
+    def _run(self, bf):
+        """The generator on bf's buffers.  ResBlock1 (models.py:59-110) chains y = y + c2(leaky(c1(leaky(y))))
+        over the dilations; the last conv of resblock j writes xs = (xs + y + c2) directly, and the last
+        resblock's scales by 1/num_kernels and adds the global-token feature (models.py:229-238), so the
+        stage has no clone / axpy / scale passes."""
+        B, T = bf.B, bf.T
+        E = self.codebook.shape[1]
+        ops.codec_embed_cl(self.codebook, E, self.codebook.shape[0], bf.ids, B, T, bf.x0)
+        ops.conv_cl(bf.x0, B, E, T, self.p_pre, 1, 3, bf.y0)
+        x, C, L = bf.y0, self.U, T
+        for i, (w, b, u, k) in enumerate(self.ups):
+            S = bf.stages[i]
+            for r, pc, pad_r in self.p_ups[i]:  # leaky -> ConvTranspose1d as u polyphase convs
+                Tq = (S.L - r + u - 1) // u
+                ops.conv_cl(x, B, C, L, pc, 1, pad_r, S.up, Tq=Tq, ostride=u, ooff=r, Tout_total=S.L, pre_leaky=0.1)
+            C, L = S.C, S.L
+            nk = len(self.p_res[i])
+            gadd = bf.g if C == bf.g.shape[1] else None
+            for j, (kk, convs) in enumerate(self.p_res[i]):
+                src, last_j = S.up, j == nk - 1
+                for m, (p1, d1, p2) in enumerate(convs):
+                    if m == len(convs) - 1:
+                        dst, res2 = S.xs, (S.xs if j > 0 else None)
+                        osc, ga = (1.0 / nk, gadd) if last_j else (1.0, None)
+                    else:
+                        dst, res2, osc, ga = (S.ya if src is not S.ya else S.yb), None, 1.0, None
+                    if p2 is None:  # ResBlock2: y = y + conv(leaky(y))
+                        ops.conv_cl(src, B, C, L, p1, d1, (kk * d1 - d1) // 2, dst, pre_leaky=0.1, res=src, res2=res2,
+                                    oscale=osc, gadd=ga)
+                    else:
+                        ops.conv_cl(src, B, C, L, p1, d1, (kk * d1 - d1) // 2, S.t1, pre_leaky=0.1)
+                        ops.conv_cl(S.t1, B, C, L, p2, 1, (kk - 1) // 2, dst, pre_leaky=0.1, res=src, res2=res2,
+                                    oscale=osc, gadd=ga)
+                    src = dst
+            x = S.xs
+        w, b = self.conv_post
+        ops.conv_post_cl(x, B, L, C, w, b, w.shape[-1], (w.shape[-1] - 1) // 2, 0.1, bf.out)
+
     def __call__(self, ids):
         """ids: device int32 [B, T] codec token ids -> pcm [B, T*upsample] fp32 (tanh output).
-        Channel-last activations [B][T][C]; every conv on the matrix cores (fo_conv_cl)."""
+        Channel-last activations [B][T][C]; every conv on the matrix cores (fo_conv_cl).  On a
+        non-default stream the call is one hipGraph replay per (B, T) (captured on first use; the
+        ~100 launches of a call otherwise cost more host time than the GPU work)."""
         B, T = ids.shape
-        dev = self.device
-        E = self.codebook.shape[1]
-        x = torch.empty(B, T, E, dtype=F32, device=dev)
-        ops.codec_embed_cl(self.codebook, E, self.codebook.shape[0], ids.contiguous(), B, T, x)
-        y = torch.empty(B, T, self.U, dtype=F32, device=dev)
-        ops.conv_cl(x, B, E, T, self.p_pre, 1, 3, y)
-        x, C, L = y, self.U, T
-        g = self.gfeat.view(1, -1).expand(B, -1).contiguous()
-        nk = len(self.res[0])
-        for i, (w, b, u, k) in enumerate(self.ups):
-            Co = C // 2
-            Lo = (L - 1) * u - 2 * ((k - u) // 2) + k
-            up = torch.empty(B, Lo, Co, dtype=F32, device=dev)
-            for r, pc, pad_r in self.p_ups[i]:  # leaky -> ConvTranspose1d as u polyphase convs
-                Tq = (Lo - r + u - 1) // u
-                ops.conv_cl(x, B, C, L, pc, 1, pad_r, up, Tq=Tq, ostride=u, ooff=r, Tout_total=Lo, pre_leaky=0.1)
-            C, L = Co, Lo
-            xs = None
-            t1 = torch.empty(B, L, C, dtype=F32, device=dev)
-            for kk, convs in self.p_res[i]:
-                yb = up.clone() if xs is not None or nk > 1 else up
-                for p1, d1, p2 in convs:
-                    if p2 is None:  # ResBlock2: y = conv(leaky(y)) + y
-                        ops.conv_cl(yb, B, C, L, p1, d1, (kk * d1 - d1) // 2, yb, pre_leaky=0.1, residual=True)
-                        continue
-                    ops.conv_cl(yb, B, C, L, p1, d1, (kk * d1 - d1) // 2, t1, pre_leaky=0.1)
-                    ops.conv_cl(t1, B, C, L, p2, 1, (kk - 1) // 2, yb, pre_leaky=0.1, residual=True)
-                if xs is None:
-                    xs = yb
-                else:
-                    ops.axpy_(xs, yb)
-            ops.scale_add_cl(xs, B, L, C, 1.0 / nk, g if C == g.shape[1] else None)
-            x = xs
-        w, b = self.conv_post
-        out = torch.empty(B, L, dtype=F32, device=dev)
-        ops.conv_post_cl(x, B, L, C, w, b, w.shape[-1], (w.shape[-1] - 1) // 2, 0.1, out)
-        return out
+        key = (B, T)
+        bf = self._graphs.pop(key, None)
+        if bf is None:
+            if len(self._graphs) >= self.MAX_GRAPHS:   # least recently used (dict order) goes
+                old = self._graphs.pop(next(iter(self._graphs)))
+                if old.exec is not None:
+                    torch.cuda.synchronize(self.device)
+                    _lib.call("fo_graph_destroy", old.exec)
+            bf = self._buffers(B, T)
+        self._graphs[key] = bf
+        bf.ids.copy_(ids)
+        st = ops.stream(self.device)
+        if not self.use_graphs or st in (0, None):
+            self._run(bf)
+        else:
+            if bf.exec is None:
+                _lib.call("fo_graph_begin", st)
+                ex = ctypes.c_void_p()
+                try:
+                    self._run(bf)
+                finally:
+                    _lib.call("fo_graph_end", st, ctypes.byref(ex))
+                bf.exec = ex
+            _lib.call("fo_graph_launch", bf.exec, st)
+        return bf.out.clone()
+
+    def destroy(self):
+        for bf in self._graphs.values():
+            if bf.exec is not None:
+                _lib.call("fo_graph_destroy", bf.exec)
+        self._graphs = {}
 
     def forward_ncl(self, ids):
         """Channel-major direct-convolution path (VALU kernels of fo_codec.hip); kept as a

@@ -433,13 +433,15 @@ class PackedConv:
 
 
 def conv_cl(x, B, Cin, Tin, pc, dil, pad, out, Tq=None, ostride=1, ooff=0, Tout_total=None, pre_leaky=None,
-            residual=False):
-    """out[b][q*ostride+ooff][:] (+)= conv(x)[b][q] for q < Tq; x [B][Tin][Cin], out [B][Tout_total][Cout]."""
+            res=None, res2=None, oscale=1.0, gadd=None):
+    """out[b][q*ostride+ooff][:] = (conv(x)[b][q] + res + res2) * oscale + gadd[b] for q < Tq;
+    x [B][Tin][Cin], out/res/res2 [B][Tout_total][Cout] (res/res2 may be out itself), gadd [B][Cout]."""
     Tq = Tin + 2 * pad - dil * (pc.K - 1) if Tq is None else Tq
     Tout_total = Tq if Tout_total is None else Tout_total
     _lib.call("fo_conv_cl", x.data_ptr(), B, Cin, Tin, pc.packed.data_ptr(), ptr(pc.bias), pc.Cout, pc.K, dil, pad,
               Tq, ostride, ooff, Tout_total, 0 if pre_leaky is None else 1,
-              0.0 if pre_leaky is None else float(pre_leaky), out.data_ptr(), 1 if residual else 0, stream(x.device))
+              0.0 if pre_leaky is None else float(pre_leaky), out.data_ptr(), ptr(res), ptr(res2), float(oscale),
+              ptr(gadd), stream(x.device))
     return out
 
 

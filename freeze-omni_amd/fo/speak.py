@@ -31,11 +31,12 @@ class SpeakState:
         self.t_first_pcm = None   # host time the first vocoder chunk's PCM was known (before the silence gate)
 
 
-def silence_cut(buffer, syn, N, threshold, res):
-    """find_min_sum_index(buffer, syn): returns (new_buffer, emitted or None); device tensors 1-D."""
-    L = syn.numel()
-    ops.silence_cut(syn, N, res)
-    r = res.cpu()
+def silence_cut(buffer, syn, N, threshold, res, r=None):
+    """find_min_sum_index(buffer, syn): returns (new_buffer, emitted or None); device tensors 1-D.
+    r: the kernel's (min_sum, cut) already read back (batched by the caller), else launched and read here."""
+    if r is None:
+        ops.silence_cut(syn, N, res)
+        r = res.cpu()
     min_sum, cut = float(r[0]), int(r[1])
     if min_sum / N < threshold:
         out = syn[:cut] if buffer is None or buffer.numel() == 0 else torch.cat([buffer, syn[:cut]])
@@ -219,6 +220,13 @@ def _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final):
     for T, members in groups.items():
         ids = torch.tensor([states[i].tokens for i in members], dtype=I32).to(engine.device)
         pcm = engine.codec(ids)
+        cuts = None
+        if not final:   # every member's window search in one go, one read-back for the call
+            resb = torch.empty(len(members), 2, dtype=F32, device=engine.device)
+            for j, i in enumerate(members):
+                s = states[i]
+                ops.silence_cut(pcm[j][s.left * up: pcm.shape[1] - pad * up], N, resb[j])
+            cuts = resb.cpu()
         for j, i in enumerate(members):
             s = states[i]
             syn = pcm[j]
@@ -235,7 +243,7 @@ def _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final):
             syn = syn[s.left * up: syn.numel() - pad * up]
             s.left = pad
             s.tokens = s.tokens[-(s.left + pad):]
-            s.buffer, seg = silence_cut(s.buffer, syn, N, thr, res)   # reads the cut back: PCM is final here
+            s.buffer, seg = silence_cut(s.buffer, syn, N, thr, res, cuts[j])   # PCM is final here (read back)
             if s.t_first_pcm is None:
                 s.t_first_pcm = time.perf_counter()
             if seg is not None:

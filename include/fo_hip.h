@@ -180,13 +180,15 @@ int fo_axpy(float* y, const float* x, long long n, hipStream_t s);
 int fo_scale_add_channel(float* y, int B, int C, int T, float sc, const float* g, hipStream_t s);
 /* ---------------------------------------------------------------- vocoder on MFMA (fo_vocoder.hip)
  * Generator.forward convs (models/decoder/ticodec/models.py:59-110,211-242) as implicit GEMMs on
- * channel-last activations [B][T][C]; ConvTranspose1d as stride-u polyphase convs. */
+ * channel-last activations [B][T][C]; ConvTranspose1d as stride-u polyphase convs.  fo_conv_cl's
+ * epilogue out = (conv + bias + res + res2) * oscale + gadd[b][c] folds ResBlock1's residual adds, the
+ * mean over resblocks and the global-token feature (models.py:104-108,229-238) into the convs. */
 long long fo_conv_pack_elems(int Cout, int Cin, int K);
 int fo_pack_conv(const void* W, int src_bf16, int Cout, int Cin, int K, int transposed, int Ktot, int j0, int u,
                  void* out, hipStream_t s);
 int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const float* bias, int Cout, int K, int dil,
                int pad, int Tq, int ostride, int ooff, int Tout_total, int pre_leaky, float slope, float* out,
-               int residual, hipStream_t s);
+               const float* res, const float* res2, float oscale, const float* gadd, hipStream_t s);
 /* Quantizer.embed (models/decoder/ticodec/models.py:661-700), channel-last output */
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 /* xs / num_kernels (+ global feature, models.py:233-238), channel-last */
