@@ -81,3 +81,31 @@ print(f"LLM stage alone     {t_llm:8.1f} us  ({wb / t_llm / 1e6:.2f} TB/s over {
 print(f"encoder stage alone {t_enc:8.1f} us")
 print(f"both, overlapped    {t_both:8.1f} us  (max of the two {max(t_llm, t_enc):.1f}, sum {t_llm + t_enc:.1f})",
       flush=True)
+
+# dispatch contention probe: beside the LLM stage, a side-stream graph of N tiny kernels (256-element axpy,
+# ~no memory or CU time) -- if the LLM stage slows by ~N x the per-dispatch cost, the two streams' kernel
+# dispatches, not HBM or CUs, are what the encoder stage contends for
+from fo import ops as _ops  # noqa: E402
+ta = torch.zeros(256, device=dev)
+tb = torch.ones(256, device=dev)
+side_s = g.side
+for nk in (150, 300, 600):
+    with torch.cuda.stream(side_s):
+        _lib.call("fo_graph_begin", side)
+        for _ in range(nk):
+            _ops.axpy_(ta, tb)
+        gx = ctypes.c_void_p()
+        _lib.call("fo_graph_end", side, ctypes.byref(gx))
+
+    def tiny_only(gx=gx):
+        _lib.call("fo_graph_launch", gx, side)
+        _lib.call("fo_event_record", ev_side, side)
+        _lib.call("fo_stream_wait_event", main, ev_side)
+
+    def both_tiny(gx=gx):
+        _lib.call("fo_graph_launch", gx, side)
+        _lib.call("fo_event_record", ev_side, side)
+        _lib.call("fo_graph_launch", g.llm_exec[0], main)
+        _lib.call("fo_stream_wait_event", main, ev_side)
+    print(f"{nk:4d} tiny side-stream kernels: alone {timed(tiny_only):8.1f} us, beside the LLM stage "
+          f"{timed(both_tiny):8.1f} us", flush=True)
