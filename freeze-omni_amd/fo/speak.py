@@ -107,6 +107,13 @@ def _emit(engine, states, chunk_due, finished, up, pad, N, thr, res):
 def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
                  min_tokens, seed, window, pen=None):
     tts = engine.tts
+    if tts.fused:
+        # the fused step (fo_tts_step) launched directly, one step at a time with an id read-back each: the
+        # eager form of the captured graph path (same kernel; steps outside its contract fall back to the
+        # multi-kernel body inside DecodeGraph)
+        yield from _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold,
+                                max_tokens, min_tokens, seed, 1, pen, capture=False)
+        return
     dev = engine.device
     up = engine.codec.upsample
     res = torch.empty(2, dtype=F32, device=dev)
@@ -140,7 +147,7 @@ def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
 
 
 def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
-                 min_tokens, seed, window, pen=None):
+                 min_tokens, seed, window, pen=None, capture=True):
     tts = engine.tts
     dev = engine.device
     up = engine.codec.upsample
@@ -155,7 +162,7 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
         while live and len(pending) < window and step < max_tokens:
             forced = bool(min_tokens and step < min_tokens)
             ng = tts.decode_graph(len(live), tts.vocab if forced else tts.vocab + 4, top_k, seed, max_keys,
-                                  max_tokens + 1, pen)
+                                  max_tokens + 1, pen, capture)
             if ng is not g:
                 if g is None or ng.B != g.B:
                     ng.ids.fill_(tts.sos) if step == 0 else ng.ids.copy_(torch.tensor(
@@ -172,6 +179,7 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
             break
         st, batch, pg, ev = pending.popleft()
         _lib.call("fo_event_sync", ev)
+        pg.check()
         row = pg.hist.np[st].tolist()
         finished, chunk_due = [], []
         for j, i in enumerate(batch):

@@ -7,6 +7,7 @@ bidirectional prefill then uses RoPE positions 0..T while writing rows P..P+T; d
 position cache_len - P (decoder.py:337-340).  Many sessions decode in one batched step.
 """
 import ctypes
+import os
 from types import SimpleNamespace
 
 import numpy as np
@@ -102,6 +103,60 @@ class TTSEngine:
             s.generated += 1
         return self.out_fnn(ws["xg"][:B], norm=(ws["sA"], self.eps))
 
+    # the fused one-launch decode step (fo_tts_step) where its contract holds, opt-in (FO_TTS_FUSED=1):
+    # measured at real geometry, 8 sessions, 285 keys (scripts/tts_step_time.py, profiles/r02m_*): 303 us per
+    # step against 182 us for the multi-kernel step -- the device barriers cost ~2.5 us each after the last
+    # arrival and the q|k|v / gate-up phases (RMSNorm staged per workgroup) 12-16 us, so the 21-barrier
+    # step does not beat ~27 graph nodes of ~5-7 us yet.  Correct (tests/test_tts_step_gpu.py), not default.
+    fused = os.environ.get("FO_TTS_FUSED", "0") == "1"
+    FUSED_KMAX = 64
+
+    def fused_step_args(self, g):
+        """FoTtsStep for DecodeGraph g, or None when the step is outside the fused kernel's contract
+        (then the graph keeps the multi-kernel body)."""
+        L = self.main.layers
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        S = max(1, -(-g.max_keys // 1024))
+        while S < 4 and g.B * self.H * (S + 1) <= ncu and g.max_keys > 256 * S:
+            S += 1
+        top_k = int(g.topk[0].item())
+        ok = (self.hd in (32, 64) and self.D % 128 == 0 and self.D <= 1024 and len(L) <= _lib.TTS_MAXL and g.B <= 16 and
+              1 <= top_k <= self.FUSED_KMAX and L[0].qkv.bias is None and g.B * self.H * S <= ncu and
+              -(-g.max_keys // S) <= 1024 and max(3 * self.D // 32, (self.D // 16) * 4, (self.vocab + 19) // 16) <= ncu
+              and (L[0].gu.N // 32) % 4 == 0 and L[0].gu.N // 128 <= 40)
+        if not ok:
+            return None
+        a = _lib.FoTtsStep()
+        a.B, a.D, a.H, a.hd, a.F, a.nl = g.B, self.D, self.H, self.hd, L[0].gu.N, len(L)
+        a.V, a.V_sample = g.logits.shape[1], g.V_sample
+        a.PS, a.maxb, a.S = self.pool.PS, g.maxb, S
+        a.eps, a.scale = self.eps, self.hd ** -0.5
+        a.penalty, a.W = (float(g.pen[1]), int(g.pen[0])) if g.pen else (1.0, 0)
+        a.seed = int(g.seed) & 0xFFFFFFFFFFFFFFFF
+        for i, ly in enumerate(L):
+            a.wqkv[i], a.wo[i] = ly.qkv.packed.data_ptr(), ly.o.packed.data_ptr()
+            a.wgu[i], a.wdown[i] = ly.gu.packed.data_ptr(), ly.down.packed.data_ptr()
+            a.ln1[i], a.ln2[i] = ly.ln1.data_ptr(), ly.ln2.data_ptr()
+            a.kc[i], a.vc[i] = self.pool.k[self.main.kv_layer0 + i].data_ptr(), self.pool.v[self.main.kv_layer0 + i].data_ptr()
+        a.norm, a.wout = self.norm.data_ptr(), self.out_fnn.packed.data_ptr()
+        a.bout = self.out_fnn.bias.data_ptr() if self.out_fnn.bias is not None else None
+        a.emb, a.emb_ld = self.embedding.data_ptr(), self.embedding.stride(0)
+        a.cos_t, a.sin_t = self.main.cos.data_ptr(), self.main.sin.data_ptr()
+        m = g.meta
+        a.tok_pos, a.tok_slot, a.tok_nvis = m.tok_pos.data_ptr(), m.tok_slot.data_ptr(), m.tok_nvis.data_ptr()
+        a.step, a.key, a.hist_row = m.step.data_ptr(), m.key.data_ptr(), m.hist_row.data_ptr()
+        a.block_table, a.top_k = m.block_table.data_ptr(), g.topk.data_ptr()
+        a.win = g.win.data_ptr() if g.win is not None else None
+        a.x, a.ids, a.logits = g.x.data_ptr(), g.ids.data_ptr(), g.logits.data_ptr()
+        a.hist, a.hist_ld = g.hist.dev, g.B
+        g._fws = torch.empty(_lib.load().fo_tts_step_ws_floats(self.D, self.H, self.hd, a.F, S), dtype=F32,
+                             device=self.device)
+        g._bar = torch.zeros(256, dtype=I32, device=self.device)
+        g._err = ops.HostBuffer(1, 1)   # host-mapped: read after a step's event, no device sync
+        g._err.np[0, 0] = 0
+        a.ws, a.bar, a.err = g._fws.data_ptr(), g._bar.data_ptr(), g._err.dev
+        return a
+
     def embed_input(self, tokens, ws, B, x=None):
         """x = embedding[tokens] (fp32) and ws["h"] = the first layer's RMSNorm of it: the decode step's
         input, as fo_sample_embed writes it for the next step inside the captured graph."""
@@ -109,17 +164,18 @@ class TTSEngine:
         ops.rmsnorm(x, self.main.layers[0].ln1, self.eps, out=ws["h"], M=B)
         return x
 
-    def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None):
+    def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None, capture=True):
         """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows).
-        pen = (window, penalty) adds the repetition penalty before the draw (None: off)."""
-        key = (B, V_sample, top_k, seed, pen)
+        pen = (window, penalty) adds the repetition penalty before the draw (None: off).
+        capture=False: the same step body launched directly each step (the eager loop of the fused path)."""
+        key = (B, V_sample, top_k, seed, pen, bool(self.fused), capture)
         g = self._graphs.get(key) if hasattr(self, "_graphs") else None
         if g is None or g.max_keys < max_keys or g.hist_rows < hist_rows:
             if not hasattr(self, "_graphs"):
                 self._graphs = {}
             if g is not None:
                 g.destroy()
-            g = DecodeGraph(self, B, V_sample, top_k, seed, max(max_keys, 1024), max(hist_rows, 1024), pen)
+            g = DecodeGraph(self, B, V_sample, top_k, seed, max(max_keys, 1024), max(hist_rows, 1024), pen, capture)
             self._graphs[key] = g
         return g
 
@@ -152,7 +208,7 @@ class DecodeGraph:
 
     RING = 64
 
-    def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None):
+    def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None, capture=True):
         dev = tts.device
         self.pen = pen
         self.win = torch.full((B, pen[0]), -1, dtype=I32, device=dev) if pen else None
@@ -176,17 +232,22 @@ class DecodeGraph:
         self.logits = torch.empty(B, tts.vocab + 4, dtype=F32, device=dev)
         self.topk = torch.tensor([top_k] * B, dtype=I32).to(dev)
         self.ws = tts.main.workspace(B, ops.attn_nsplit(max_keys, B, tts.H), dev)
+        self.fused = tts.fused_step_args(self) if tts.fused else None
         self.events = []
         for _ in range(self.RING):
             e = ctypes.c_void_p()
             _lib.call("fo_event_create", ctypes.byref(e))
             self.events.append(e)
         self.exec = None
-        self._capture()
+        if capture:
+            self._capture()
 
     def _body(self):
         # x / ws["h"] hold this step's input (prime() or the previous replay's sampler); the sampler
         # records the drawn ids and writes the next step's input rows (fo_sample_embed)
+        if self.fused is not None:   # the whole step as one persistent kernel (fo_tts_step)
+            _lib.call("fo_tts_step", ctypes.byref(self.fused), ops.stream(self.tts.device))
+            return
         t = self.tts
         t.main.forward(self.x, self.meta, self.ws, pre_normed=True, final_norm=t.norm)
         t.out_fnn(self.ws["xg"], out=self.logits, norm=(self.ws["sA"], t.eps))
@@ -207,6 +268,11 @@ class DecodeGraph:
             self.win.copy_(other.win)
         self.x.copy_(other.x)
         self.ws["h"].copy_(other.ws["h"])
+
+    def check(self):
+        """Raise if a fused step's device barrier ever timed out (it never blocks: it gives up and flags)."""
+        if self.fused is not None and int(self._err.np[0, 0]) != 0:
+            raise RuntimeError("fo_tts_step: a device barrier timed out (workgroups not co-resident)")
 
     def _capture(self):
         s = ops.stream(self.tts.device)
@@ -252,7 +318,10 @@ class DecodeGraph:
             s.generated += 1
         self.meta_d.copy_(self.host[slot % self.RING], non_blocking=True)
         st = ops.stream(self.tts.device)
-        _lib.call("fo_graph_launch", self.exec, st)
+        if self.exec is None:
+            self._body()
+        else:
+            _lib.call("fo_graph_launch", self.exec, st)
         ev = self.events[slot % self.RING]
         _lib.call("fo_event_record", ev, st)
         return ev
@@ -265,3 +334,5 @@ class DecodeGraph:
             _lib.call("fo_event_destroy", e)
         self.events = []
         self.hist.free()
+        if self.fused is not None:
+            self._err.free()
