@@ -14,10 +14,9 @@
 //   QKV(l):  R0 = xa (l = 0) | xb + sum_s dpart[s] (written back to xa); h = RMSNorm(R0) * ln1;
 //            tile pair u = g of q|k|v (rope-paired packing), K = D; RoPE + paged KV append in the epilogue.
 //   ATTN(l): item (b, h, s) = g: keys [s L/S, (s+1) L/S) of session b, head h -> (max, sum, sum p v).
-//   O(l):    job (tile t, K part p) = g: the attention rows of heads in part p are combined from the split
-//            partials as they are staged; partial o rows -> opart[p].
-//   GU(l):   R1 = xa + sum_p opart[p] (written back to xb); RMSNorm * ln2; gate/up tile pairs g, g + G;
-//            m = silu(gate) * up.
+//   O(l):    tile t = g, whole K: the attention rows are combined from the split partials as they are
+//            staged; xb[:, tile] = R1 = xa + o (the residual added in the epilogue).
+//   GU(l):   RMSNorm(xb) * ln2; gate/up tile pairs g, g + G; m = silu(gate) * up.
 //   DOWN(l): job (tile t, K part p) = g: m[:, part p] -> dpart[p].
 //   OUT:     R = xb + sum dpart; final norm; out_fnn tile g (+ bias) -> logits.
 //   DRAW:    row g < B: penalty ring, top-k draw (fo_sample's small-k path, same RNG stream), history,
@@ -35,8 +34,7 @@ constexpr int TS_T = 256, TS_W = 4;  // threads, waves per workgroup
 constexpr int TS_KW = 10;            // max k-steps per wave of one tile job (prefetch registers)
 constexpr int TS_XKS = 40;           // max k-steps of X staged in LDS
 constexpr int TS_KEYS = 1024;        // max keys per attention split
-constexpr int TS_SO = 4;             // o-projection K parts
-constexpr int TS_SD = 4;             // down-projection K parts
+constexpr int TS_SD = 2;             // down-projection K parts (o takes the whole K and adds the residual)
 constexpr int TS_KMAX = 64;          // largest top-k of the draw
 
 struct SmemGemm {
@@ -80,13 +78,29 @@ typedef __attribute__((address_space(1))) float ts_gf32;
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store((ts_gf32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// ...and every load of such a value is an sc1 buffer load (past this CU's L1), so the barrier needs no
+// acquire either.  One buffer descriptor per array (wave-uniform base), per-lane byte offsets.
+typedef __amdgpu_buffer_rsrc_t TsRs;
+__device__ __forceinline__ TsRs rs_of(const void* base) {
+  const unsigned long long b = (unsigned long long)base;
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
+                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)b)),
+      (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 ld4(TsRs r, size_t off_floats) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(off_floats * 4), 0, 16));
+}
+__device__ __forceinline__ float ld1(TsRs r, size_t off_floats) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (unsigned)(off_floats * 4), 0, 16));
+}
 
 // Device-wide barrier, monotonic within a launch: workgroup g arrives on the counter of its dispatch
 // group x = g % 8 (one cache line each), the last arrival of a group on the top counter, the last group
 // raises the epoch word; lane 0 of wave 0 polls it with a bounded, sleeping spin.  Every wave drains its
-// own (write-through) stores (s_waitcnt vmcnt(0)) before the workgroup barrier, lane 0 takes the ticket
-// and acquires after the epoch is seen (the sc1 form of the in-launch split-K hand-off).  Waves 1-3 then
-// issue their next-phase weight loads (pf), which stay in flight across the wait.
+// own (write-through) stores (s_waitcnt vmcnt(0)) before the workgroup barrier, lane 0 takes the ticket;
+// every handed-off value is read back with sc1 loads, so no acquire fence (the sc1 form of the in-launch
+// hand-off).  Waves 1-3 then issue their next-phase weight loads (pf), which stay in flight across the wait.
 struct TsBar {
   unsigned* w;  // [0]: top counter, [16 * (1 + x)]: group counters, [16 * 9]: epoch word, [16 * 10]: exit
   unsigned epoch;
@@ -125,11 +139,14 @@ __device__ __forceinline__ void ts_barrier(TsBar& b, PF&& pf) {
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
     if (b.trace && b.epoch <= 30) b.trace[blockIdx.x * 64 + 2 * b.epoch] = wall_clock64();
   }
   if (wave == 0) pf();  // after the poll: its loads would sit ahead of every poll in the in-order vmcnt
-  __syncthreads();
+  // raw barrier: the waves wait for lane 0's acquire, not for wave 0's prefetch to land
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 // The last workgroup to leave re-arms the barrier words for the next launch (nobody reads them after
 // its own exit ticket).
@@ -214,120 +231,171 @@ __device__ __forceinline__ void split_store(SmemGemm& sg, int ks, int lane, cons
   sg.xl[ks][lane] = lo;
 }
 
-// Stage RMSNorm(R) * gamma, R = base + sum_{s < NP} parts[s] ([16][D] rows, part stride pst), as MFMA
-// A fragments of all D / 32 k-steps.  TPR = 256 / 16 threads per row when B > 8, 256 / 8 otherwise, so all
-// threads work at B <= 8; thread: row t / TPR, fragment slots q = t % TPR + TPR i (k-step q / 4, columns
-// 8 (q % 4) ..).  Each slot's NP + 1 row pieces are loaded together.  Slots with (row * D/8 + q) % G == g
-// are written back (write-through) to wb when non-null.
+// Stage R * gamma, R = base + sum_{s < NP} parts[s] ([16][D] rows, part stride pst floats), as MFMA A
+// fragments of all D / 32 k-steps, and rstd(row) = rsqrt(mean(R^2) + eps) into misc[16]: the RMSNorm is
+// applied after the GEMM (acc * rstd, linear).  TPR = 16 threads per row when B > 8, else 32 (all threads
+// busy); thread: row t / TPR, fragment slots q = t % TPR + TPR i (k-step q / 4, columns 8 (q % 4) ..).
+// Four slots' loads are issued together (one memory round trip per pass, not per slot).  Slots with
+// (row * D/8 + q) % G == g are written back (write-through) to wb when non-null.
 template <int NP>
 __device__ void stage_norm(SmemGemm& sg, const float* base, const float* parts, size_t pst, const float* gamma,
                            int B, int D, float eps, float* wb, int g, int G) {
   const int tpr = B > 8 ? 16 : 32;
   const int r = threadIdx.x / tpr, sub = threadIdx.x % tpr;
-  const int nq = D / 8;               // slots per row
-  constexpr int MAXI = 1024 / 8 / 16;  // D <= 1024
-  float v[MAXI][8];
+  const int nq = D / 8;  // slots per row
+  const TsRs rb = rs_of(base), rp = rs_of(parts ? parts : base);
   float ss = 0.f;
+  for (int q0 = 0; q0 < nq; q0 += 4 * tpr) {
+    float4 x[4][NP + 1][2];
+    float4 gm[4][2];
 #pragma unroll
-  for (int i = 0; i < MAXI; ++i) {
-    const int q = sub + tpr * i;
+    for (int i = 0; i < 4; ++i) {
+      const int q = q0 + sub + tpr * i;
+      if (q < nq && r < B) {
+        const size_t o = (size_t)r * D + 8 * q;
+        x[i][0][0] = ld4(rb, o);
+        x[i][0][1] = ld4(rb, o + 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
-    if (q < nq && r < B) {
-      const size_t o = (size_t)r * D + 8 * q;
-      float4 x[NP + 1][2];
-      x[0][0] = *reinterpret_cast<const float4*>(base + o);
-      x[0][1] = *reinterpret_cast<const float4*>(base + o + 4);
-#pragma unroll
-      for (int s = 0; s < NP; ++s) {
-        x[s + 1][0] = *reinterpret_cast<const float4*>(parts + s * pst + o);
-        x[s + 1][1] = *reinterpret_cast<const float4*>(parts + s * pst + o + 4);
+        for (int s = 0; s < NP; ++s) {
+          x[i][s + 1][0] = ld4(rp, s * pst + o);
+          x[i][s + 1][1] = ld4(rp, s * pst + o + 4);
+        }
+        gm[i][0] = *reinterpret_cast<const float4*>(gamma + 8 * q);
+        gm[i][1] = *reinterpret_cast<const float4*>(gamma + 8 * q + 4);
       }
+    }
 #pragma unroll
-      for (int s = 0; s <= NP; ++s) {
-        v[i][0] += x[s][0].x; v[i][1] += x[s][0].y; v[i][2] += x[s][0].z; v[i][3] += x[s][0].w;
-        v[i][4] += x[s][1].x; v[i][5] += x[s][1].y; v[i][6] += x[s][1].z; v[i][7] += x[s][1].w;
+    for (int i = 0; i < 4; ++i) {
+      const int q = q0 + sub + tpr * i;
+      if (q >= nq) continue;
+      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (r < B) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s <= NP; ++s) {
+          v[0] += x[i][s][0].x; v[1] += x[i][s][0].y; v[2] += x[i][s][0].z; v[3] += x[i][s][0].w;
+          v[4] += x[i][s][1].x; v[5] += x[i][s][1].y; v[6] += x[i][s][1].z; v[7] += x[i][s][1].w;
+        }
+        if (wb && (r * nq + q) % G == g) {
+          const size_t o = (size_t)r * D + 8 * q;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) st_sc1(wb + o + e, v[e]);
+        }
+        const float gv[8] = {gm[i][0].x, gm[i][0].y, gm[i][0].z, gm[i][0].w,
+                             gm[i][1].x, gm[i][1].y, gm[i][1].z, gm[i][1].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ss += v[e] * v[e];
+          f[e] = v[e] * gv[e];
+        }
       }
-      if (wb && (r * nq + q) % G == g) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) st_sc1(wb + o + e, v[i][e]);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+      if (r < 16) split_store(sg, q >> 2, r + 16 * (q & 3), f);
     }
   }
   for (int o = tpr >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);  // the row's tpr threads
-  const float rs = rsqrtf(ss / (float)D + eps);
+  if (sub == 0 && r < 16) sg.misc[r] = r < B ? rsqrtf(ss / (float)D + eps) : 0.f;
+  if (B <= 8) {  // rows 8..15 are nobody's at 32 threads per row: zero their fragments
+    const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x < 8) sg.misc[8 + threadIdx.x] = 0.f;
+    for (int e = threadIdx.x; e < 8 * nq; e += TS_T) split_store(sg, (e % nq) >> 2, 8 + e / nq + 16 * ((e % nq) & 3), z);
+  }
+}
+
+// Stage plain fp32 rows src[r][col0 + ...] (row stride ld) over nks k-steps (no norm); four items' loads
+// issued together
+__device__ void stage_plain(SmemGemm& sg, const float* src, int ld, int col0, int nks, int B) {
+  const TsRs rs = rs_of(src);
+  const int n = 16 * nks * 4;
+  for (int e0 = 0; e0 < n; e0 += 4 * TS_T) {
+    float4 x[4][2];
 #pragma unroll
-  for (int i = 0; i < MAXI; ++i) {
-    const int q = sub + tpr * i;
-    if (q < nq && r < 16) {
-      float f[8];
+    for (int i = 0; i < 4; ++i) {
+      const int e = e0 + threadIdx.x + TS_T * i;
+      const int r = e / (nks * 4), q = e % (nks * 4);
+      if (e < n && r < B) {
+        const size_t o = (size_t)r * ld + col0 + 8 * q;
+        x[i][0] = ld4(rs, o);
+        x[i][1] = ld4(rs, o + 4);
+      }
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = r < B ? v[i][e] * rs * gamma[8 * q + e] : 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const int e = e0 + threadIdx.x + TS_T * i;
+      if (e >= n) continue;
+      const int r = e / (nks * 4), q = e % (nks * 4);
+      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (r < B) {
+        f[0] = x[i][0].x; f[1] = x[i][0].y; f[2] = x[i][0].z; f[3] = x[i][0].w;
+        f[4] = x[i][1].x; f[5] = x[i][1].y; f[6] = x[i][1].z; f[7] = x[i][1].w;
+      }
       split_store(sg, q >> 2, r + 16 * (q & 3), f);
     }
   }
-  if (B <= 8) {  // rows 8..15 are nobody's at 32 threads per row: zero their fragments
-    for (int e = threadIdx.x; e < 8 * nq; e += TS_T) {
-      const int rr = 8 + e / nq, q = e % nq;
-      const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      split_store(sg, q >> 2, rr + 16 * (q & 3), z);
-    }
-  }
 }
 
-// Stage plain fp32 rows src[r][col0 + ...] (row stride ld) over nks k-steps (no norm)
-__device__ void stage_plain(SmemGemm& sg, const float* src, int ld, int col0, int nks, int B) {
-  for (int e = threadIdx.x; e < 16 * nks * 4; e += TS_T) {
-    const int r = e / (nks * 4), q = e % (nks * 4);
-    float f[8];
-    if (r < B) {
-      const float* p = src + (size_t)r * ld + col0 + 8 * q;
-      const float4 a0 = *reinterpret_cast<const float4*>(p), a1 = *reinterpret_cast<const float4*>(p + 4);
-      f[0] = a0.x; f[1] = a0.y; f[2] = a0.z; f[3] = a0.w; f[4] = a1.x; f[5] = a1.y; f[6] = a1.z; f[7] = a1.w;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) f[i] = 0.f;
-    }
-    split_store(sg, q >> 2, r + 16 * (q & 3), f);
-  }
-}
-
-// Stage the attention output columns [col0, col0 + 32 nks) of every row, combining the S key-split
+// Stage the attention output columns [col0, col0 + 32 nks) of every row, combining the S <= TS_SMAX key-split
 // partials (max, sum, sum p v) of the heads they belong to: o = sum_s e^(m_s - M) o_s / sum_s e^(m_s - M) l_s.
+// Two items' partial loads are issued together.
+constexpr int TS_SMAX = 4;
 __device__ void stage_att(SmemGemm& sg, const float* apart, int col0, int nks, int B, int H, int hd, int S) {
-  for (int e = threadIdx.x; e < 16 * nks * 4; e += TS_T) {
-    const int r = e / (nks * 4), q = e % (nks * 4);
-    float f[8];
+  const TsRs ra = rs_of(apart);
+  const int n = 16 * nks * 4;
+  for (int e0 = 0; e0 < n; e0 += 2 * TS_T) {
+    float ml[2][TS_SMAX][2];
+    float4 ov[2][TS_SMAX][2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = 0.f;
-    if (r < B) {
-      const int col = col0 + 8 * q, h = col / hd, d = col - h * hd;
-      const float* p = apart + (size_t)(r * H + h) * S * (hd + 4);
-      float M = -INFINITY;
-      for (int s = 0; s < S; ++s) M = fmaxf(M, p[s * (hd + 4)]);
-      float l = 0.f;
-      for (int s = 0; s < S; ++s) {
-        const float* ps = p + s * (hd + 4);
-        const float wgt = ps[0] == -INFINITY ? 0.f : expf(ps[0] - M);
-        l += wgt * ps[1];
-        const float4 o0 = *reinterpret_cast<const float4*>(ps + 4 + d);
-        const float4 o1 = *reinterpret_cast<const float4*>(ps + 4 + d + 4);
-        f[0] += wgt * o0.x; f[1] += wgt * o0.y; f[2] += wgt * o0.z; f[3] += wgt * o0.w;
-        f[4] += wgt * o1.x; f[5] += wgt * o1.y; f[6] += wgt * o1.z; f[7] += wgt * o1.w;
+    for (int i = 0; i < 2; ++i) {
+      const int e = e0 + threadIdx.x + TS_T * i;
+      const int r = e / (nks * 4), q = e % (nks * 4);
+      if (e < n && r < B) {
+        const int col = col0 + 8 * q, h = col / hd, d = col - h * hd;
+        const size_t p = (size_t)(r * H + h) * S * (hd + 4);
+#pragma unroll
+        for (int s = 0; s < TS_SMAX; ++s) {
+          if (s < S) {
+            const size_t ps = p + s * (hd + 4);
+            ml[i][s][0] = ld1(ra, ps);
+            ml[i][s][1] = ld1(ra, ps + 1);
+            ov[i][s][0] = ld4(ra, ps + 4 + d);
+            ov[i][s][1] = ld4(ra, ps + 8 + d);
+          }
+        }
       }
-      const float il = 1.f / l;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) f[i] *= il;
     }
-    split_store(sg, q >> 2, r + 16 * (q & 3), f);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = e0 + threadIdx.x + TS_T * i;
+      if (e >= n) continue;
+      const int r = e / (nks * 4), q = e % (nks * 4);
+      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (r < B) {
+        float M = -INFINITY;
+#pragma unroll
+        for (int s = 0; s < TS_SMAX; ++s)
+          if (s < S) M = fmaxf(M, ml[i][s][0]);
+        float l = 0.f;
+#pragma unroll
+        for (int s = 0; s < TS_SMAX; ++s) {
+          if (s < S) {
+            const float wgt = ml[i][s][0] == -INFINITY ? 0.f : expf(ml[i][s][0] - M);
+            l += wgt * ml[i][s][1];
+            f[0] += wgt * ov[i][s][0].x; f[1] += wgt * ov[i][s][0].y; f[2] += wgt * ov[i][s][0].z;
+            f[3] += wgt * ov[i][s][0].w; f[4] += wgt * ov[i][s][1].x; f[5] += wgt * ov[i][s][1].y;
+            f[6] += wgt * ov[i][s][1].z; f[7] += wgt * ov[i][s][1].w;
+          }
+        }
+        const float il = 1.f / l;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] *= il;
+      }
+      split_store(sg, q >> 2, r + 16 * (q & 3), f);
+    }
   }
 }
 
 // ---------------------------------------------------------------- the step
 struct TsPtrs {  // scratch carve of a.ws
-  float *xb, *q, *apart, *opart, *m, *dpart;
+  float *xb, *q, *apart, *m, *dpart;
 };
 
 __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
@@ -341,8 +409,7 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
   P.xb = a.ws;
   P.q = P.xb + RD;
   P.apart = P.q + RD;
-  P.opart = P.apart + (size_t)16 * H * a.S * (hd + 4);
-  P.m = P.opart + TS_SO * RD;
+  P.m = P.apart + (size_t)16 * H * a.S * (hd + 4);
   P.dpart = P.m + (size_t)16 * F;
   TsBar bar{a.bar, 0u, G, a.err, a.trace};
   if (a.trace && tid == 0) a.trace[g * 64] = wall_clock64();
@@ -351,7 +418,7 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
   const int nqkv = 3 * D / 32;             // rope tile pairs of q|k|v
   const int nattn = B * H * a.S;
   const int nt_d = D / 16;                 // o / down output tiles
-  const int nk_o = KSd / TS_SO, nk_d = KSf / TS_SD;
+  const int nk_d = KSf / TS_SD;
   const int ngu = F / 16;                  // gate/up tile pairs
   const int nout = (a.V + 15) / 16;
 
@@ -359,14 +426,14 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
     return g < nqkv ? TsJob{(const bf16_t*)a.wqkv[l], KSd, 2 * g, 2, 0, KSd} : TsJob{nullptr, 0, 0, 0, 0, 0};
   };
   auto o_job = [&](int l) {
-    return g < nt_d * TS_SO ? TsJob{(const bf16_t*)a.wo[l], KSd, g / TS_SO, 1, (g % TS_SO) * nk_o, nk_o}
-                            : TsJob{nullptr, 0, 0, 0, 0, 0};
+    return g < nt_d ? TsJob{(const bf16_t*)a.wo[l], KSd, g, 1, 0, KSd} : TsJob{nullptr, 0, 0, 0, 0, 0};
   };
   auto gu_job = [&](int l, int u) {
     return u < ngu ? TsJob{(const bf16_t*)a.wgu[l], KSd, 2 * u, 2, 0, KSd} : TsJob{nullptr, 0, 0, 0, 0, 0};
   };
-  auto down_job = [&](int l) {
-    return g < nt_d * TS_SD ? TsJob{(const bf16_t*)a.wdown[l], KSf, g / TS_SD, 1, (g % TS_SD) * nk_d, nk_d}
+  constexpr int DCH = 38;                  // down K part processed in chunks of <= DCH k-steps
+  auto down_job = [&](int l) {             // (the first chunk: what the barrier prefetches)
+    return g < nt_d * TS_SD ? TsJob{(const bf16_t*)a.wdown[l], KSf, g / TS_SD, 1, (g % TS_SD) * nk_d, min(DCH, nk_d)}
                             : TsJob{nullptr, 0, 0, 0, 0, 0};
   };
   auto out_job = [&]() {
@@ -383,18 +450,22 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
     {
       const TsJob j = qkv_job(l);
       if (j.W) {
+        const bool tr = a.trace && l == 1 && tid == 0;  // sub-phase clocks of layer 1's q|k|v (profiling)
         if (l == 0) stage_norm<0>(sm.g, xa, nullptr, 0, a.ln1[l], B, D, a.eps, nullptr, g, nqkv);
-        else stage_norm<TS_SD>(sm.g, P.xb, P.dpart, RD, a.ln1[l], B, D, a.eps, xa, g, nqkv);
+        else stage_norm<TS_SD>(sm.g, P.xb, P.dpart, RD, a.ln1[l], B, D, a.eps, xa, g, nqkv);  // -> xa
         __syncthreads();
+        if (tr) a.trace[g * 64 + 50] = wall_clock64();
         f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         job_mma(w, j, sm.g, 0, acc);
+        if (tr) a.trace[g * 64 + 51] = wall_clock64();
         job_reduce(sm.g, acc);
+        if (tr) a.trace[g * 64 + 52] = wall_clock64();
         const int r = tid >> 4, c = tid & 15;
         if (r < B) {
           const int half = hd >> 1, per = hd >> 5;
           const int n = (g / per) * hd + (g % per) * 16 + c;  // rope_col: columns (n, n + hd/2) of head n / hd
           const int h = n / hd, i = n - h * hd;
-          const float x1 = sm.g.red[0][0][r][c], x2 = sm.g.red[0][1][r][c];
+          const float x1 = sm.g.red[0][0][r][c] * sm.g.misc[r], x2 = sm.g.red[0][1][r][c] * sm.g.misc[r];
           const int sl = a.tok_slot[r], page = sl / a.PS, off = sl - page * a.PS;
           if (h < 2 * H) {
             const int p = a.tok_pos[r];
@@ -410,6 +481,7 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
             st_sc1(d + i + half, x2);
           }
         }
+        if (tr) a.trace[g * 64 + 53] = wall_clock64();
       }
       ts_barrier(bar, [] {});
     }
@@ -428,16 +500,15 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
         } else {
           const int* bt = a.block_table + (size_t)b * a.maxb;
           const size_t page_sz = (size_t)H * a.PS * hd, head_off = (size_t)h * a.PS * hd;
-          const float* kc = a.kc[l];
-          const float* vc = a.vc[l];
-          if (tid < hd) sm.at.q[tid] = P.q[(size_t)b * D + (size_t)h * hd + tid] * a.scale;
+          const TsRs rk = rs_of(a.kc[l]), rv = rs_of(a.vc[l]), rq = rs_of(P.q);  // sc1: the new key is this launch's
+          if (tid < hd) sm.at.q[tid] = ld1(rq, (size_t)b * D + (size_t)h * hd + tid) * a.scale;
           __syncthreads();
           float mx = -INFINITY;
           for (int j = k0 + tid; j < k1; j += TS_T) {
-            const float* kr = kc + (size_t)bt[j / a.PS] * page_sz + head_off + (size_t)(j % a.PS) * hd;
+            const size_t kr = (size_t)bt[j / a.PS] * page_sz + head_off + (size_t)(j % a.PS) * hd;
             float sc = 0.f;
             for (int d = 0; d < hd; d += 4) {
-              const float4 k4 = *reinterpret_cast<const float4*>(kr + d);
+              const float4 k4 = ld4(rk, kr + d);
               sc += sm.at.q[d] * k4.x + sm.at.q[d + 1] * k4.y + sm.at.q[d + 2] * k4.z + sm.at.q[d + 3] * k4.w;
             }
             sm.at.s[j - k0] = sc;
@@ -460,8 +531,7 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
           float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
           for (int j = k0 + wave * kpw + sub; j < k1; j += kpw * TS_W) {
             const float p = sm.at.s[j - k0];
-            const float4 v = *reinterpret_cast<const float4*>(vc + (size_t)bt[j / a.PS] * page_sz + head_off +
-                                                              (size_t)(j % a.PS) * hd + 4 * l4);
+            const float4 v = ld4(rv, (size_t)bt[j / a.PS] * page_sz + head_off + (size_t)(j % a.PS) * hd + 4 * l4);
             acc.x += p * v.x;
             acc.y += p * v.y;
             acc.z += p * v.z;
@@ -490,26 +560,29 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
       const TsJob jn = o_job(l);
       ts_barrier(bar, [&] { job_load(w, jn); });
     }
-    // ---------------- O: job (tile, K part) = g -> opart[part][row][tile cols]
+    // ---------------- O: tile g, whole K: xb[:, tile] = xa[:, tile] + attention rows . Wo^T
     {
       const TsJob j = o_job(l);
       if (j.W) {
-        stage_att(sm.g, P.apart, j.kb * 32, j.nk, B, H, hd, a.S);
+        const int r = tid >> 4, c = tid & 15;
+        const float res = r < B ? ld1(rs_of(xa), (size_t)r * D + j.t0 * 16 + c) : 0.f;
+        stage_att(sm.g, P.apart, 0, j.nk, B, H, hd, a.S);
         __syncthreads();
         f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         job_mma(w, j, sm.g, 0, acc);
         job_reduce(sm.g, acc);
-        const int r = tid >> 4, c = tid & 15;
-        st_sc1(P.opart + (g % TS_SO) * RD + (size_t)r * D + j.t0 * 16 + c, r < B ? sm.g.red[0][0][r][c] : 0.f);
+        if (r < B) st_sc1(P.xb + (size_t)r * D + j.t0 * 16 + c, res + sm.g.red[0][0][r][c]);
       }
       const TsJob jn = gu_job(l, g);
       ts_barrier(bar, [&] { job_load(w, jn); });
     }
-    // ---------------- GU: R1 = xa + sum opart (-> xb); RMSNorm * ln2; pairs g, g + G -> m
+    // ---------------- GU: RMSNorm(xb) * ln2 (post-scaled); pairs g, g + G -> m
     {
       if (g < ngu) {
-        stage_norm<TS_SO>(sm.g, xa, P.opart, RD, a.ln2[l], B, D, a.eps, P.xb, g, min(G, ngu));
+        const bool tr = a.trace && l == 1 && tid == 0;
+        stage_norm<0>(sm.g, P.xb, nullptr, 0, a.ln2[l], B, D, a.eps, nullptr, g, min(G, ngu));
         __syncthreads();
+        if (tr) a.trace[g * 64 + 54] = wall_clock64();
         for (int u = g; u < ngu; u += G) {
           const TsJob j = gu_job(l, u);
           if (u != g) job_load(w, j);
@@ -517,22 +590,31 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
           job_mma(w, j, sm.g, 0, acc);
           job_reduce(sm.g, acc);
           const int r = tid >> 4, c = tid & 15;
-          const float gt = sm.g.red[0][0][r][c], up = sm.g.red[0][1][r][c];
+          const float gt = sm.g.red[0][0][r][c] * sm.g.misc[r], up = sm.g.red[0][1][r][c] * sm.g.misc[r];
           st_sc1(P.m + (size_t)r * F + u * 16 + c, r < B ? gt / (1.f + expf(-gt)) * up : 0.f);
           __syncthreads();  // red[] is rewritten by the next pair
+          if (tr && u == g) a.trace[g * 64 + 55] = wall_clock64();
         }
+        if (tr) a.trace[g * 64 + 56] = wall_clock64();
       }
       const TsJob jn = down_job(l);
       ts_barrier(bar, [&] { job_load(w, jn); });
     }
-    // ---------------- DOWN: job (tile, K part) = g -> dpart[part][row][tile cols]
+    // ---------------- DOWN: job (tile, K part) = g -> dpart[part][row][tile cols], in chunks of DCH k-steps
     {
       const TsJob j = down_job(l);
       if (j.W) {
-        stage_plain(sm.g, P.m, F, j.kb * 32, j.nk, B);
-        __syncthreads();
         f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-        job_mma(w, j, sm.g, 0, acc);
+        for (int c0 = 0; c0 < nk_d; c0 += DCH) {
+          const TsJob jc{j.W, KSf, j.t0, 1, j.kb + c0, min(DCH, nk_d - c0)};
+          if (c0 > 0) {
+            job_load(w, jc);
+            __syncthreads();  // the previous chunk's fragments are read
+          }
+          stage_plain(sm.g, P.m, F, jc.kb * 32, jc.nk, B);
+          __syncthreads();
+          job_mma(w, jc, sm.g, 0, acc);
+        }
         job_reduce(sm.g, acc);
         const int r = tid >> 4, c = tid & 15;
         st_sc1(P.dpart + (g % TS_SD) * RD + (size_t)r * D + j.t0 * 16 + c, r < B ? sm.g.red[0][0][r][c] : 0.f);
@@ -551,7 +633,8 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
       job_mma(w, j, sm.g, 0, acc);
       job_reduce(sm.g, acc);
       const int r = tid >> 4, c = tid & 15, n = g * 16 + c;
-      if (r < B && n < a.V) st_sc1(a.logits + (size_t)r * a.V + n, sm.g.red[0][0][r][c] + (a.bout ? a.bout[n] : 0.f));
+      if (r < B && n < a.V)
+        st_sc1(a.logits + (size_t)r * a.V + n, sm.g.red[0][0][r][c] * sm.g.misc[r] + (a.bout ? a.bout[n] : 0.f));
     }
     ts_barrier(bar, [] {});
   }
@@ -567,7 +650,7 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
         const int n = st + 1 < a.W ? st + 1 : a.W;
         for (int j = 0; j < n; ++j) {
           const int t = wr[j];
-          if (t >= 0 && t < a.V) lg[t] = lg[t] / a.penalty;
+          if (t >= 0 && t < a.V) st_sc1(lg + t, ld1(rs_of(lg), t) / a.penalty);
         }
       }
       __syncthreads();
@@ -577,11 +660,12 @@ __global__ __launch_bounds__(TS_T) void k_tts_step(FoTtsStep a) {
     const float u01 =
         (float)(uint32_t)(ts_smix(a.seed ^ (0x9E37ull * (key + 1)) + (uint64_t)st) >> 40) * (1.0f / 16777216.0f);
     SmemDraw& d = sm.dr;
+    const TsRs rlg = rs_of(lg);  // the logits rows came from other workgroups (sc1)
     for (int q = 0; q < k; ++q) {  // k block arg-max passes (ties -> smallest index), as fo_sample
       float best = -INFINITY;
       int besti = 0x7fffffff;
       for (int i = tid; i < a.V_sample; i += TS_T) {
-        const float x = lg[i];
+        const float x = ld1(rlg, i);
         bool skip = false;
         for (int t = 0; t < q; ++t) skip |= d.taken[t] == i;
         if (!skip && (x > best || (x == best && i < besti))) {
@@ -647,7 +731,7 @@ extern "C" {
 
 long long fo_tts_step_ws_floats(int D, int H, int hd, int F, int S) {
   const long long RD = 16ll * D;
-  return RD * 2 + 16ll * H * S * (hd + 4) + TS_SO * RD + 16ll * F + TS_SD * RD;
+  return RD * 2 + 16ll * H * S * (hd + 4) + 16ll * F + TS_SD * RD;
 }
 
 int fo_tts_step(const FoTtsStep* p, hipStream_t s) {
@@ -657,10 +741,9 @@ int fo_tts_step(const FoTtsStep* p, hipStream_t s) {
   FO_REQUIRE((a.hd == 64 || a.hd == 32) && a.H * a.hd == a.D && a.D % 128 == 0 && a.D <= 1024,
              "fo_tts_step: D=%d H=%d hd=%d (hd 32 or 64, D = H hd, D %% 128 == 0, D <= 1024)", a.D, a.H, a.hd);
   FO_REQUIRE(a.nl >= 1 && a.nl <= FO_TTS_MAXL, "fo_tts_step: %d layers", a.nl);
-  FO_REQUIRE(a.D / 32 <= TS_XKS && (a.D / 32) % TS_SO == 0 && (a.D / 32) / TS_SO <= TS_KW && a.D / 32 <= TS_W * TS_KW,
+  FO_REQUIRE(a.D / 32 <= TS_XKS && a.D / 32 <= TS_W * TS_KW,
              "fo_tts_step: D=%d outside the staged / prefetched k-steps", a.D);
-  FO_REQUIRE(a.F % 32 == 0 && (a.F / 32) % TS_SD == 0 && (a.F / 32) / TS_SD <= TS_XKS &&
-                 (a.F / 32) / TS_SD <= TS_W * TS_KW && a.F % 16 == 0,
+  FO_REQUIRE(a.F % 32 == 0 && (a.F / 32) % TS_SD == 0 && a.F % 16 == 0,
              "fo_tts_step: F=%d outside the staged / prefetched k-steps", a.F);
   FO_REQUIRE(a.V >= 1 && a.V_sample >= 1 && a.V_sample <= a.V && a.S >= 1 && a.PS >= 1 && a.maxb >= 1,
              "fo_tts_step: V=%d V_sample=%d S=%d", a.V, a.V_sample, a.S);
@@ -673,7 +756,7 @@ int fo_tts_step(const FoTtsStep* p, hipStream_t s) {
   FO_HIP(hipGetDevice(&dev));
   FO_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   // every phase's jobs must fit the grid: one workgroup per CU, all resident (barriers)
-  const int need = std::max({3 * a.D / 32, a.B * a.H * a.S, (a.D / 16) * TS_SO, (a.D / 16) * TS_SD,
+  const int need = std::max({3 * a.D / 32, a.B * a.H * a.S, a.D / 16, (a.D / 16) * TS_SD,
                              (a.V + 15) / 16, a.B});
   FO_REQUIRE(need <= ncu, "fo_tts_step: %d jobs in a phase > %d CUs", need, ncu);
   hipLaunchKernelGGL(k_tts_step, dim3(ncu), dim3(TS_T), 0, s, a);

@@ -104,10 +104,11 @@ class TTSEngine:
         return self.out_fnn(ws["xg"][:B], norm=(ws["sA"], self.eps))
 
     # the fused one-launch decode step (fo_tts_step) where its contract holds, opt-in (FO_TTS_FUSED=1):
-    # measured at real geometry, 8 sessions, 285 keys (scripts/tts_step_time.py, profiles/r02m_*): 303 us per
-    # step against 182 us for the multi-kernel step -- the device barriers cost ~2.5 us each after the last
-    # arrival and the q|k|v / gate-up phases (RMSNorm staged per workgroup) 12-16 us, so the 21-barrier
-    # step does not beat ~27 graph nodes of ~5-7 us yet.  Correct (tests/test_tts_step_gpu.py), not default.
+    # measured at real geometry, 8 sessions, 285 keys (scripts/tts_step_time.py, profiles/r02m_*): 257 us per
+    # step against 181 us for the multi-kernel step -- each device barrier still ends ~2.8 us after its last
+    # arrival and every phase that reads another workgroup's output pays a 2-3 us memory round trip first
+    # (q|k|v staging 6 us, down 10 us), so the 21-barrier step does not beat ~27 graph nodes of ~5-7 us
+    # yet.  Correct (tests/test_tts_step_gpu.py), not the default.
     fused = os.environ.get("FO_TTS_FUSED", "0") == "1"
     FUSED_KMAX = 64
 
@@ -122,8 +123,8 @@ class TTSEngine:
         top_k = int(g.topk[0].item())
         ok = (self.hd in (32, 64) and self.D % 128 == 0 and self.D <= 1024 and len(L) <= _lib.TTS_MAXL and g.B <= 16 and
               1 <= top_k <= self.FUSED_KMAX and L[0].qkv.bias is None and g.B * self.H * S <= ncu and
-              -(-g.max_keys // S) <= 1024 and max(3 * self.D // 32, (self.D // 16) * 4, (self.vocab + 19) // 16) <= ncu
-              and (L[0].gu.N // 32) % 4 == 0 and L[0].gu.N // 128 <= 40)
+              -(-g.max_keys // S) <= 1024 and max(3 * self.D // 32, (self.D // 16) * 2, (self.vocab + 19) // 16) <= ncu
+              and (L[0].gu.N // 32) % 2 == 0)
         if not ok:
             return None
         a = _lib.FoTtsStep()

@@ -52,3 +52,10 @@ for e, n in enumerate(names):
           f"  exit spread {(ext.max() - ext.min()) / 100:5.2f}  wait med {np.median(ext - arr) / 100:6.2f} us", flush=True)
     prev = ext
 print(f"draw + exit: {(t[:, 63].max() - prev.min()) / 100:.1f} us")
+# layer-1 sub-phases (workgroups that had the job), from the exit of the barrier before the phase
+q0 = t[:84, 2 + 2 * 4]
+print("L1 qkv: stage %.2f  mma %.2f  reduce %.2f  epilogue %.2f us (median over its 84 WGs)" % tuple(
+    np.median(np.diff(np.stack([q0, t[:84, 50], t[:84, 51], t[:84, 52], t[:84, 53]]), axis=0), axis=1) / 100))
+g0 = t[:, 2 + 2 * 7]
+print("L1 gu: stage %.2f  first pair %.2f  rest %.2f us (median over WGs)" % tuple(
+    np.median(np.diff(np.stack([g0, t[:, 54], t[:, 55], t[:, 56]]), axis=0), axis=1) / 100))
