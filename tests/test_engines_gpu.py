@@ -338,3 +338,24 @@ def test_codec_ar_facade_infer_matches_golden(dev, speech_engine, window, penalt
     p = torch.from_numpy(t["prefix"]).unsqueeze(0).to(dev)
     ids = [int(x) for x in m.infer(h, 1, p, window, penalty, max_tokens=120)]
     assert ids == want.tolist()
+
+
+def test_codec_graph_replay_matches_eager(dev, src):
+    """The vocoder captured once per (users, tokens) and replayed on a non-default stream gives the eager
+    launch sequence's PCM bit for bit, across shapes, repeated replays with new ids, and LRU eviction."""
+    from fo import ops
+    from fo.codec import CodecEngine
+    eng = CodecEngine(src, CFG["codec_json"], dev)
+    eng.MAX_GRAPHS = 2
+    rng = np.random.default_rng(11)
+    with torch.cuda.stream(ops.engine_stream(dev)):
+        for B, T in [(1, 20), (3, 33), (1, 20), (2, 8), (3, 33)]:
+            ids = torch.from_numpy(rng.integers(0, CFG["codec_json"]["n_codes"], size=(B, T))).to(dev, torch.int32)
+            eng.use_graphs = True
+            g = eng(ids)
+            eng.use_graphs = False
+            e = eng(ids)
+            torch.cuda.synchronize()
+            assert torch.equal(g, e), (B, T)
+        assert len(eng._graphs) <= 2
+    eng.destroy()

@@ -38,14 +38,14 @@ def _items(dev, n, seed):
     return out
 
 
-def _run(tts, dev, items, fused, steps, top_k, pen=None):
+def _run(tts, dev, items, fused, steps, top_k, pen=None, max_keys=4096):
     from fo import ops
     tts.fused = fused
     es = ops.engine_stream(dev)
     with torch.cuda.stream(es):
         seqs = tts.start(items)
         B = len(seqs)
-        g = tts.decode_graph(B, tts.vocab + 4, top_k, 7, 4096, steps + 1, pen, capture=False)
+        g = tts.decode_graph(B, tts.vocab + 4, top_k, 7, max_keys, steps + 1, pen, capture=False)
         assert (g.fused is not None) == fused
         g.ids.fill_(tts.sos)
         g.set_window([[tts.sos]] * B)
@@ -78,6 +78,15 @@ def test_fused_step_full_batch_of_sixteen(dev, tts):
     items = _items(dev, 16, 5)
     lf, idf = _run(tts, dev, items, True, 12, 1)
     lm, idm = _run(tts, dev, items, False, 12, 1)
+    assert torch.equal(idf, idm)
+    assert ((lf - lm).abs() / lm.abs().amax(dim=-1, keepdim=True)).max().item() < 1e-4
+
+
+def test_fused_step_one_session_one_key_split(dev, tts):
+    """B = 1 and a 1024-key bound (one attention key split, S = 1): ids and logits as the multi-kernel step."""
+    items = _items(dev, 1, 7)
+    lf, idf = _run(tts, dev, items, True, 30, 4, None, max_keys=1024)
+    lm, idm = _run(tts, dev, items, False, 30, 4, None, max_keys=1024)
     assert torch.equal(idf, idm)
     assert ((lf - lm).abs() / lm.abs().amax(dim=-1, keepdim=True)).max().item() < 1e-4
 
