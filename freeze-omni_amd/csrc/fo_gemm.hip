@@ -449,10 +449,21 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
     if (n < a.N / 2) {
       const int P = n >> 4, c = n & 15;
       float x1 = 0.f, x2 = 0.f;
-      for (int q = 0; q < a.S; ++q) {
-        const float* p = a.ws + q * slab + (size_t)m * Ncols + P * 32 + c;
-        x1 += p[0];
-        x2 += p[16];
+      const float* p = a.ws + (size_t)m * Ncols + P * 32 + c;
+      for (int q0 = 0; q0 < a.S; q0 += 4) {  // four slabs' loads in flight, summed in slab order
+        float t1[4], t2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < a.S) {
+            t1[j] = p[(q0 + j) * slab];
+            t2[j] = p[(q0 + j) * slab + 16];
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < a.S) {
+            x1 += t1[j];
+            x2 += t2[j];
+          }
       }
       rope_store(a, m, rope_col(a, P, c), x1 * rs, x2 * rs);
     }
@@ -462,10 +473,21 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
   if (n < a.N) {
     const int col = sw ? (n >> 4) * 32 + (n & 15) : n;
     float v = 0.f, u = 0.f;
-    for (int q = 0; q < a.S; ++q) {
-      const float* p = a.ws + q * slab + (size_t)m * Ncols + col;
-      v += p[0];
-      if (sw) u += p[16];
+    const float* p = a.ws + (size_t)m * Ncols + col;
+    for (int q0 = 0; q0 < a.S; q0 += 4) {  // four slabs' loads in flight (one round trip, not four), summed in
+      float tv[4], tu[4];                   // slab order: the same result bit for bit
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (q0 + j < a.S) {
+          tv[j] = p[(q0 + j) * slab];
+          tu[j] = sw ? p[(q0 + j) * slab + 16] : 0.f;
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (q0 + j < a.S) {
+          v += tv[j];
+          if (sw) u += tu[j];
+        }
     }
     y = epilogue_store(a, sw != 0, m, n, v * rs, u * rs);
   }
