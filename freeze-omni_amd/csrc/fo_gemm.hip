@@ -68,6 +68,7 @@ struct GemmArgs {
   float lneps;
   float* sout1;          // producer: [M][groups] partial sums of Y (with sout: LayerNorm statistics)
   const float* rstats1;  // LayerNorm consumer: the producer's partial sums (rstats: sums of squares)
+  unsigned long long* trc;  // probes only (fo_gemm_set_trace): per-workgroup wall clocks, 24 slots
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -159,6 +160,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   const int m0 = mt * ROWS;
   int rbeff = (a.M - m0 + 15) >> 4;
   if (rbeff > RB) rbeff = RB;
+  unsigned long long* const trc =
+      a.trc ? a.trc + (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 24 : nullptr;
+  if (trc && threadIdx.x == 0) trc[0] = wall_clock64();
 
   // post-scaled RMSNorm: prefetch the producer's partial sums of this workgroup's rows now, reduce
   // them after the main loop (their latency hides behind the weight stream)
@@ -341,6 +345,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     }
   }
 
+  if (trc && lane == 0) trc[1 + wave] = wall_clock64();
   // D layout (16x16x32): col = lane & 15, row = 4*(lane>>4) + i
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -349,6 +354,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) red[wave][t][r * 16 + 4 * (lane >> 4) + i][lane & 15] = acc[t][r][i];
   __syncthreads();
+  if (trc && threadIdx.x == 0) trc[17] = wall_clock64();
 
   constexpr int NE = NT * ROWS * 16;
   for (int e = threadIdx.x; e < NE; e += NTH) {
@@ -385,6 +391,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
       slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = red[0][t][rr][c];
     }
+    if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
     return;
   }
   if constexpr (NT == 2 && !SW) {
@@ -393,6 +400,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         const int rr = e >> 4, c = e & 15, m = m0 + rr;
         if (m < a.M) rope_store(a, m, rope_col(a, tg, c), red[0][0][rr][c], red[0][1][rr][c]);
       }
+      if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
       return;
     }
   }
@@ -425,6 +433,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       if (a.yg && lane < cnt) a.yg[(size_t)m * a.ldy + n0 + lane] = v * a.gnext[n0 + lane];
     }
   }
+  if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
 }
 
 // Sum of the S partial slabs + epilogue for the split-K path.  Grid (ceil(N/256), M): one row
@@ -551,6 +560,8 @@ void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStre
     else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
   }
 }
+
+thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
 
 // forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
 thread_local int g_force_nw = 0, g_force_nt = 0;
@@ -845,6 +856,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.lneps = lneps;
   a.sout1 = sout1;
   a.rstats1 = rstats1;
+  a.trc = g_trc;
   FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
   if (lnw) {
     FO_REQUIRE(lnb && x_f32 && M <= 32 && !swiglu && rstats && rstats1 && rgroups > 0 && !rope && ldx % 4 == 0,
@@ -1111,6 +1123,11 @@ int fo_gemm_set_xs(int on) {
   const int prev = xs_mode() ? 1 : 0;
   g_xs = on;
   return prev;
+}
+
+int fo_gemm_set_trace(void* trace) {
+  g_trc = reinterpret_cast<unsigned long long*>(trace);
+  return 0;
 }
 
 int fo_gemm_tune(int nw, int nt) {

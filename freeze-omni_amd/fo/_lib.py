@@ -56,6 +56,7 @@ _SIGS = {
     "fo_event_destroy": (c_int, [c_vp]),
     "fo_gemm_tune": (c_int, [c_int, c_int]),
     "fo_gemm_set_xs": (c_int, [c_int]),
+    "fo_gemm_set_trace": (c_int, [c_vp]),
     "fo_tts_step_ws_floats": (c_ll, [c_int, c_int, c_int, c_int, c_int]),
     "fo_tts_step": (c_int, [ctypes.POINTER(FoTtsStep), c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),

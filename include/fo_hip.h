@@ -81,6 +81,10 @@ int fo_gemm_tune(int nw, int nt);
  * o, gate/up, lm_head): 0 off, 1 on (default; FO_GEMM_XS=0 turns it off).  Process-global; returns the
  * previous setting. */
 int fo_gemm_set_xs(int on);
+/* probe hook: the calling thread's following fo_gemm launches (grid kernels) write per-workgroup wall clocks
+ * (100 MHz) to trace[wg * 24 + slot]: 0 start, 1 + w the end of wave w's weight stream, 17 the K reduce done,
+ * 18 the epilogue issued.  nullptr turns it off (the default).  Returns 0. */
+int fo_gemm_set_trace(void* trace);
 /* Software-pipelined one-row-tile fp32-X weight-stream GEMMs (M <= 16, >= 32 MB of weights: the next
  * k-group's weights + X in flight during this group's MFMAs).  3 (default): the measured policy; 0: plain
  * loops; 1 / 2: every such GEMM pipelined with 4 / 2 k-steps per group (sweeps).  Unset, the
