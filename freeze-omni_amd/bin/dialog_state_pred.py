@@ -4,8 +4,9 @@ Same class name, constructor arguments, public methods and decision rule as the 
 session; the five polling threads become synchronous stages (fo.duplex.DuplexSession.pump) and every
 session of a replica is prefilled in one batched launch sequence per tick by the replica's
 fo.duplex.DuplexScheduler (start_all_threads registers the session with it; run_scheduler() or
-tick() drives it).  Transport (flask-socketio emits, the task-manager 'tm_audio_chunk' stream) is out
-of scope: socketio is accepted and ignored.
+tick() drives it).  Transport: `socketio` is any object with
+emit(event, data, to=sid) -- bin/server.py's hub -- and receives the reference's emits (VAD state and
+events, dialog_ss, dialog state updates, and 'tm_audio_chunk' to the task manager's sid; web/emit.py).
 """
 import os
 
@@ -49,7 +50,6 @@ class DialogStateParams(DuplexSession):
         return cls.PIPELINE_POOL
 
     def __init__(self, sid, socketio=None, event_outlet=None, user_ipu_outlet_list=(), parent_logger=None, vad=None):
-        self.socketio = socketio
         self.pipeline_pool = self._pool()
         self.pipeline_obj = self.pipeline_pool.acquire()
         if self.pipeline_obj is None:
@@ -57,7 +57,8 @@ class DialogStateParams(DuplexSession):
         self.tm_sid = None
         try:
             super().__init__(self.pipeline_obj.pipeline_proc, sid, self.DIALOG_STATE_PRED_CONFIGS, vad=vad,
-                             event_outlet=event_outlet, user_ipu_outlet_list=user_ipu_outlet_list)
+                             event_outlet=event_outlet, user_ipu_outlet_list=user_ipu_outlet_list,
+                             socketio=socketio)
         except Exception:
             self.pipeline_pool.release(self.pipeline_obj)
             raise

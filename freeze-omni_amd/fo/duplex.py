@@ -23,6 +23,8 @@ import copy
 import numpy as np
 import torch
 
+from web import emit as ev
+
 RESPONSE_THRESHOLD = 0.5   # configs/dialog_state_pred_config.yaml:40-41
 
 DEFAULT_CONFIG = {         # configs/dialog_state_pred_config.yaml (the fork's duplex settings)
@@ -86,6 +88,33 @@ class ScriptedVAD:
         return {"audio": audio, "status": status, "cached_audio": cached, "time_stamp": audio_dict.get("time_stamp")}
 
 
+class EnergyVAD(ScriptedVAD):
+    """Live-audio PureVAD stand-in for the server transport (silero-vad is not installed): a chunk is
+    speech when its RMS is above `threshold_dbfs`; an IPU closes only after `min_silent_duration_second`
+    of consecutive silence (the YAML's hangover, configs/dialog_state_pred_config.yaml vad block), so
+    short pauses stay inside one IPU.  Same predict() contract and pre-roll as ScriptedVAD."""
+
+    def __init__(self, chunk_size, sample_rate=16000, cache_history_size=2, threshold_dbfs=-40.0,
+                 min_silent_duration_second=0.5):
+        self.threshold = 10.0 ** (threshold_dbfs / 20.0)
+        self.hang = max(1, int(round(min_silent_duration_second * sample_rate / chunk_size)))
+        super().__init__(chunk_size, [], sample_rate, cache_history_size)
+
+    def reset(self):
+        super().reset()
+        self.silent = 0
+
+    def is_speech(self, k):
+        a = self._audio
+        loud = a.size > 0 and float(np.sqrt(np.mean(np.square(a, dtype=np.float64)))) > self.threshold
+        self.silent = 0 if loud else self.silent + 1
+        return loud or (self.in_speech and self.silent < self.hang)
+
+    def predict(self, audio_dict):
+        self._audio = np.asarray(audio_dict["audio"], dtype=np.float32)
+        return super().predict(audio_dict)
+
+
 class IPURecord:
     """One inter-pausal unit of a speaker (stands in for AudioLLMInterface.IPUHandle, absent from the
     reference tree): the response state the predictor last registered for it."""
@@ -111,9 +140,12 @@ class DuplexSession:
     as synchronous stages.  pipeline: a models.pipeline.inferencePipeline (fork API)."""
 
     def __init__(self, pipeline, sid=0, config=None, vad=None, event_outlet=None, user_ipu_outlet_list=(),
-                 dialog_state_callback=None, feature_gater=None):
+                 dialog_state_callback=None, feature_gater=None, socketio=None):
         cfg = copy.deepcopy(DEFAULT_CONFIG if config is None else config)
         self.cfg, self.sid, self.pipeline = cfg, sid, pipeline
+        # transport (bin/server.py): emit(event, data, to=sid) or None; tm_sid receives 'tm_audio_chunk'
+        self.socketio = socketio
+        self.tm_sid = getattr(self, "tm_sid", None)
         self.sr = cfg["audio"]["expected_sampling_rate"]
         self.threshold = cfg["dialog_state_decision"]["resp_threshold"]
         g = cfg["audio_feature_gating"]
@@ -228,6 +260,11 @@ class DuplexSession:
         else:
             return  # outside any IPU: the VAD thread forwards nothing to feature gating (:565-571)
         ann["ipu_id"] = self.current_ipu[ident].id if self.current_ipu[ident] is not None else ipu.id
+        if self.socketio is not None:                              # :565-590
+            ev.emit_vad_state_update(self.socketio, self.sid, status != "ipu_el", ident)
+            ev.emit_vad_event(self.socketio, self.sid, status, ident)
+            ev.emit_tm_audio_chunk(self.socketio, self.tm_sid, ident, status, ann["audio"], ann["time_stamp"],
+                                   ann.get("cached_audio"))
         gated = self.feature_gater[ident].process_and_gate(ann)
         if not gated:
             return
@@ -264,8 +301,11 @@ class DuplexSession:
         state = None
         if ident == "user" and probs is not None:
             state = "dialog_ss" if probs["state_1"] > self.threshold else "dialog_cl"
-            if state == "dialog_ss" and self.dialog_state_callback is not None:
-                self.dialog_state_callback(self, data)
+            if state == "dialog_ss":
+                ev.emit_dialog_ss_callback(self.socketio, self.sid)       # :826
+                if self.dialog_state_callback is not None:
+                    self.dialog_state_callback(self, data)
+            ev.emit_dialog_state_update(self.socketio, self.sid, state)  # :833-837
         self.prediction_cnt += 1
         if ident == "user":
             ipu = self.all_ipus["user"].get(data["ipu_id"])

@@ -116,3 +116,61 @@ def test_duplex_scheduler_matches_per_session(pipe):
             else:
                 assert p1 is None and st1 is None
     assert n_sys > 0   # system speech really went through the system encoder / prefill
+
+
+def test_server_transport_on_device(dev, pipe):
+    """bin/server.py with the production session factory (DialogStateParams on the replica pool, tiny
+    config) over loopback TCP: the emitted VAD events follow the scripted schedule and the emitted
+    dialog states equal a direct sequential llm_prefill run of the same audio."""
+    import argparse
+    import threading
+    from bin.dialog_state_pred import DialogStateParams
+    from bin.server import DialogClient, DialogServer, TransportServer, dialog_session_factory
+    from fo.duplex import DuplexSession, ScriptedVAD
+
+    u_iv, s_iv = [(0.2, 1.3)], [(1.5, 2.2)]
+    ch, n = 3584, 11
+    pcm = {"user": (np.clip(_pcm(n * ch, 31), -1, 1) * 32767).astype(np.int16),
+           "system": (np.clip(_pcm(n * ch, 32), -1, 1) * 32767).astype(np.int16)}
+    # direct run
+    ds = DuplexSession(pipe, sid=0, vad={"user": ScriptedVAD(ch, u_iv), "system": ScriptedVAD(ch, s_iv)},
+                       config=None)
+    for k in range(n):
+        for ident in ("user", "system"):
+            ds.enqueue_audio_data(ident, {"audio": pcm[ident][k * ch:(k + 1) * ch].tobytes(), "sr": 16000,
+                                          "enc": "s16le", "time_stamp": k * ch / 16000})
+    ds.pump()
+    while (d := ds.next_feature()) is not None:
+        ds.llm_prefill(d)
+    want = [(st, p["state_1"]) for ident, _, st, p in ds.states if ident == "user"]
+    ds.release()
+
+    DialogStateParams.PIPELINE_POOL = None
+    args = argparse.Namespace(config=None, model_path=TINY, llm_path=os.path.join(TINY, "llm"), top_k=1, top_p=0.0,
+                              temperature=1.0, llm_exec_nums=1)
+    dialog = DialogServer(dialog_session_factory(args), max_users=2, timeout=60.0)
+    srv = TransportServer(("127.0.0.1", 0), dialog)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    c = DialogClient(*srv.server_address, timeout=120.0)
+    try:
+        c.send("start", {"vad_intervals": u_iv, "system_vad_intervals": s_iv})
+        c.wait("started")
+        for k in range(n):
+            for ident in ("user", "system"):
+                c.send_audio(ident, pcm[ident][k * ch:(k + 1) * ch], k * ch / 16000)
+        c.send("stop")
+        c.wait("stopped")
+    finally:
+        c.close()
+        srv.shutdown()
+        srv.server_close()
+        dialog.shutdown()
+        DialogStateParams.PIPELINE_POOL = None
+    vad_u = [m["data"]["event_type"] for m in c.events if m["event"] == "vad_event" and m["data"]["identity"] == "user"]
+    assert vad_u == ["ipu_sl"] + ["ipu_cl"] * 4 + ["ipu_el"]
+    got = [m["data"]["dialog_state"] for m in c.events if m["event"] == "dialog_state_update"]
+    assert len(got) == len(want) > 0
+    for g, (w, p1) in zip(got, want):
+        if abs(p1 - 0.5) > 1e-3:
+            assert g == w
+    assert sum(m["event"] == "dialog_ss" for m in c.events) == got.count("dialog_ss")
