@@ -137,6 +137,25 @@ __device__ __forceinline__ void rope_store(const GemmArgs& a, int m, int n, floa
     d[i + half] = x2;
   }
 }
+// rope_store with the bias already added and the slot / cos / sin loaded ahead (gemm_body EPRE)
+__device__ __forceinline__ void rope_store_pre(const GemmArgs& a, int m, int n, float x1, float x2, int sl, float c,
+                                               float sn) {
+  const int hd = a.rhd, half = hd >> 1;
+  const int h = n / hd, i = n - h * hd;
+  const int page = sl / a.rPS, off = sl - page * a.rPS;
+  float* d;
+  if (h < a.rH + a.rKVH) {
+    const float o1 = x1 * c - x2 * sn, o2 = x2 * c + x1 * sn;
+    x1 = o1;
+    x2 = o2;
+    d = h < a.rH ? a.rq + (size_t)m * a.rH * hd + (size_t)h * hd
+                 : a.rk + (((size_t)page * a.rKVH + (h - a.rH)) * a.rPS + off) * hd;
+  } else {
+    d = a.rv + (((size_t)page * a.rKVH + (h - a.rH - a.rKVH)) * a.rPS + off) * hd;
+  }
+  d[i] = x1;
+  d[i + half] = x2;
+}
 // logical first column of rope tile pair P, column c
 __device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
   const int per = a.rhd >> 5;  // tile pairs per head
@@ -163,6 +182,51 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   unsigned long long* const trc =
       a.trc ? a.trc + (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 24 : nullptr;
   if (trc && threadIdx.x == 0) trc[0] = wall_clock64();
+
+  // Epilogue operands prefetched before the weight stream when every output element of the workgroup
+  // has its own thread (the small-M, latency-bound shapes): the residual, bias and next-norm gamma (plain
+  // path) or the token's slot / position, its cos / sin and the q|k|v bias (RoPE path) arrive while the
+  // weights stream, instead of costing one or two dependent memory round trips after the K reduction.
+  constexpr int LT = SW ? NT / 2 : NT;  // logical output tiles
+  constexpr bool EPRE = !SW && !LN && NT <= 2 && LT * ROWS * 16 <= NTH;
+  const int ee = threadIdx.x;
+  const int e_lt = ee / (ROWS * 16), e_rr = (ee >> 4) % ROWS, e_c = ee & 15;
+  float p_res = 0.f, p_bias = 0.f, p_b2 = 0.f, p_cos = 1.f, p_sin = 0.f, p_gn = 0.f;
+  int p_slot = 0;
+  const bool e_rope = (NT == 2 && !SW) && a.rq != nullptr;
+  if constexpr (EPRE) {
+    if (a.S == 1 && ee < LT * ROWS * 16) {
+      const int m = m0 + e_rr;
+      if (e_rope) {
+        if (ee < ROWS * 16 && m < a.M) {
+          const int n = rope_col(a, tg, e_c), half = a.rhd >> 1;
+          const int h = n / a.rhd, i = n - h * a.rhd;
+          p_slot = a.rslot[m];
+          if (a.bias) {
+            p_bias = a.bias[n];
+            p_b2 = a.bias[n + half];
+          }
+          if (h < a.rH + a.rKVH) {
+            const int p = a.rpos[m];
+            p_cos = a.rcos[(size_t)p * half + i];
+            p_sin = a.rsin[(size_t)p * half + i];
+          }
+        }
+      } else {
+        const int n = (tg * LT + e_lt) * 16 + e_c;
+        if (m < a.M && n < a.N) {
+          const size_t o = (size_t)m * a.ldy + n;
+          if (a.residual) p_res = a.out_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(a.Y)[o])
+                                             : reinterpret_cast<const float*>(a.Y)[o];
+          if (a.bias) p_bias = a.bias[n];
+        }
+      }
+    }
+    if (a.S == 1 && !e_rope && a.yg) {
+      const int n0 = tg * LT * 16;
+      if (lane < min(LT * 16, a.N - n0)) p_gn = a.gnext[n0 + lane];
+    }
+  }
 
   // post-scaled RMSNorm: prefetch the producer's partial sums of this workgroup's rows now, reduce
   // them after the main loop (their latency hides behind the weight stream)
@@ -396,6 +460,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   }
   if constexpr (NT == 2 && !SW) {
     if (a.rq) {
+      if constexpr (EPRE) {
+        if (ee < ROWS * 16 && m0 + e_rr < a.M)
+          rope_store_pre(a, m0 + e_rr, rope_col(a, tg, e_c), red[0][0][e_rr][e_c] + p_bias,
+                         red[0][1][e_rr][e_c] + p_b2, p_slot, p_cos, p_sin);
+        if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
+        return;
+      }
       for (int e = threadIdx.x; e < ROWS * 16; e += NTH) {
         const int rr = e >> 4, c = e & 15, m = m0 + rr;
         if (m < a.M) rope_store(a, m, rope_col(a, tg, c), red[0][0][rr][c], red[0][1][rr][c]);
@@ -404,7 +475,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       return;
     }
   }
-  constexpr int LT = SW ? NT / 2 : NT;  // logical output tiles
+  if constexpr (EPRE) {
+    if (ee < LT * ROWS * 16) {
+      const int m = m0 + e_rr, n = (tg * LT + e_lt) * 16 + e_c;
+      if (m < a.M && n < a.N) {
+        float v = red[0][e_lt][e_rr][e_c] + p_bias;
+        if (a.scale) v = v * a.scale[n] + a.shift[n];
+        v = apply_act(v, a.act) + p_res;
+        const size_t o = (size_t)m * a.ldy + n;
+        if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(v);
+        else reinterpret_cast<float*>(a.Y)[o] = v;
+        red[0][e_lt][e_rr][e_c] = v;
+      }
+    }
+  } else
   for (int e = threadIdx.x; e < LT * ROWS * 16; e += NTH) {
     const int lt = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
     const int m = m0 + rr;
@@ -430,7 +514,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         const float s1 = wave_sum(v);
         if (lane == 0) a.sout1[(size_t)m * gridDim.x + tg] = s1;
       }
-      if (a.yg && lane < cnt) a.yg[(size_t)m * a.ldy + n0 + lane] = v * a.gnext[n0 + lane];
+      if (a.yg && lane < cnt) a.yg[(size_t)m * a.ldy + n0 + lane] = v * (EPRE ? p_gn : a.gnext[n0 + lane]);
     }
   }
   if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
@@ -443,12 +527,22 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
   const int m = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  // epilogue operands first: their loads overlap the statistics and slab loads below instead of
+  // costing dependent round trips after the sum
+  float p_res = 0.f, p_bias = 0.f, p_gn = 0.f;
+  if (!a.rq && !sw && n < a.N) {
+    const size_t o = (size_t)m * a.ldy + n;
+    if (a.residual) p_res = a.out_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(a.Y)[o]) : reinterpret_cast<const float*>(a.Y)[o];
+    if (a.bias) p_bias = a.bias[n];
+    if (a.yg) p_gn = a.gnext[n];
+  }
   float rs = 1.f;
   if (a.rstats && !a.lnw) {  // RMSNorm consumer split over K: the row's rstd scales the summed partials
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {  // lane-strided + wave_sum: the order gemm_body's unsplit path uses
       float ss = 0.f;
-      for (int j = 0; j < a.rgroups; ++j) ss += a.rstats[(size_t)m * a.rgroups + j];
-      red_s[0] = rsqrtf(ss / (float)a.K + a.reps);
+      for (int j = threadIdx.x; j < a.rgroups; j += 64) ss += a.rstats[(size_t)m * a.rgroups + j];
+      ss = wave_sum(ss);
+      if (threadIdx.x == 0) red_s[0] = rsqrtf(ss / (float)a.K + a.reps);
     }
     __syncthreads();
     rs = red_s[0];
@@ -498,7 +592,16 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
           if (sw) u += tu[j];
         }
     }
-    y = epilogue_store(a, sw != 0, m, n, v * rs, u * rs);
+    if (sw) {
+      y = epilogue_store(a, true, m, n, v * rs, u * rs);
+    } else {
+      y = v * rs + p_bias;
+      if (a.scale) y = y * a.scale[n] + a.shift[n];
+      y = apply_act(y, a.act) + p_res;
+      const size_t o = (size_t)m * a.ldy + n;
+      if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(y);
+      else reinterpret_cast<float*>(a.Y)[o] = y;
+    }
   }
   if (a.sout && !sw) {
     const float ss = block_sum<4>(n < a.N ? y * y : 0.f, red_s);
@@ -507,7 +610,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       const float s1 = block_sum<4>(n < a.N ? y : 0.f, red_s);
       if (threadIdx.x == 0) a.sout1[(size_t)m * gridDim.x + blockIdx.x] = s1;
     }
-    if (a.yg && n < a.N) a.yg[(size_t)m * a.ldy + n] = y * a.gnext[n];
+    if (a.yg && n < a.N) a.yg[(size_t)m * a.ldy + n] = y * p_gn;
   }
 }
 

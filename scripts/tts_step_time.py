@@ -18,7 +18,7 @@ from oracle import configs  # noqa: E402
 from oracle.params import tts_shapes  # noqa: E402
 
 dev = torch.device("cuda:0")
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 8   # argv[2] == "multi": the multi-kernel step only
 cfg = configs.get("real")
 src = SynthSource(cfg["seed"], tts_shapes(cfg), dev, cfg["overrides"])
 tts = TTSEngine(src, cfg["decoder_json"], dev, kv_tokens=1 << 15)
@@ -27,7 +27,8 @@ e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
 lib.fo_event_create(ctypes.byref(e0))
 lib.fo_event_create(ctypes.byref(e1))
 gen = torch.Generator().manual_seed(0)
-for fused in (True, False, True, False):
+modes = (False, False) if "multi" in sys.argv[2:] else (True, False, True, False)
+for fused in modes:
     tts.fused = fused
     es = ops.engine_stream(dev)
     with torch.cuda.stream(es):
