@@ -180,11 +180,18 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   __shared__ int pg_s[MAXPG];
 
   const int it = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
-  const int seq = a.items[3 * it], t0 = a.items[3 * it + 1], tn = a.items[3 * it + 2];
+  const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it;  // NULL: one token each
+  const int tn = a.items ? a.items[3 * it + 2] : 1;
   const int G = a.H / a.KVH;
   const int R = tn * G;  // <= 16
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = lane >> 4, col = lane & 15;
+  const int* bt = a.block_table + (size_t)seq * a.maxb;
+  // a block-table row that fits is staged whole, requested together with the key counts (no wait for
+  // this split's page range first); longer rows stage the split's pages once the range is known
+  const bool whole = a.maxb <= MAXPG;
+  if (whole)
+    for (int i = tid; i < a.maxb; i += 256) pg_s[i] = bt[i];
   int Lmax = 0;
   for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
   int ns = a.nsplit;
@@ -203,13 +210,14 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
     if (a.cnt) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
     return;
   }
-  const int* bt = a.block_table + (size_t)seq * a.maxb;
-  const int pb = c0 / a.PS, npg = (c1 - 1) / a.PS - pb + 1;
-  if (npg > MAXPG) {  // host contract broken (split wider than 4096 keys): poison rather than read wrong keys
+  const int pb0 = c0 / a.PS, npg = (c1 - 1) / a.PS - pb0 + 1;
+  if (npg > MAXPG || (whole && (c1 - 1) / a.PS >= a.maxb)) {  // host contract broken: poison, never read wrong keys
     for (int r = tid; r < R; r += 256) a.out[((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD] = NAN;
     return;
   }
-  for (int i = tid; i < npg; i += 256) pg_s[i] = bt[pb + i];
+  const int pb = whole ? 0 : pb0;  // pg_s holds pages pb..
+  if (!whole)
+    for (int i = tid; i < npg; i += 256) pg_s[i] = bt[pb + i];
   if (tid < 16) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
 
   // Q as A fragments: row = col (lane & 15), d = 32 c + 8 grp; rows >= R are zero
@@ -392,17 +400,21 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
   __shared__ int pg_s[MAXPG];
   const int it = blockIdx.x, h = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int seq = a.items[3 * it], t0 = a.items[3 * it + 1];
+  // items == NULL: the dense decode batch (item b = sequence b = token b), nothing to look up first
+  const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it;
+  // the visible-key count, the whole block-table row and q are requested together (none waits on
+  // another); pages past the session's keys are staged but never dereferenced
   const int L = a.tok_nvis[t0];
+  const int* bt = a.block_table + (size_t)seq * a.maxb;
+  const int nb = a.maxb < MAXPG ? a.maxb : MAXPG;
+  for (int i = tid; i < nb; i += DEC_NT) pg_s[i] = bt[i];
+  const float* qr = a.q + ((size_t)t0 * a.H + h) * HD;
+  for (int d = tid; d < HD; d += DEC_NT) q_s[d] = qr[d] * a.scale;
   float* orow = a.out + ((size_t)t0 * a.H + h) * HD;
-  if (L > DEC_MAXK || (L + a.PS - 1) / a.PS > MAXPG) {  // host contract broken: poison, never read wrong keys
+  if (L > DEC_MAXK || (L + a.PS - 1) / a.PS > nb) {  // host contract broken: poison, never read wrong keys
     if (tid < HD) orow[tid] = NAN;
     return;
   }
-  const int* bt = a.block_table + (size_t)seq * a.maxb;
-  for (int i = tid; i < (L + a.PS - 1) / a.PS; i += DEC_NT) pg_s[i] = bt[i];
-  const float* qr = a.q + ((size_t)t0 * a.H + h) * HD;
-  for (int d = tid; d < HD; d += DEC_NT) q_s[d] = qr[d] * a.scale;
   __syncthreads();
   const size_t page_sz = (size_t)a.KVH * a.PS * HD, head_off = (size_t)h * a.PS * HD;
   // P.V layout: HD/4 lanes per key (one float4 of the V row each), 64/(HD/4) keys per wave-instruction,
@@ -715,6 +727,7 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
                  float scale, int nsplit, float* part_ml, float* part_o, float* out, int* tickets,
                  int keys_per_split, hipStream_t s) {
   FO_REQUIRE(T > 0 && n_items > 0 && KVH > 0 && H % KVH == 0, "fo_attention: bad shape");
+  FO_REQUIRE(items || n_items == T, "fo_attention: items NULL needs one token per item (n_items == T)");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
   FO_REQUIRE(max_rows >= 1 && max_rows <= 16, "fo_attention: %d query rows per item (max 16)", max_rows);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");

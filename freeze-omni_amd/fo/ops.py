@@ -362,10 +362,13 @@ ATTN_KEYS_PER_SPLIT = 256
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,
               part_ml, part_o, out, tickets=None, keys_per_split=ATTN_KEYS_PER_SPLIT):
     """tickets: zeroed int32 [>= n_items * KVH] -> splits sized from each item's key count (at most
-    nsplit) merged inside the launch; None -> nsplit static splits + a combine launch."""
+    nsplit) merged inside the launch; None -> nsplit static splits + a combine launch.
+    items None: a decode batch, one token per sequence (item b = sequence b = token b)."""
+    if items is None and n_items != T:
+        raise ValueError("attention: items=None needs one token per sequence (n_items == T)")
     if tickets is not None and tickets.numel() < n_items * KVH:
         raise ValueError("attention tickets buffer smaller than n_items * KVH")
-    _lib.call("fo_attention", q.data_ptr(), T, items.data_ptr(), n_items, max_rows, tok_nvis.data_ptr(),
+    _lib.call("fo_attention", q.data_ptr(), T, ptr(items), n_items, max_rows, tok_nvis.data_ptr(),
               block_table.data_ptr(), block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd, float(scale),
               nsplit, ptr(part_ml), ptr(part_o), out.data_ptr(), ptr(tickets), int(keys_per_split), stream(q.device))
     return out

@@ -8,11 +8,17 @@ models/audioLLM.py:479-484 and models/decoder/decoder.py:127-188,294-312):
   down GEMM (+residual, in place).
 The residual stream is fp32; GEMMs read it as fp32 (bf16 hi/lo split) against bf16 weights.
 """
+import os
+
 import torch
 
 from . import ops
 from .kv import BatchMeta
 from .ops import F32, PackedLinear
+
+# FO_ATTN_DENSE=0 passes the item table even for one-token-per-sequence batches (A/B against a
+# library older than fo_attention's items == NULL form)
+ATTN_DENSE = os.environ.get("FO_ATTN_DENSE", "1") == "1"
 
 
 class Layer:
@@ -84,6 +90,8 @@ class DecoderStack:
         scale = hd ** -0.5
         sA, sB, xg = ws["sA"], ws["sB"], ws["xg"][:T]
         last = len(self.layers) - 1
+        # one token per sequence (decode): the attention needs no item table (fo_attention items NULL)
+        dense = ATTN_DENSE and meta.n_items == T == meta.S
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
@@ -94,7 +102,7 @@ class DecoderStack:
                 L.qkv.qkv_rope(h, T, *rope)
             else:       # input RMSNorm fused: x*gamma and row sums came from the previous down proj
                 L.qkv.qkv_rope(xg, T, *rope, norm=(sA, self.eps))
-            ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
+            ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
                           self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
                           att, tickets=ws["tickets"], keys_per_split=self.attn_kps)
             L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))

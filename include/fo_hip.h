@@ -144,7 +144,8 @@ int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, c
 /* GQA attention over paged KV for a ragged batch (transformers sdpa/eager attention reached from
  * models/audioLLM.py:482 and models/decoder/decoder.py:142-153,299-311); token t sees the first
  * tok_nvis[t] keys of its sequence (causal: own cache index + 1, full/unmasked: all).  items
- * [n_items][3] = (sequence, first token, token count), token count * H/KVH <= max_rows <= 16.
+ * [n_items][3] = (sequence, first token, token count), token count * H/KVH <= max_rows <= 16;
+ * items may be NULL when every sequence contributes one token (n_items == T: item b = sequence b = token b).
  * Split-KV (nsplit from fo_attn_nsplit) + combine. */
 int fo_attention(const float* q, int T, const int* items, int n_items, int max_rows, const int* tok_nvis,
                  const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,

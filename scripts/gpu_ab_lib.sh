@@ -9,15 +9,15 @@ O=gpurun_out/ab_lib.txt
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log >> $O
 for L in base new; do
-  if [ $L = base ]; then export FO_LIB_PATH=$BASE; else unset FO_LIB_PATH; fi
+  if [ $L = base ]; then export FO_LIB_PATH=$BASE FO_ATTN_DENSE=${BASE_ATTN_DENSE:-1}; else unset FO_LIB_PATH FO_ATTN_DENSE; fi
   echo "== $L tts step" >> $O
   timeout -k 10 120 python -u scripts/tts_step_time.py 8 multi >> $O 2>&1 || exit 1
   echo "== $L gemm trace" >> $O
   timeout -k 10 200 python -u scripts/gemm_trace.py >> $O 2>&1 || exit 1
 done
-unset FO_LIB_PATH
+unset FO_LIB_PATH FO_ATTN_DENSE
 for i in 1 2; do
-  FO_LIB_PATH=$BASE timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 > gpurun_out/ab_base$i.log 2>&1 || exit 1
+  FO_LIB_PATH=$BASE FO_ATTN_DENSE=${BASE_ATTN_DENSE:-1} timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 > gpurun_out/ab_base$i.log 2>&1 || exit 1
   timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 > gpurun_out/ab_new$i.log 2>&1 || exit 1
 done
 for f in gpurun_out/ab_base1.log gpurun_out/ab_new1.log gpurun_out/ab_base2.log gpurun_out/ab_new2.log; do

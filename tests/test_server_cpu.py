@@ -116,7 +116,7 @@ def test_server_streams_session_events_and_tm_chunks():
 def test_server_max_users_errors_and_timeout():
     from bin.server import DialogClient
 
-    srv, dialog, _ = _serve(max_users=1, timeout=0.3)
+    srv, dialog, _ = _serve(max_users=1, timeout=1.5)
     host, port = srv.server_address
     a, b = DialogClient(host, port), DialogClient(host, port)
     try:
