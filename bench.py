@@ -97,6 +97,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
     import torch
     from fo.speak import speak
     B = len(pcms)
+    t_begin = time.perf_counter()
     turns = [Turn(engine, base_kv, p) for p in pcms]
     fb = engine.fbank("A")
     CH = turns[0].framer.chunk
@@ -145,6 +146,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
         if len(hiddens) == args.text_tokens:
             break
         nxt, hid = engine.text_step([(t.kv, [text_ids[b][-1]]) for b, t in enumerate(turns)])
+    t_text = time.perf_counter()   # the last text step's ids were read back: the text stage is done
     D = engine.llm.D
     idim = engine.cfg["decoder_json"][0]
     items = []
@@ -166,9 +168,12 @@ def run_turn(engine, base_kv, pcms, args, sync):
             first[i] = now
         last[i] = now
         samples[i] += seg.numel()
+    t_end = time.perf_counter()
     for t in turns:
         t.kv.free()
-    return dict(t_ss=t_ss, first=first, last=last, samples=samples, first_pcm=[s.t_first_pcm for s in states])
+    stage = {"listen": (t_ss - t_begin) * 1e3, "text": (t_text - t_ss) * 1e3, "speak": (t_end - t_text) * 1e3}
+    return dict(t_ss=t_ss, first=first, last=last, samples=samples, first_pcm=[s.t_first_pcm for s in states],
+                stage=stage)
 
 
 def cpu_model():
@@ -600,6 +605,11 @@ def main():
                          "rocprof_calls": rp_calls,
                          "rocprof_frac": None if rp_us is None else round(probe["bytes"] / (rp_us * 1e-6) / 1e9 / peak, 4),
                          "rocprof_source": rp_src},
+            # wall ms per stage of a timed turn (median over the timed turns): listen = 63 chunks through
+            # fbank / encoder / adapter / Qwen2 / state head (pipelined), text = dialog_ss -> the last text
+            # token's id on the host, speak = TTS prefill + AR decode + vocoder until the last PCM segment
+            "stage_ms": {k: round(float(np.median([s["stage"][k] for s in stats])), 2)
+                         for k in ("listen", "text", "speak")},
             "single_user": single,
             "cpu_baseline": cpu,
         }
