@@ -47,6 +47,9 @@ if len(sys.argv) > 1 and sys.argv[1] == "mid":   # duplex: 8 sessions x 7 encode
               ("enc_ff1_56", 4096, 1024, 56, False), ("enc_ff2_56", 1024, 4096, 56, False),
               ("qwen_gu32", 18944, 3584, 32, True), ("qwen_gu48", 18944, 3584, 48, True),
               ("qwen_down32", 3584, 18944, 32, False), ("qwen_qkv32", 4608, 3584, 32, False)]
+elif len(sys.argv) > 1 and sys.argv[1] == "tts":   # the AR decode step's shapes only
+    shapes = [("tts_qkv", 1152, 896, 8, False), ("tts_o", 896, 896, 8, False), ("tts_gu", 4864, 896, 8, True),
+              ("tts_down", 896, 4864, 8, False), ("tts_out", 1028, 896, 8, False)]
 else:
     shapes = None
 shapes = shapes or [("tts_qkv", 2688, 896, 8, False), ("tts_o", 896, 896, 8, False), ("tts_gu", 4864, 896, 8, True),
