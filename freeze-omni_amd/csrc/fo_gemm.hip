@@ -90,6 +90,25 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
   }
 }
 
+// In-launch split-K merge (gemm_body, a.counters set by fo_gemm): each split's partial tile is stored
+// write-through (sc1: a relaxed agent-scope atomic store, so it leaves this XCD's L2 without a release
+// fence), the split drains its stores and takes the tile's ticket; the last split to arrive reads the others
+// back with sc1 buffer loads (past its L1 / L2) and runs the epilogue -- no second launch, no fences.
+typedef __attribute__((address_space(1))) float g_f32;
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store((g_f32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  const unsigned long long b = (unsigned long long)base;
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
+                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)b)),
+      (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float ld_sc1(__amdgpu_buffer_rsrc_t r, size_t off_floats) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (unsigned)(off_floats * 4), 0, 16));
+}
+
 // Output element (m, n): bias, folded-BN affine, activation or SwiGLU, residual, store.
 __device__ __forceinline__ float epilogue_store(const GemmArgs& a, bool sw, int m, int n, float v, float u) {
   if (sw) {
@@ -194,8 +213,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   float p_res = 0.f, p_bias = 0.f, p_b2 = 0.f, p_cos = 1.f, p_sin = 0.f, p_gn = 0.f;
   int p_slot = 0;
   const bool e_rope = (NT == 2 && !SW) && a.rq != nullptr;
+  // split over K with the in-launch merge (fo_gemm passes counters only for plain tiles): any split may be
+  // the last to arrive, so every split prefetches the epilogue operands
+  const bool merge = !SW && !LN && a.S > 1 && a.counters != nullptr;
   if constexpr (EPRE) {
-    if (a.S == 1 && ee < LT * ROWS * 16) {
+    if ((a.S == 1 || merge) && ee < LT * ROWS * 16) {
       const int m = m0 + e_rr;
       if (e_rope) {
         if (ee < ROWS * 16 && m < a.M) {
@@ -222,7 +244,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         }
       }
     }
-    if (a.S == 1 && !e_rope && a.yg) {
+    if ((a.S == 1 || merge) && !e_rope && a.yg) {
       const int n0 = tg * LT * 16;
       if (lane < min(LT * 16, a.N - n0)) p_gn = a.gnext[n0 + lane];
     }
@@ -428,7 +450,59 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     for (int w = 0; w < NW; ++w) v += red[w][t][rr][c];
     red[0][t][rr][c] = v;
   }
-  if (a.rstats && !LN && a.S == 1) {  // (split over K: k_gemm_reduce scales the summed partials)
+  if (a.S > 1) {
+    // K split across workgroups: write this split's partial slab; without the merge k_gemm_reduce (the
+    // next launch on the stream) sums the slabs in split order and applies the epilogue
+    const int Mrows = gridDim.y * ROWS;
+    const int Ncols = a.ntiles * 16;
+    float* slab = a.ws + (size_t)sp * Mrows * Ncols;
+    if (!merge) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < NE; e += NTH) {
+        const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+        slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = red[0][t][rr][c];
+      }
+      if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
+      return;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NE; e += NTH) {
+      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+      st_wt(slab + (size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c, red[0][t][rr][c]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int last_s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int* tk = a.counters + (blockIdx.x + gridDim.x * blockIdx.y);
+      const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = old == a.S - 1;
+      if (old == a.S - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_s) return;
+    // the last split: every split's partial, summed in split order (k_gemm_reduce's order, bit for bit)
+    const __amdgpu_buffer_rsrc_t rws = rsrc_of(a.ws);
+    const size_t sl = (size_t)Mrows * Ncols;
+    for (int e = threadIdx.x; e < NE; e += NTH) {
+      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
+      const size_t o = (size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c;
+      const float own = red[0][t][rr][c];
+      float v = 0.f;
+      for (int q0 = 0; q0 < a.S; q0 += 4) {
+        float tv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          tv[j] = (q0 + j < a.S && q0 + j != sp) ? ld_sc1(rws, (q0 + j) * sl + o) : own;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < a.S) v += tv[j];
+      }
+      red[0][t][rr][c] = v;
+    }
+    __syncthreads();
+  }
+  if (a.rstats && !LN && (a.S == 1 || merge)) {  // (split without the merge: k_gemm_reduce scales the sums)
     if (!RPRE) load_rpart();
     __shared__ float rstd_s[ROWS];
 #pragma unroll
@@ -444,20 +518,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     }
   }
   __syncthreads();
-  if (a.S > 1) {
-    // K split across workgroups: write this split's partial slab; k_gemm_reduce (the next launch
-    // on the stream) sums the slabs in split order and applies the epilogue -- deterministic, and no
-    // cross-workgroup fence or ticket inside the GEMM.
-    const int Mrows = gridDim.y * ROWS;
-    const int Ncols = a.ntiles * 16;
-    float* slab = a.ws + (size_t)sp * Mrows * Ncols;
-    for (int e = threadIdx.x; e < NE; e += NTH) {
-      const int t = e / (ROWS * 16), rr = (e / 16) % ROWS, c = e & 15;
-      slab[(size_t)(m0 + rr) * Ncols + (tg * NT + t) * 16 + c] = red[0][t][rr][c];
-    }
-    if (trc && threadIdx.x == 0) trc[18] = wall_clock64();
-    return;
-  }
   if constexpr (NT == 2 && !SW) {
     if (a.rq) {
       if constexpr (EPRE) {
@@ -829,6 +889,18 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
   }
 }
 
+// in-launch split-K merge: 0 off, 1 every eligible split, 2 (default) splits of small weights only -- measured
+// (profiles/r02t_*): the TTS down (8.7 MB) 184.8 -> 181.5 us per AR step, the Qwen2 down (136 MB) slower
+// (LLM stage 3313 -> 3340 us: every one of its 224 workgroups drains write-through partials before exiting).
+// -1 = FO_GEMM_MERGE (0-2) decides at first use.
+int g_merge = -1;
+inline int merge_mode() {
+  if (g_merge < 0) {
+    const char* e = getenv("FO_GEMM_MERGE");
+    g_merge = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
+  }
+  return g_merge;
+}
 int g_xs = -1;  // X-stationary kernel for eligible M <= 16 GEMMs: -1 = FO_GEMM_XS (default on), 0 off, 1 on
 inline bool xs_mode() {
   if (g_xs < 0) {
@@ -1029,6 +1101,14 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     else if (KS >= 256 && a.ntiles >= 128) { NT = 4; S_auto = 4; }
     else if (KS >= 128 && a.ntiles <= 64) S_auto = 4;  // narrow long-K (TTS down): 10.9 -> 8.2 us in a graph
     else if (a.ntiles > 256) NT = 2;
+    // small SwiGLU pairs over 512+ tiles (the TTS gate/up, 608 tiles, 17.4 MB): 2 pairs per workgroup on 8
+    // waves keeps the grid within one round of the 256 CUs (152 instead of 304 workgroups): 7.83 -> 7.16 us
+    // graph-replayed (profiles/r02s_tts_gemm_sweep.txt)
+    if (swiglu && a.ntiles >= 512 && a.ntiles < 1024 && (long long)a.ntiles * 16 * K < (32ll << 20) &&
+        a.ntiles % 4 == 0) {
+      NT = 4;
+      nw_pref = 8;
+    }
     // Pipelined weight stream, 2-step groups (policy measured in the turn bench, A/B twice in one
     // call: 388-390 -> 383-386 ms/turn, p50 first PCM 50 -> 48.5 ms).  Isolated (scripts/
     // gemm_gu_sweep.py, gemm_pipe_ab.py; two alternating weight copies): gate/up at <= 8 rows on 2
@@ -1081,7 +1161,14 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     FO_REQUIRE(ws && need <= ws_floats, "fo_gemm: split-K workspace too small (%lld > %lld)", need, ws_floats);
   }
   dim3 grid(groups, mt, S);
-  if (sgroups) *sgroups = S > 1 ? (N + 255) / 256 : groups;
+  // one-row-tile plain splits merge inside the launch (last split to arrive sums and finishes; tickets in
+  // the caller's zeroed counters, left zeroed); otherwise k_gemm_reduce follows
+  const bool small_w = (long long)a.ntiles * 16 * K < (32ll << 20);
+  const bool merged = S > 1 && counters && RB == 1 && !swiglu && !lnw && !mid &&
+                      (merge_mode() == 1 || (merge_mode() == 2 && small_w));
+  a.counters = merged ? counters : nullptr;
+  if (merged) FO_REQUIRE((long long)groups * mt <= (1 << 20), "fo_gemm: too many tiles for the merge tickets");
+  if (sgroups) *sgroups = (S > 1 && !merged) ? (N + 255) / 256 : groups;
   const bool wstream = (long long)a.ntiles * 16 * K >= (32ll << 20);
   const long long wgs = (long long)groups * mt * S;
   if (lnw) {
@@ -1146,7 +1233,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     }
   }
   g_launch_pipe = 0;
-  if (S > 1) {
+  if (S > 1 && !merged) {
     int rc = fo::check_launch("fo_gemm/split");
     if (rc) return rc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, mt * RB * 16);
@@ -1225,6 +1312,13 @@ int fo_gemm_set_xs(int on) {
   FO_REQUIRE(on == 0 || on == 1, "fo_gemm_set_xs: 0 or 1");
   const int prev = xs_mode() ? 1 : 0;
   g_xs = on;
+  return prev;
+}
+
+int fo_gemm_set_merge(int on) {
+  FO_REQUIRE(on >= 0 && on <= 2, "fo_gemm_set_merge: 0, 1 or 2");
+  const int prev = merge_mode();
+  g_merge = on;
   return prev;
 }
 

@@ -56,6 +56,7 @@ _SIGS = {
     "fo_event_destroy": (c_int, [c_vp]),
     "fo_gemm_tune": (c_int, [c_int, c_int]),
     "fo_gemm_set_xs": (c_int, [c_int]),
+    "fo_gemm_set_merge": (c_int, [c_int]),
     "fo_gemm_set_trace": (c_int, [c_vp]),
     "fo_tts_step_ws_floats": (c_ll, [c_int, c_int, c_int, c_int, c_int]),
     "fo_tts_step": (c_int, [ctypes.POINTER(FoTtsStep), c_vp]),
@@ -158,7 +159,10 @@ def load(path=None):
             f"libfo_hip.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the Freeze-Omni MI355X path has no CPU fallback)")
     lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    override = p != os.path.join(_HERE, "libfo_hip.so")
     for name, (rt, at) in _SIGS.items():
+        if override and not hasattr(lib, name):
+            continue   # an older build under A/B (FO_LIB_PATH): entries it predates stay unbound
         fn = getattr(lib, name)
         fn.restype = rt
         fn.argtypes = at

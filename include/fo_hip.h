@@ -81,6 +81,14 @@ int fo_gemm_tune(int nw, int nt);
  * o, gate/up, lm_head): 0 off, 1 on (default; FO_GEMM_XS=0 turns it off).  Process-global; returns the
  * previous setting. */
 int fo_gemm_set_xs(int on);
+/* Split-K of the one-row-tile plain GEMMs (Qwen2 / TTS down, encoder FFN w2) merged inside the launch:
+ * each split stores its partial tile write-through and takes the tile's ticket in `counters` (zeroed
+ * ints, left zeroed); the last split sums every partial in split order (k_gemm_reduce's order, bit for
+ * bit) and runs the epilogue, so no reduce launch follows.  0: slabs + k_gemm_reduce everywhere; 1: merge
+ * every eligible split; 2 (default, FO_GEMM_MERGE overrides): merge splits of weights < 32 MB (the TTS
+ * down), where the reduce launch costs more than the write-through drain.  NULL counters always take the
+ * two-launch form.  Process-global; returns the previous setting. */
+int fo_gemm_set_merge(int on);
 /* probe hook: the calling thread's following fo_gemm launches (grid kernels) write per-workgroup wall clocks
  * (100 MHz) to trace[wg * 24 + slot]: 0 start, 1 + w the end of wave w's weight stream, 17 the K reduce done,
  * 18 the epilogue issued.  nullptr turns it off (the default).  Returns 0. */

@@ -10,6 +10,8 @@ tail -1 gpurun_out/pytest_gpu.log >> $O
 for E in "$ENV_A" "$ENV_B"; do
   echo "== $E stage probe" >> $O
   env $E timeout -k 10 200 python -u scripts/llm_stage_time.py 2>&1 | grep -v amdgpu.ids >> $O || exit 1
+  echo "== $E AR decode step" >> $O
+  env $E timeout -k 10 120 python -u scripts/tts_step_time.py 8 multi 2>&1 | grep -v amdgpu.ids >> $O || exit 1
 done
 for i in 1 2; do
   env $ENV_A timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 > gpurun_out/ab_A$i.log 2>&1 || exit 1

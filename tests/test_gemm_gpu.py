@@ -249,3 +249,43 @@ def test_gemm_pipelined_weight_stream(dev, mode, M, N, K, sw):
     a = x.double() @ w.double().t()
     ref = torch.nn.functional.silu(a) * (x.double() @ u.double().t()) if sw else a
     torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(8, 896, 4864), (16, 3584, 18944), (5, 1024, 4096)])
+def test_gemm_split_merge_in_launch_bit_exact(dev, M, N, K):
+    """Split-K merged inside the launch (fo_gemm_set_merge(1): write-through partials, per-tile ticket, the
+    last split sums in split order and runs the epilogue) == slabs + k_gemm_reduce bit for bit: the
+    residual-updated output and yg = y * gamma, launch after launch (tickets left zeroed); the RMSNorm row
+    statistics agree as sums (their grouping differs: per tile group vs per 256 columns)."""
+    from fo import _lib
+    from fo.ops import PackedLinear, RowStats
+    g = torch.Generator().manual_seed(M * N + K)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(dev)
+    res0 = torch.randn(M, N, generator=g).to(dev)
+    gamma = (1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    lin = PackedLinear(w.to(dev))
+    lib = _lib.load()
+
+    def run():
+        y = res0.clone()
+        yg = torch.empty_like(y)
+        st = RowStats(M, dev).set(gamma, yg)
+        lin(x, out=y, residual=True, splitk=4, stats_out=st)
+        ss = st.buf[:M * st.groups].view(M, st.groups).sum(1)
+        return y.cpu(), yg.cpu(), ss.cpu()
+
+    prev = lib.fo_gemm_set_merge(0)
+    assert prev in (0, 1, 2)
+    try:
+        y0, g0, s0 = run()
+        lib.fo_gemm_set_merge(1)
+        outs = [run() for _ in range(3)]
+    finally:
+        lib.fo_gemm_set_merge(prev)
+    for y1, g1, s1 in outs:
+        assert torch.equal(y1, y0) and torch.equal(g1, g0)
+        torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-3)
+    ref = x.cpu().double() @ w.double().t() + res0.cpu().double()
+    torch.testing.assert_close(y0.double(), ref, rtol=5e-5, atol=5e-5)
+    torch.testing.assert_close(s0.double(), (ref ** 2).sum(1), rtol=1e-4, atol=1e-2)
