@@ -891,7 +891,9 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
 
 // in-launch split-K merge: 0 off, 1 every eligible split, 2 (default) splits of small weights only -- measured
 // (profiles/r02t_*): the TTS down (8.7 MB) 184.8 -> 181.5 us per AR step, the Qwen2 down (136 MB) slower
-// (LLM stage 3313 -> 3340 us: every one of its 224 workgroups drains write-through partials before exiting).
+// (LLM stage 3313 -> 3340 us: every one of its 224 workgroups drains write-through partials before exiting),
+// and so were the speech encoder's 32-row FFN-down LayerNorm producers (encoder stage 1594 -> 1624 us), which
+// keep the reduce launch.
 // -1 = FO_GEMM_MERGE (0-2) decides at first use.
 int g_merge = -1;
 inline int merge_mode() {
@@ -1164,7 +1166,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   // one-row-tile plain splits merge inside the launch (last split to arrive sums and finishes; tickets in
   // the caller's zeroed counters, left zeroed); otherwise k_gemm_reduce follows
   const bool small_w = (long long)a.ntiles * 16 * K < (32ll << 20);
-  const bool merged = S > 1 && counters && RB == 1 && !swiglu && !lnw && !mid &&
+  const bool merged = S > 1 && counters && RB == 1 && !a.sout1 && !swiglu && !lnw && !mid &&
                       (merge_mode() == 1 || (merge_mode() == 2 && small_w));
   a.counters = merged ? counters : nullptr;
   if (merged) FO_REQUIRE((long long)groups * mt <= (1 << 20), "fo_gemm: too many tiles for the merge tickets");
@@ -1266,11 +1268,11 @@ int fo_gemm_ln(const float* X, int ldx, int M, int K, const void* Wp, int N, con
 }
 
 int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,
-                     float* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int splitk,
-                     float* rsum, float* rsumsq, int* sgroups, hipStream_t stream) {
+                     float* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int* counters,
+                     int splitk, float* rsum, float* rsumsq, int* sgroups, hipStream_t stream) {
   FO_REQUIRE(rsum && rsumsq, "fo_gemm_rowstats: statistics buffers required");
   return gemm_impl(X, x_f32, ldx, M, K, Wp, N, 0, bias, nullptr, nullptr, Y, ldy, 0, act, residual, ws, ws_floats,
-                   nullptr, splitk, nullptr, 0, 0.f, rsumsq, nullptr, nullptr, sgroups, nullptr, stream, nullptr,
+                   counters, splitk, nullptr, 0, 0.f, rsumsq, nullptr, nullptr, sgroups, nullptr, stream, nullptr,
                    nullptr, 0.f, rsum, nullptr);
 }
 

@@ -72,7 +72,7 @@ _SIGS = {
     "fo_gemm_ln": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_int, c_vp,
                            c_int, c_int, c_vp, c_ll, c_int, c_vp]),
     "fo_gemm_rowstats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp,
-                                 c_ll, c_int, c_vp, c_vp, ctypes.POINTER(c_int), c_vp]),
+                                 c_ll, c_vp, c_int, c_vp, c_vp, ctypes.POINTER(c_int), c_vp]),
     "fo_gemm_qkv_rope": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_ll, c_vp, c_int, c_vp,
                                  c_int, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                  c_vp]),

@@ -176,8 +176,8 @@ class PackedLinear:
         sg = ctypes.c_int(0)
         _lib.call("fo_gemm_rowstats", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
                   self.packed.data_ptr(), self.N, ptr(self.bias), out.data_ptr(), out.stride(0), ACT[act],
-                  1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), splitk, stats.buf1.data_ptr(),
-                  stats.buf.data_ptr(), ctypes.byref(sg), stream(x.device))
+                  1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
+                  stats.buf1.data_ptr(), stats.buf.data_ptr(), ctypes.byref(sg), stream(x.device))
         if sg.value > stats.max_groups:
             raise RuntimeError(f"RowStats holds {stats.max_groups} groups per row, GEMM wrote {sg.value}")
         stats.groups = sg.value

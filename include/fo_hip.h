@@ -73,8 +73,8 @@ int fo_gemm_ln(const float* X, int ldx, int M, int K, const void* Wp, int N, con
 /* fo_gemm (fp32 Y) that also writes per-row partial sums of Y and Y^2 per workgroup column group
  * (*sgroups of them) for a following fo_gemm_ln (the residual-stream producers of an encoder block). */
 int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void* Wp, int N, const float* bias,
-                     float* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int splitk,
-                     float* rsum, float* rsumsq, int* sgroups, hipStream_t stream);
+                     float* Y, int ldy, int act, int residual, float* ws, long long ws_floats, int* counters,
+                     int splitk, float* rsum, float* rsumsq, int* sgroups, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
 /* X-stationary persistent weight stream (k_gemm_xs) for the M <= 16 fp32-X GEMMs with K = 3584 (Qwen2 q|k|v,
