@@ -479,9 +479,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # FO_DIST_REHEARSAL=1: the N > 1 path (receive-only replicas, weight broadcast, result gathering) with
+    # every rank on cuda:0 over gloo -- a one-GPU rehearsal of what the 8-GPU run does over RCCL
+    rehearsal = os.environ.get("FO_DIST_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from fo.engine import FreezeOmniEngine
@@ -493,6 +501,7 @@ def main():
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     bcast_s = bcast_bytes = None
+    weights_verified = None
     if dist is not None:
         # frozen-weight broadcast from rank 0 over RCCL/xGMI (timed separately, excluded from RTF)
         torch.cuda.synchronize()
@@ -502,6 +511,14 @@ def main():
         bcast_n, bcast_bytes = broadcast_frozen(eng, dist)
         torch.cuda.synchronize()
         bcast_s = time.perf_counter() - tb
+        # every replica now holds rank 0's weights, bit for bit (checksums gathered; a mismatch aborts the run)
+        from fo.replica import frozen_checksum
+        ck = torch.tensor([frozen_checksum(eng)], dtype=torch.int64, device=dev)
+        cks = [torch.zeros_like(ck) for _ in range(world)]
+        dist.all_gather(cks, ck)
+        if len({int(c.item()) for c in cks}) != 1:
+            raise RuntimeError(f"frozen weights differ across replicas after the broadcast: {[int(c) for c in cks]}")
+        weights_verified = True
 
     if args.scenario == "duplex":
         main_duplex(args, eng, dev, dist, world, rank, load_s)
@@ -591,7 +608,7 @@ def main():
             "p50_first_emit_gated_ms": round(float(np.percentile(lat_gated, 50)), 2) if lat_gated else None,
             "rtf_per_user_p50": round(float(np.percentile(rtf_user, 50)), 3) if rtf_user else None,
             "load_s": round(load_s, 2), "weight_broadcast_s": None if bcast_s is None else round(bcast_s, 3),
-            "weight_broadcast_bytes": bcast_bytes,
+            "weight_broadcast_bytes": bcast_bytes, "weights_verified": weights_verified,
             "roofline": {"bound": "hbm", "achieved": round(probe["gbps"], 1), "peak": peak, "unit": "GB/s",
                          "frac": round(probe["gbps"] / peak, 4),
                          "traffic": None if traffic is None else round(traffic),

@@ -70,3 +70,16 @@ def broadcast_frozen(root, dist, src=0, bucket_bytes=256 << 20):
                 total += size
             bucket, size = ([t], t.numel() * esz) if t is not None else ([], 0)
     return len(tens), total
+
+
+def frozen_checksum(root):
+    """Order-independent integer checksum of every frozen tensor's bytes (int64 sum of the raw 32-bit words of
+    each tensor, mixed with its index): equal on every rank iff the broadcast delivered rank 0's weights."""
+    acc = 0
+    for i, t in enumerate(t for t in frozen_tensors(root) if t.is_contiguous()):
+        b = t.reshape(-1).view(torch.uint8)
+        n4 = b.numel() // 4 * 4
+        w = b[:n4].view(torch.int32).to(torch.int64).sum().item() if n4 else 0
+        tail = int(b[n4:].to(torch.int64).sum().item()) if b.numel() > n4 else 0
+        acc = (acc * 1000003 + w + tail + i) & ((1 << 63) - 1)
+    return acc

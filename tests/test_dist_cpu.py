@@ -49,6 +49,8 @@ def _worker(rank, world, port, q):
         n, nbytes = broadcast_frozen(m, dist, bucket_bytes=3000)   # small buckets: exercise splitting
         ref = _Model(0)
         same = all(torch.equal(a, b) for a, b in zip(frozen_tensors(m), frozen_tensors(ref)))
+        from fo.replica import frozen_checksum
+        same = same and frozen_checksum(m) == frozen_checksum(ref) != frozen_checksum(_Model(1))
         q.put((rank, got, n, nbytes, same, float(m.pool.k[0]), m.alias.data_ptr() == m.layers[0].packed.data_ptr()))
     finally:
         dist.destroy_process_group()
