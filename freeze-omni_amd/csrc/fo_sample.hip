@@ -30,7 +30,9 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
     const float x = v[i];
     bool skip = (i == ban);
     for (int q = 0; q < ntaken; ++q) skip |= (taken[q] == i);
-    if (!skip && (x > best || (x == best && i < besti))) {
+    // besti == INT_MAX: the first candidate is taken whatever its value, so NaN / -inf rows still give an
+    // index inside [0, n) (the caller gathers an embedding row with it)
+    if (!skip && (x > best || (x == best && i < besti) || besti == 0x7fffffff)) {
       best = x;
       besti = i;
     }
@@ -42,7 +44,8 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
     if (threadIdx.x < o) {
       const float v2 = bv[threadIdx.x + o];
       const int i2 = bi[threadIdx.x + o];
-      if (v2 > bv[threadIdx.x] || (v2 == bv[threadIdx.x] && i2 < bi[threadIdx.x])) {
+      if (i2 != 0x7fffffff &&
+          (v2 > bv[threadIdx.x] || (v2 == bv[threadIdx.x] && i2 < bi[threadIdx.x]) || bi[threadIdx.x] == 0x7fffffff)) {
         bv[threadIdx.x] = v2;
         bi[threadIdx.x] = i2;
       }
@@ -479,7 +482,8 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
     }
   } else {
     float mv;
-    const int pick = sample_row_general(lg, V, k, T, tp, ban_id, u01, probs, &mv, sm);
+    int pick = sample_row_general(lg, V, k, T, tp, ban_id, u01, probs, &mv, sm);
+    if ((unsigned)pick >= (unsigned)V) pick = 0;  // never an out-of-table id (NaN rows)
     if (threadIdx.x == 0) {
       out_ids[row] = pick;
       if (out_val) out_val[row] = mv;
@@ -489,7 +493,8 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
   }
   if constexpr (NEXT) {
     __syncthreads();
-    const int id = sm.si[0];
+    // an id outside the table (a NaN row through the general path) must never address memory: row 0
+    const int id = (unsigned)sm.si[0] < (unsigned)V ? sm.si[0] : 0;
     if (threadIdx.x == 0 && nx.hist) nx.hist[(size_t)nx.hist_row[0] * nx.hist_ld + row] = id;
     const bf16_t* er = nx.emb + (size_t)id * nx.emb_ld;
     float* xr = nx.x + (size_t)row * nx.ldx;

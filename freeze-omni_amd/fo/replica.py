@@ -44,9 +44,23 @@ def frozen_tensors(root):
     return out
 
 
+def frozen_storages(root):
+    """A byte view over the WHOLE storage of every frozen tensor, one per storage, in walk order.  Broadcasting
+    storages rather than tensors covers views at an offset, non-contiguous views and a smaller view that
+    shares its first byte with a larger tensor (frozen_tensors keeps one tensor per data pointer)."""
+    out, seen = [], set()
+    for t in frozen_tensors(root):
+        st = t.untyped_storage()
+        if st.data_ptr() in seen or st.nbytes() == 0:
+            continue
+        seen.add(st.data_ptr())
+        out.append(torch.empty(0, dtype=torch.uint8, device=t.device).set_(st))
+    return out
+
+
 def broadcast_frozen(root, dist, src=0, bucket_bytes=256 << 20):
-    """Broadcast every frozen tensor of `root` from rank `src`.  Returns (n_tensors, n_bytes)."""
-    tens = [t for t in frozen_tensors(root) if t.is_contiguous()]
+    """Broadcast every frozen storage of `root` from rank `src`.  Returns (n_storages, n_bytes)."""
+    tens = frozen_storages(root)
     by_dtype = {}
     for t in tens:
         by_dtype.setdefault(t.dtype, []).append(t)
@@ -73,11 +87,10 @@ def broadcast_frozen(root, dist, src=0, bucket_bytes=256 << 20):
 
 
 def frozen_checksum(root):
-    """Order-independent integer checksum of every frozen tensor's bytes (int64 sum of the raw 32-bit words of
-    each tensor, mixed with its index): equal on every rank iff the broadcast delivered rank 0's weights."""
+    """Integer checksum of every frozen storage's bytes (int64 sum of its raw 32-bit words, mixed in walk
+    order): equal on every rank when the broadcast delivered rank 0's weights."""
     acc = 0
-    for i, t in enumerate(t for t in frozen_tensors(root) if t.is_contiguous()):
-        b = t.reshape(-1).view(torch.uint8)
+    for i, b in enumerate(frozen_storages(root)):
         n4 = b.numel() // 4 * 4
         w = b[:n4].view(torch.int32).to(torch.int64).sum().item() if n4 else 0
         tail = int(b[n4:].to(torch.int64).sum().item()) if b.numel() > n4 else 0
