@@ -35,10 +35,15 @@ def frozen_tensors(root):
         elif isinstance(o, (list, tuple)):
             for v in o:
                 walk(v)
-        elif hasattr(o, "__dict__") and type(o).__module__.split(".")[0] not in _FOREIGN:
-            for k in sorted(vars(o)):
-                if k not in _SKIP_ATTRS:
-                    walk(vars(o)[k])
+        elif type(o).__module__.split(".")[0] not in _FOREIGN:
+            # instance dict AND __slots__ (fo.stack.Layer is slotted: its weights live only in slots)
+            names = set(vars(o)) if hasattr(o, "__dict__") else set()
+            for c in type(o).__mro__:
+                sl = getattr(c, "__slots__", ())
+                names.update((sl,) if isinstance(sl, str) else sl)
+            for k in sorted(names):
+                if k not in _SKIP_ATTRS and k not in ("__dict__", "__weakref__") and hasattr(o, k):
+                    walk(getattr(o, k))
 
     walk(root)
     return out

@@ -25,11 +25,21 @@ class _Lin:
         self.bias = torch.randn(17, generator=g) * scale
 
 
+class _Slot:
+    __slots__ = ("w", "b")   # like fo.stack.Layer: the weights live only in slots
+
+    def __init__(self, g):
+        self.w = torch.randn(64, generator=g)
+        self.b = torch.randn(8, generator=g)
+
+
 class _Model:
     def __init__(self, rank):
         g = torch.Generator().manual_seed(7 if rank == 0 else 100 + rank)
         self.layers = [_Lin(g, 1.0) for _ in range(5)]
         self.table = torch.randn(300, 4, generator=g)
+        self.row = self.table[10:20]                 # a view at an offset: covered by the table's storage
+        self.slotted = _Slot(g)
         self.alias = self.layers[0].packed          # shared storage is sent once
         self.pool = type("KVPool", (), {})()         # per-session state: never broadcast
         self.pool.k = torch.full((8,), float(rank))
@@ -69,7 +79,7 @@ def test_gloo_world2_gather_and_weight_broadcast():
         assert p.exitcode == 0
     for rank, got, n, nbytes, same, kv0, alias in res:
         assert got == [0.0, 10.0, 11.0]
-        assert n == 11 and nbytes == 5 * (1000 * 2 + 17 * 4) + 300 * 4 * 4
+        assert n == 13 and nbytes == 5 * (1000 * 2 + 17 * 4) + 300 * 4 * 4 + (64 + 8) * 4
         assert same and alias
         assert kv0 == float(rank)
 
