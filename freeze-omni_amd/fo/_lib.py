@@ -79,6 +79,7 @@ _SIGS = {
     "fo_fill_hash": (c_int, [c_vp, c_int, c_ll, ctypes.c_ulonglong, c_float, c_float, c_vp]),
     "fo_rmsnorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
     "fo_layernorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
+    "fo_decode_meta_advance": (c_int, [c_vp, c_int, c_int, c_int, c_vp]),
     "fo_gather_rows": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "fo_im2col_3x3s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
                                 c_vp]),

@@ -553,6 +553,13 @@ def penalty(logits, V, ids, win, step, penalty, B=None):
     return logits
 
 
+def decode_meta_advance(meta, B, maxb, PS):
+    """The captured decode step's metadata block advanced to the next step on the device (fo_decode_meta_advance)."""
+    if meta.dtype != I32 or not meta.is_contiguous() or meta.numel() < 5 * B + 1 + B * maxb:
+        raise ValueError("decode_meta_advance: int32 contiguous block of 5B + 1 + B*maxb entries required")
+    _lib.call("fo_decode_meta_advance", meta.data_ptr(), B, maxb, PS, stream(meta.device))
+
+
 def sample_embed(logits, V, out_ids, emb, x, gamma, eps, h, top_k=None, temperature=None, top_p=None, seed=0,
                  step=None, B=None, ban_id=-1, key=None, hist_ptr=None, hist_row=None, hist_ld=0):
     """sample(), then the next decode step's input from the drawn ids: x[b] = emb[id_b] (fp32), h[b] =

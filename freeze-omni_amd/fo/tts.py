@@ -208,10 +208,15 @@ class DecodeGraph:
     """
 
     RING = 64
+    AHEAD = 128   # KV positions reserved ahead of the decode, so a session's page list changes every ~7 pages
 
     def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None, capture=True):
         dev = tts.device
         self.pen = pen
+        # the captured step advances its own metadata for the next step (fo_decode_meta_advance); the host
+        # uploads a fresh block only when the batch, its RNG keys or a session's page list changed
+        self.advance = capture and not tts.fused
+        self._uploaded = None
         self.win = torch.full((B, pen[0]), -1, dtype=I32, device=dev) if pen else None
         PS = tts.pool.PS
         self.tts, self.B, self.V_sample, self.seed = tts, B, V_sample, seed
@@ -257,13 +262,17 @@ class DecodeGraph:
         ops.sample_embed(self.logits, self.V_sample, self.ids, t.embedding, self.x, t.main.layers[0].ln1, t.eps,
                          self.ws["h"], top_k=self.topk, seed=self.seed, step=self.meta.step, B=self.B,
                          key=self.meta.key, hist_ptr=self.hist.dev, hist_row=self.meta.hist_row, hist_ld=self.B)
+        if self.advance:
+            ops.decode_meta_advance(self.meta_d, self.B, self.maxb, t.pool.PS)
 
     def prime(self):
         """Input rows of the next replay from self.ids (first step of a batch, or after the batch changed)."""
+        self._uploaded = None
         self.tts.embed_input(self.ids, self.ws, self.B, x=self.x)
 
     def adopt(self, other):
         """Continue another graph's batch (same sessions, other sampler bound): take its ids and input rows."""
+        self._uploaded = None
         self.ids.copy_(other.ids)
         if self.pen:
             self.win.copy_(other.win)
@@ -294,30 +303,43 @@ class DecodeGraph:
             self.win.copy_(torch.tensor(rings, dtype=I32).to(self.win.device))
 
     def set_ids(self, ids_dev):
+        self._uploaded = None
         self.ids.copy_(ids_dev[:self.B])
 
     def launch(self, seqs, keys, step, slot):
         """Replay one step for seqs (len B, batch order) with RNG stream ids `keys` at step `step`,
         history row `slot`; appends one KV position to every sequence.  Returns the step's event."""
-        B, maxb = self.B, self.maxb
-        h = self.host_np[slot % self.RING]
-        h[4 * B:5 * B] = keys
-        h[5 * B] = slot
-        bt = h[5 * B + 1:].reshape(B, maxb)
-        for b, s in enumerate(seqs):
+        B, maxb, PS = self.B, self.maxb, self.tts.pool.PS
+        for s in seqs:
             kv = s.kv
             L = kv.length
+            if len(kv.pages) * PS < L + 1 + 16:   # reserve a run of pages ahead (bounded by the block table)
+                kv.reserve(min(L + 1 + self.AHEAD, maxb * PS))
             kv.reserve(L + 1)
             if len(kv.pages) > maxb:
                 raise RuntimeError("decode graph block table too small")
-            h[b] = L - s.P
-            h[B + b] = kv.slot(L)
-            h[2 * B + b] = L + 1
-            h[3 * B + b] = step
-            bt[b, :len(kv.pages)] = kv.pages
-            kv.length = L + 1
+        sig = (tuple(id(s) for s in seqs), tuple(int(k) for k in keys), tuple(len(s.kv.pages) for s in seqs))
+        up = self._uploaded
+        if not (self.advance and up is not None and up[0] == sig and step == up[1] + 1 and slot == up[2] + 1):
+            # the device-advanced block is not this step's: upload it from the host
+            h = self.host_np[slot % self.RING]
+            h[4 * B:5 * B] = keys
+            h[5 * B] = slot
+            bt = h[5 * B + 1:].reshape(B, maxb)
+            for b, s in enumerate(seqs):
+                kv = s.kv
+                L = kv.length
+                h[b] = L - s.P
+                h[B + b] = kv.slot(L)
+                h[2 * B + b] = L + 1
+                h[3 * B + b] = step
+                bt[b, :len(kv.pages)] = kv.pages
+                bt[b, len(kv.pages):] = kv.pages[-1]   # defensive: never a foreign page past the list
+            self.meta_d.copy_(self.host[slot % self.RING], non_blocking=True)
+        self._uploaded = (sig, step, slot)
+        for s in seqs:
+            s.kv.length += 1
             s.generated += 1
-        self.meta_d.copy_(self.host[slot % self.RING], non_blocking=True)
         st = ops.stream(self.tts.device)
         if self.exec is None:
             self._body()

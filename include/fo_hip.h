@@ -123,6 +123,11 @@ int fo_rmsnorm(const float* x, int ldx, int M, int D, const float* w, float eps,
 int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const float* b, float eps, float* out, int ldo,
                  int act, hipStream_t s);
 /* embedding / row gather (wte at models/audioLLM.py:303,330; decoder embedding decoder.py:318,336) */
+/* The captured AR decode step's metadata advanced to the next step on the device (replaces the per-step
+ * host upload of positions / slots / visible keys, models/decoder/decoder.py:337-340): meta = [pos B][slot B]
+ * [nvis B][step B][key B][hist_row 1][block table B x maxb]; pos, nvis, step and hist_row += 1, slot = the
+ * block table's page for the new cache index.  The caller re-uploads the block whenever a page list changed. */
+int fo_decode_meta_advance(int* meta, int B, int maxb, int PS, hipStream_t stream);
 int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,
                    int ldo, const int* out_rows, int round_fp16, hipStream_t s);
 /* Conv2dSubsampling4 front end as im2col (+ fused GlobalCMVN) (models/encoder/subsampling.py:67-73,
