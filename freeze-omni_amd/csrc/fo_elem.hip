@@ -199,24 +199,6 @@ inline int grid_for(long long n, int bs = 256) {
   return (int)g;
 }
 
-// The AR decode step's metadata for the NEXT step, advanced on the device at the end of a captured step
-// (models/decoder/decoder.py:337-340: position = cache length - P grows by one per token): m = [pos B]
-// [slot B][nvis B][step B][key B][hist_row 1][block table B x maxb].  The new token's cache index is this
-// step's nvis; its slot comes from the block table already on the device (the host uploads a fresh block
-// whenever a session's page list changed, so the page is always there).
-__global__ void k_decode_meta_advance(int* m, int B, int maxb, int PS) {
-  const int b = threadIdx.x;
-  if (b < B) {
-    const int L = m[2 * B + b];
-    const int pg = L / PS;
-    m[b] += 1;
-    m[2 * B + b] = L + 1;
-    m[3 * B + b] += 1;
-    m[B + b] = (pg < maxb ? m[5 * B + 1 + b * maxb + pg] : 0) * PS + L % PS;
-  }
-  if (b == 0) m[5 * B] += 1;
-}
-
 }  // namespace
 
 __global__ void k_record_ids(const int* ids, int B, int* dst, int ld, const int* row) {
@@ -247,13 +229,6 @@ int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const fl
   FO_REQUIRE(act == FO_ACT_NONE || act == FO_ACT_RELU || act == FO_ACT_GELU, "fo_layernorm: act %d", act);
   hipLaunchKernelGGL(k_layernorm, dim3(M), dim3(256), 0, s, x, ldx, D, w, b, eps, out, ldo, act);
   return fo::check_launch("fo_layernorm");
-}
-
-int fo_decode_meta_advance(int* meta, int B, int maxb, int PS, hipStream_t s) {
-  FO_REQUIRE(meta && B > 0 && B <= 1024 && maxb > 0 && PS > 0, "fo_decode_meta_advance: bad shape B=%d maxb=%d", B,
-             maxb);
-  hipLaunchKernelGGL(k_decode_meta_advance, dim3(1), dim3(B < 64 ? 64 : (B + 63) / 64 * 64), 0, s, meta, B, maxb, PS);
-  return fo::check_launch("fo_decode_meta_advance");
 }
 
 int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,

@@ -74,6 +74,11 @@ struct NextInput {
   float eps;
   float* h;             // [B][ldh] RMSNorm(x) * gamma
   int ldh;
+  // the captured AR step's metadata block [pos B][slot B][nvis B][step B][key B][hist_row 1][block table B x
+  // maxb] (nullable): this row's entries advance to the next step once the row is drawn (positions,
+  // visible keys, step + 1; the slot from the block table on the device), and the history row is the row's step
+  int* meta;
+  int B, maxb, PS;
 };
 
 struct SampleSmem {
@@ -495,7 +500,19 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
     __syncthreads();
     // an id outside the table (a NaN row through the general path) must never address memory: row 0
     const int id = (unsigned)sm.si[0] < (unsigned)V ? sm.si[0] : 0;
-    if (threadIdx.x == 0 && nx.hist) nx.hist[(size_t)nx.hist_row[0] * nx.hist_ld + row] = id;
+    if (threadIdx.x == 0 && nx.hist) {
+      const int hr = nx.meta ? nx.meta[3 * nx.B + row] : nx.hist_row[0];  // meta: the row's own step (no shared word)
+      nx.hist[(size_t)hr * nx.hist_ld + row] = id;
+    }
+    if (threadIdx.x == 0 && nx.meta) {
+      int* m = nx.meta;
+      const int B = nx.B, L = m[2 * B + row], pg = L / nx.PS;
+      m[row] += 1;
+      m[2 * B + row] = L + 1;
+      m[3 * B + row] += 1;
+      m[B + row] = (pg < nx.maxb ? m[5 * B + 1 + row * nx.maxb + pg] : 0) * nx.PS + L % nx.PS;
+      if (row == 0) m[5 * B] += 1;
+    }
     const bf16_t* er = nx.emb + (size_t)id * nx.emb_ld;
     float* xr = nx.x + (size_t)row * nx.ldx;
     // same per-thread float4 sums and wave order as k_rmsnorm's 256-thread block (threads >= 256 add
@@ -576,11 +593,14 @@ int fo_sample_probs(const float* logits, int ld, int B, int V, const int* top_k,
 int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
                     int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
-                    int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, hipStream_t s) {
+                    int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, int* meta, int maxb,
+                    int PS, hipStream_t s) {
   FO_REQUIRE(B > 0 && V > 0 && D > 0 && (D % 4) == 0 && D <= 4096, "fo_sample_embed: bad shape B=%d V=%d D=%d", B, V, D);
-  FO_REQUIRE(emb && x && gamma && h && (!hist || (hist_row && hist_ld >= B)), "fo_sample_embed: missing buffers");
+  FO_REQUIRE(emb && x && gamma && h && (!hist || ((hist_row || meta) && hist_ld >= B)), "fo_sample_embed: missing buffers");
   FO_REQUIRE((ldx % 4) == 0 && (ldh % 4) == 0, "fo_sample_embed: row strides must be float4-aligned");
-  NextInput nx{hist, hist_row, hist_ld, (const bf16_t*)emb, emb_ld, D, x, ldx, gamma, eps, h, ldh};
+  FO_REQUIRE(!meta || (maxb > 0 && PS > 0 && step == meta + 3 * B && key == meta + 4 * B),
+             "fo_sample_embed: meta must be the decode block whose step / key rows are passed");
+  NextInput nx{hist, hist_row, hist_ld, (const bf16_t*)emb, emb_ld, D, x, ldx, gamma, eps, h, ldh, meta, B, maxb, PS};
   hipLaunchKernelGGL(k_sample<true>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
                      key, ban_id, out_ids, nullptr, nullptr, 0, nx);
   return fo::check_launch("fo_sample_embed");

@@ -79,7 +79,6 @@ _SIGS = {
     "fo_fill_hash": (c_int, [c_vp, c_int, c_ll, ctypes.c_ulonglong, c_float, c_float, c_vp]),
     "fo_rmsnorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
     "fo_layernorm": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_vp]),
-    "fo_decode_meta_advance": (c_int, [c_vp, c_int, c_int, c_int, c_vp]),
     "fo_gather_rows": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "fo_im2col_3x3s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
                                 c_vp]),
@@ -123,7 +122,7 @@ _SIGS = {
                                 c_vp, c_vp, c_int, c_vp]),
     "fo_sample_embed": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int,
                                 c_vp, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp, c_float, c_vp, c_int,
-                                c_vp]),
+                                c_vp, c_int, c_int, c_vp]),
     "fo_gemm_set_pipe": (c_int, [c_int]),
     "fo_conv1d_ex": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                              c_vp, c_int, c_vp]),

@@ -553,21 +553,17 @@ def penalty(logits, V, ids, win, step, penalty, B=None):
     return logits
 
 
-def decode_meta_advance(meta, B, maxb, PS):
-    """The captured decode step's metadata block advanced to the next step on the device (fo_decode_meta_advance)."""
-    if meta.dtype != I32 or not meta.is_contiguous() or meta.numel() < 5 * B + 1 + B * maxb:
-        raise ValueError("decode_meta_advance: int32 contiguous block of 5B + 1 + B*maxb entries required")
-    _lib.call("fo_decode_meta_advance", meta.data_ptr(), B, maxb, PS, stream(meta.device))
-
-
 def sample_embed(logits, V, out_ids, emb, x, gamma, eps, h, top_k=None, temperature=None, top_p=None, seed=0,
-                 step=None, B=None, ban_id=-1, key=None, hist_ptr=None, hist_row=None, hist_ld=0):
+                 step=None, B=None, ban_id=-1, key=None, hist_ptr=None, hist_row=None, hist_ld=0, meta=None, maxb=0,
+                 PS=0):
     """sample(), then the next decode step's input from the drawn ids: x[b] = emb[id_b] (fp32), h[b] =
-    RMSNorm(x[b]) * gamma, and (hist_ptr) hist[hist_row[0] * hist_ld + b] = id_b -- one launch."""
+    RMSNorm(x[b]) * gamma, and (hist_ptr) hist[hist_row[0] * hist_ld + b] = id_b -- one launch.  meta: the
+    captured step's metadata block (step / key are its rows): it advances to the next step in the same launch."""
     B = logits.shape[0] if B is None else B
     _lib.call("fo_sample_embed", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
               int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), hist_ptr,
               ptr(hist_row), hist_ld, emb.data_ptr(), emb.stride(0), emb.shape[1], x.data_ptr(), x.stride(0),
-              gamma.data_ptr(), float(eps), h.data_ptr(), h.stride(0), stream(logits.device))
+              gamma.data_ptr(), float(eps), h.data_ptr(), h.stride(0), ptr(meta), int(maxb), int(PS),
+              stream(logits.device))
     return out_ids
 

@@ -213,7 +213,7 @@ class DecodeGraph:
     def __init__(self, tts, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None, capture=True):
         dev = tts.device
         self.pen = pen
-        # the captured step advances its own metadata for the next step (fo_decode_meta_advance); the host
+        # the captured step advances its own metadata for the next step (inside the sampler launch); the host
         # uploads a fresh block only when the batch, its RNG keys or a session's page list changed
         self.advance = capture and not tts.fused
         self._uploaded = None
@@ -261,9 +261,8 @@ class DecodeGraph:
             ops.penalty(self.logits, t.vocab + 4, self.ids, self.win, self.meta.step, self.pen[1], B=self.B)
         ops.sample_embed(self.logits, self.V_sample, self.ids, t.embedding, self.x, t.main.layers[0].ln1, t.eps,
                          self.ws["h"], top_k=self.topk, seed=self.seed, step=self.meta.step, B=self.B,
-                         key=self.meta.key, hist_ptr=self.hist.dev, hist_row=self.meta.hist_row, hist_ld=self.B)
-        if self.advance:
-            ops.decode_meta_advance(self.meta_d, self.B, self.maxb, t.pool.PS)
+                         key=self.meta.key, hist_ptr=self.hist.dev, hist_row=self.meta.hist_row, hist_ld=self.B,
+                         **(dict(meta=self.meta_d, maxb=self.maxb, PS=t.pool.PS) if self.advance else {}))
 
     def prime(self):
         """Input rows of the next replay from self.ids (first step of a batch, or after the batch changed)."""
@@ -318,6 +317,8 @@ class DecodeGraph:
             kv.reserve(L + 1)
             if len(kv.pages) > maxb:
                 raise RuntimeError("decode graph block table too small")
+        if self.advance and slot != step:
+            raise ValueError("decode graph: the history row is the step when the step advances its own metadata")
         sig = (tuple(id(s) for s in seqs), tuple(int(k) for k in keys), tuple(len(s.kv.pages) for s in seqs))
         up = self._uploaded
         if not (self.advance and up is not None and up[0] == sig and step == up[1] + 1 and slot == up[2] + 1):

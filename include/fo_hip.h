@@ -123,11 +123,6 @@ int fo_rmsnorm(const float* x, int ldx, int M, int D, const float* w, float eps,
 int fo_layernorm(const float* x, int ldx, int M, int D, const float* w, const float* b, float eps, float* out, int ldo,
                  int act, hipStream_t s);
 /* embedding / row gather (wte at models/audioLLM.py:303,330; decoder embedding decoder.py:318,336) */
-/* The captured AR decode step's metadata advanced to the next step on the device (replaces the per-step
- * host upload of positions / slots / visible keys, models/decoder/decoder.py:337-340): meta = [pos B][slot B]
- * [nvis B][step B][key B][hist_row 1][block table B x maxb]; pos, nvis, step and hist_row += 1, slot = the
- * block table's page for the new cache index.  The caller re-uploads the block whenever a page list changed. */
-int fo_decode_meta_advance(int* meta, int B, int maxb, int PS, hipStream_t stream);
 int fo_gather_rows(const void* table, int table_bf16, long long ld_tab, const int* idx, int M, int D, float* out,
                    int ldo, const int* out_rows, int round_fp16, hipStream_t s);
 /* Conv2dSubsampling4 front end as im2col (+ fused GlobalCMVN) (models/encoder/subsampling.py:67-73,
@@ -250,11 +245,14 @@ int fo_sample_probs(const float* logits, int ld, int B, int V, const int* top_k,
                     int* out_ids, float* probs, int ldp, hipStream_t s);
 /* fo_sample fused with the next AR decode step's input (models/decoder/decoder.py:341-346: embed(id) ->
  * first LlamaRMSNorm): hist[hist_row[0] * hist_ld + row] = id (hist nullable), x[row] = emb[id] (bf16
- * table -> fp32), h[row] = RMSNorm(x[row]) * gamma. */
+ * table -> fp32), h[row] = RMSNorm(x[row]) * gamma.  meta (nullable): the captured step's metadata block
+ * ([pos B][slot B][nvis B][step B][key B][hist_row 1][block table B x maxb]; step / key point into it): the history row is then each row's step,
+ * and each row's entries advance to the next step inside this launch (no separate advance launch). */
 int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
                     int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
-                    int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, hipStream_t s);
+                    int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, int* meta, int maxb,
+                    int PS, hipStream_t s);
 /* Repetition penalty of the AR decode loop (models/decoder/decoder.py:348-351), applied before the
  * draw: win[row][step[row] % W] = ids[row], then logits[row][t] /= penalty for every entry t of the
  * last min(step+1, W) ids -- once per occurrence, as the reference's set() of 0-d tensors does. */
