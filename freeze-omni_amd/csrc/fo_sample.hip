@@ -21,22 +21,44 @@ __device__ __forceinline__ uint64_t smix(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-// block arg-max over v[0..n) excluding indices already in `taken`; ties -> smallest index
+constexpr int NOIDX = 0x7fffffff;
+
+// arg-max order: does candidate (v2, i2) replace (v1, i1)?  Larger value, ties -> smaller index; any
+// candidate replaces "none yet" (i1 == NOIDX), so a row of NaN / -inf still yields an index inside the
+// table (the caller gathers an embedding row with it); a NaN never replaces a number and a number always
+// replaces a NaN, so one NaN does not win over the real maximum of the rest of the row.
+__device__ __forceinline__ bool amax_better(float v2, int i2, float v1, int i1) {
+  if (i2 == NOIDX) return false;
+  if (i1 == NOIDX) return true;
+  if (v2 != v2) return false;
+  if (v1 != v1) return true;
+  return v2 > v1 || (v2 == v1 && i2 < i1);
+}
+
+// logits the reference cannot sample from: torch.multinomial raises on the NaN probabilities a NaN or +inf
+// logit (or a row of -inf) gives after the softmax (models/audioLLM.py:455-476, models/decoder/decoder.py:355-359)
+__device__ __forceinline__ bool bad_logit(float x) { return x != x || x == INFINITY; }
+
+// block arg-max over v[0..n) excluding indices already in `taken`; ties -> smallest index.
+// *bad (nullable): set when the scanned values hold a NaN or +inf (block-uniform result).
 __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken, int ban, float* bv, int* bi,
-                             float& mval, int& midx) {
+                             float& mval, int& midx, int* bad = nullptr) {
   float best = -INFINITY;
-  int besti = 0x7fffffff;
+  int besti = NOIDX;
+  int b = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const float x = v[i];
     bool skip = (i == ban);
     for (int q = 0; q < ntaken; ++q) skip |= (taken[q] == i);
-    // besti == INT_MAX: the first candidate is taken whatever its value, so NaN / -inf rows still give an
-    // index inside [0, n) (the caller gathers an embedding row with it)
-    if (!skip && (x > best || (x == best && i < besti) || besti == 0x7fffffff)) {
-      best = x;
-      besti = i;
+    if (!skip) {
+      b |= bad_logit(x);
+      if (amax_better(x, i, best, besti)) {
+        best = x;
+        besti = i;
+      }
     }
   }
+  if (bad) *bad = __syncthreads_or(b);
   bv[threadIdx.x] = best;
   bi[threadIdx.x] = besti;
   __syncthreads();
@@ -44,8 +66,7 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
     if (threadIdx.x < o) {
       const float v2 = bv[threadIdx.x + o];
       const int i2 = bi[threadIdx.x + o];
-      if (i2 != 0x7fffffff &&
-          (v2 > bv[threadIdx.x] || (v2 == bv[threadIdx.x] && i2 < bi[threadIdx.x]) || bi[threadIdx.x] == 0x7fffffff)) {
+      if (amax_better(v2, i2, bv[threadIdx.x], bi[threadIdx.x])) {
         bv[threadIdx.x] = v2;
         bi[threadIdx.x] = i2;
       }
@@ -55,6 +76,64 @@ __device__ void block_argmax(const float* v, int n, const int* taken, int ntaken
   mval = bv[0];
   midx = bi[0];
   __syncthreads();
+}
+
+// First pass of the split arg-max (fo_sample with a workspace, top_k == 1 rows over a large vocabulary:
+// the text decoder's 152,064-wide lm_head rows): workgroup (c, row) reduces chunk c of the row to
+// (max, index, bad) so the row is read by ~75 workgroups at HBM rate instead of by one.
+constexpr int AMAX_CH = 2048;  // logits per chunk (256 threads x 8)
+struct AmaxPart {
+  float v;
+  int i;
+  int bad;
+  int pad;
+};
+__global__ __launch_bounds__(256) void k_argmax_part(const float* logits, int ld, int V, int ban, AmaxPart* parts,
+                                                     int nc) {
+  __shared__ float sv[256];
+  __shared__ int si[256];
+  const int c = blockIdx.x, row = blockIdx.y;
+  const float* lg = logits + (size_t)row * ld;
+  const int i0 = c * AMAX_CH + threadIdx.x * 8;
+  float best = -INFINITY;
+  int besti = NOIDX, b = 0;
+  if (i0 + 8 <= V && (ld & 3) == 0) {
+    const float4 p0 = reinterpret_cast<const float4*>(lg + i0)[0];
+    const float4 p1 = reinterpret_cast<const float4*>(lg + i0)[1];
+    const float f[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j != ban) {
+        b |= bad_logit(f[j]);
+        if (amax_better(f[j], i0 + j, best, besti)) {
+          best = f[j];
+          besti = i0 + j;
+        }
+      }
+  } else {
+    for (int j = 0; j < 8; ++j) {
+      const int i = i0 + j;
+      if (i >= V || i == ban) continue;
+      const float x = lg[i];
+      b |= bad_logit(x);
+      if (amax_better(x, i, best, besti)) {
+        best = x;
+        besti = i;
+      }
+    }
+  }
+  b = __syncthreads_or(b);
+  sv[threadIdx.x] = best;
+  si[threadIdx.x] = besti;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o && amax_better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
+      sv[threadIdx.x] = sv[threadIdx.x + o];
+      si[threadIdx.x] = si[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[(size_t)row * nc + c] = AmaxPart{sv[0], si[0], b, 0};
 }
 
 // The next decode step's input, produced by the sampler itself (AR speech decoder step,
@@ -209,18 +288,22 @@ __device__ int block_exscan1024_int(int v, SampleSmem& sm, int* total) {
 // Returns the drawn id; writes the kept-set distribution e_i / Z (the reference's pre-multinomial
 // `probs`) to probs when non-null.
 __device__ int sample_row_general(const float* lg, int V, int k, float T, float tp, int ban, float u01,
-                                  float* probs, float* max_out, SampleSmem& sm) {
+                                  float* probs, float* max_out, int* bad_out, SampleSmem& sm) {
   const int tid = threadIdx.x;
   const float invT = 1.f / T;
   float m = -INFINITY;
-  int nallowed = 0;
+  int nallowed = 0, bad = 0;
   for (int i = tid; i < V; i += 1024)
     if (i != ban) {
-      m = fmaxf(m, lg[i]);
+      const float x = lg[i];
+      bad |= bad_logit(x);
+      m = fmaxf(m, x);
       ++nallowed;
     }
+  bad = __syncthreads_or(bad);
   m = block_max1024(m, sm);
   *max_out = m;
+  *bad_out = bad || !(m > -INFINITY);
   {
     int total;
     block_exscan1024_int(nallowed, sm, &total);
@@ -410,7 +493,7 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
                                                  const float* temp_rows, const float* top_p_rows,
                                                  unsigned long long seed, const int* step_rows, const int* key_rows, int ban_id,
                                                  int* out_ids, float* out_val, float* out_probs, int ldp,
-                                                 NextInput nx) {
+                                                 NextInput nx, const AmaxPart* parts, int nc, int* err) {
   __shared__ SampleSmem sm;
   const int row = blockIdx.x;
   const float* lg = logits + (size_t)row * ld;
@@ -422,14 +505,50 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
   const uint64_t key = key_rows ? (uint64_t)key_rows[row] : (uint64_t)row;  // stream id: session, not batch row
   const float u01 = (float)(uint32_t)(smix(seed ^ (0x9E37ull * (key + 1)) + st) >> 40) * (1.0f / 16777216.0f);
   const int allowed = V - ((ban_id >= 0 && ban_id < V) ? 1 : 0);
-  if (k >= 1 && k <= KMAXS && k < allowed) {
+  int bad = 0;
+  if (parts && k == 1 && !probs) {
+    // arg-max from the split first pass (k_argmax_part): reduce the row's nc chunk results
+    float best = -INFINITY;
+    int besti = NOIDX, b = 0;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+      const AmaxPart p = parts[(size_t)row * nc + c];
+      b |= p.bad;
+      if (amax_better(p.v, p.i, best, besti)) {
+        best = p.v;
+        besti = p.i;
+      }
+    }
+    bad = __syncthreads_or(b);
+    sm.bv[threadIdx.x] = best;
+    sm.bi[threadIdx.x] = besti;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if (threadIdx.x < o && amax_better(sm.bv[threadIdx.x + o], sm.bi[threadIdx.x + o], sm.bv[threadIdx.x],
+                                         sm.bi[threadIdx.x])) {
+        sm.bv[threadIdx.x] = sm.bv[threadIdx.x + o];
+        sm.bi[threadIdx.x] = sm.bi[threadIdx.x + o];
+      }
+      __syncthreads();
+    }
+    const float mv = sm.bv[0];
+    const int pick = (unsigned)sm.bi[0] < (unsigned)V ? sm.bi[0] : 0;
+    bad = bad || !(mv > -INFINITY);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      out_ids[row] = pick;
+      if (out_val) out_val[row] = mv;
+      sm.si[0] = pick;
+    }
+    __syncthreads();
+  } else if (k >= 1 && k <= KMAXS && k < allowed) {
     // small top-k: k block arg-max passes, then the top-p / draw over the (sorted) k candidates
     for (int q = 0; q < k; ++q) {
       float mv;
       int i;
-      block_argmax(lg, V, sm.taken, q, ban_id, sm.bv, sm.bi, mv, i);
+      block_argmax(lg, V, sm.taken, q, ban_id, sm.bv, sm.bi, mv, i, q == 0 ? &bad : nullptr);
+      if (q == 0) bad = bad || !(mv > -INFINITY);
       if (threadIdx.x == 0) {
-        sm.taken[q] = i;
+        sm.taken[q] = (unsigned)i < (unsigned)V ? i : 0;
         sm.tv[q] = mv;
       }
       __syncthreads();
@@ -487,7 +606,7 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
     }
   } else {
     float mv;
-    int pick = sample_row_general(lg, V, k, T, tp, ban_id, u01, probs, &mv, sm);
+    int pick = sample_row_general(lg, V, k, T, tp, ban_id, u01, probs, &mv, &bad, sm);
     if ((unsigned)pick >= (unsigned)V) pick = 0;  // never an out-of-table id (NaN rows)
     if (threadIdx.x == 0) {
       out_ids[row] = pick;
@@ -496,6 +615,9 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
     }
     __syncthreads();
   }
+  // a row the reference could not sample from: flag it for the host (which raises, as torch.multinomial
+  // does); the id above is still a valid table index, so nothing downstream addresses outside memory
+  if (bad && err && threadIdx.x == 0) *err = 1;
   if constexpr (NEXT) {
     __syncthreads();
     // an id outside the table (a NaN row through the general path) must never address memory: row 0
@@ -566,13 +688,31 @@ extern "C" {
 
 // logits [B][ld] fp32.  top_k/temp/top_p/step are per-row device arrays (nullable: k=1, T=1, p=0, step 0).
 // ban_id >= 0 excludes one token (benchmark policy: EOS masked until a fixed response length).
+// err (nullable): set to 1 (never cleared here) when a row cannot be sampled by the reference's rule.
+// ws (nullable, >= fo_sample_ws_floats(B, V) floats): rows with top_k == 1 over V >= 8192 take the split
+// arg-max (k_argmax_part over 2048-logit chunks, then the per-row reduction), one HBM pass at chip rate.
+long long fo_sample_ws_floats(int B, int V) {
+  const int nc = (V + AMAX_CH - 1) / AMAX_CH;
+  return (long long)B * nc * (sizeof(AmaxPart) / sizeof(float));
+}
+
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
               const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id, int* out_ids,
-              float* out_maxlogit, hipStream_t s) {
-  FO_REQUIRE(B > 0 && V > 0, "fo_sample: bad shape");
+              float* out_maxlogit, int* err, float* ws, long long ws_floats, hipStream_t s) {
+  FO_REQUIRE(B > 0 && V > 0 && ld >= V, "fo_sample: bad shape B=%d V=%d ld=%d", B, V, ld);
   NextInput nx{};
+  AmaxPart* parts = nullptr;
+  const int nc = (V + AMAX_CH - 1) / AMAX_CH;
+  if (ws && V >= 8192 && nc <= 1024) {
+    FO_REQUIRE(ws_floats >= fo_sample_ws_floats(B, V), "fo_sample: workspace of %lld floats < %lld", ws_floats,
+               fo_sample_ws_floats(B, V));
+    parts = reinterpret_cast<AmaxPart*>(ws);
+    hipLaunchKernelGGL(k_argmax_part, dim3(nc, B), dim3(256), 0, s, logits, ld, V, ban_id, parts, nc);
+    const int rc = fo::check_launch("fo_sample/argmax_part");
+    if (rc) return rc;
+  }
   hipLaunchKernelGGL(k_sample<false>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
-                     key, ban_id, out_ids, out_maxlogit, nullptr, 0, nx);
+                     key, ban_id, out_ids, out_maxlogit, nullptr, 0, nx, parts, nc, err);
   return fo::check_launch("fo_sample");
 }
 
@@ -580,11 +720,11 @@ int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const
 // models/audioLLM.py:455-476) to probs [B][ldp] (ldp >= V).
 int fo_sample_probs(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
-                    int* out_ids, float* probs, int ldp, hipStream_t s) {
+                    int* out_ids, float* probs, int ldp, int* err, hipStream_t s) {
   FO_REQUIRE(B > 0 && V > 0 && probs && ldp >= V, "fo_sample_probs: bad shape B=%d V=%d ldp=%d", B, V, ldp);
   NextInput nx{};
   hipLaunchKernelGGL(k_sample<false>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
-                     key, ban_id, out_ids, nullptr, probs, ldp, nx);
+                     key, ban_id, out_ids, nullptr, probs, ldp, nx, nullptr, 0, err);
   return fo::check_launch("fo_sample_probs");
 }
 
@@ -594,7 +734,7 @@ int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
                     int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
                     int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, int* meta, int maxb,
-                    int PS, hipStream_t s) {
+                    int PS, int* err, hipStream_t s) {
   FO_REQUIRE(B > 0 && V > 0 && D > 0 && (D % 4) == 0 && D <= 4096, "fo_sample_embed: bad shape B=%d V=%d D=%d", B, V, D);
   FO_REQUIRE(emb && x && gamma && h && (!hist || ((hist_row || meta) && hist_ld >= B)), "fo_sample_embed: missing buffers");
   FO_REQUIRE((ldx % 4) == 0 && (ldh % 4) == 0, "fo_sample_embed: row strides must be float4-aligned");
@@ -602,7 +742,7 @@ int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k,
              "fo_sample_embed: meta must be the decode block whose step / key rows are passed");
   NextInput nx{hist, hist_row, hist_ld, (const bf16_t*)emb, emb_ld, D, x, ldx, gamma, eps, h, ldh, meta, B, maxb, PS};
   hipLaunchKernelGGL(k_sample<true>, dim3(B), dim3(1024), 0, s, logits, ld, V, top_k, temperature, top_p, seed, step,
-                     key, ban_id, out_ids, nullptr, nullptr, 0, nx);
+                     key, ban_id, out_ids, nullptr, nullptr, 0, nx, nullptr, 0, err);
   return fo::check_launch("fo_sample_embed");
 }
 

@@ -116,13 +116,14 @@ _SIGS = {
     "fo_scale_add_cl": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_conv_post_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_silence_cut": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "fo_sample_ws_floats": (c_ll, [c_int, c_int]),
     "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int, c_vp,
-                          c_vp, c_vp]),
+                          c_vp, c_vp, c_vp, c_ll, c_vp]),
     "fo_sample_probs": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int,
-                                c_vp, c_vp, c_int, c_vp]),
+                                c_vp, c_vp, c_int, c_vp, c_vp]),
     "fo_sample_embed": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int,
                                 c_vp, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp, c_float, c_vp, c_int,
-                                c_vp, c_int, c_int, c_vp]),
+                                c_vp, c_int, c_int, c_vp, c_vp]),
     "fo_gemm_set_pipe": (c_int, [c_int]),
     "fo_conv1d_ex": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                              c_vp, c_int, c_vp]),

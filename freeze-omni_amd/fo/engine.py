@@ -297,8 +297,11 @@ class FreezeOmniEngine:
         tp = torch.tensor([temperature] * B + [top_p] * B, dtype=F32).to(self.device)
         step = torch.tensor([kv.length for kv, _ in items], dtype=I32).to(self.device)
         out = torch.empty(B, dtype=I32, device=self.device)
-        ops.sample(logits, self.llm.V, out, par, tp[:B], tp[B:], seed=seed, step=step)
-        return out.cpu().tolist(), hid
+        chk = ops.sample_check(self.device)
+        ops.sample(logits, self.llm.V, out, par, tp[:B], tp[B:], seed=seed, step=step, err=chk, argmax_ws=top_k == 1)
+        ids = out.cpu().tolist()
+        chk.check("text decode")
+        return ids, hid
 
 
     def _text_graph_for(self, items, top_k, top_p, temperature, seed, extra=64):
@@ -558,6 +561,8 @@ class TextGraph:
         self.tp = torch.tensor([temperature] * B + [top_p] * B, dtype=F32).to(dev)
         self.out = torch.empty(B, dtype=I32, device=dev)
         self.out_host = torch.empty(B, dtype=I32).pin_memory()
+        self.top_k = top_k
+        self.err = ops.SampleCheck()
         self.main = ops.engine_stream(dev)
         self.exec = ListenGraph._capture(self.main, self._body)
         self.ev = ListenGraph._event()
@@ -568,7 +573,8 @@ class TextGraph:
         llm.stack.forward(self.x, self.meta, self.ws)
         ops.rmsnorm(self.x, llm.norm, llm.eps, out=self.x)
         llm.lm_head(self.x, out=self.logits)
-        ops.sample(self.logits, llm.V, self.out, self.par, self.tp[:B], self.tp[B:], seed=self.seed, step=self.step)
+        ops.sample(self.logits, llm.V, self.out, self.par, self.tp[:B], self.tp[B:], seed=self.seed, step=self.step,
+                   err=self.err, argmax_ws=self.top_k == 1)
 
     def run(self, items):
         """items: list of (kv, [token id]) in batch order; appends one KV position per session."""
@@ -595,6 +601,7 @@ class TextGraph:
             hid = self.x.clone()
         _lib.call("fo_event_record", self.ev, st.cuda_stream)
         _lib.call("fo_event_sync", self.ev)
+        self.err.check("text decode step")
         return self.out_host.tolist(), hid
 
     def destroy(self):
@@ -602,6 +609,7 @@ class TextGraph:
             _lib.call("fo_graph_destroy", self.exec)
             _lib.call("fo_event_destroy", self.ev)
             self.ring.destroy()
+            self.err.free()
             self.exec = None
 
 

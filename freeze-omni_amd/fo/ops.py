@@ -492,25 +492,71 @@ def silence_cut(x, N, res):
     return res
 
 
+class SampleCheck:
+    """Host-mapped error word of the samplers (the C-ABI's `err`): a kernel sets it when a logits row holds a
+    NaN or +inf (or only -inf) -- the rows the reference's torch.multinomial refuses (models/decoder/
+    decoder.py:355-359, models/audioLLM.py:476: "probability tensor contains either inf, nan or element < 0").
+    check() is read on the host after the sampling work has completed (an event / stream sync) and raises
+    RuntimeError, as the reference does; the drawn ids themselves always stay inside the vocabulary."""
+
+    def __init__(self):
+        self.buf = HostBuffer(1, 1)
+        self.buf.np[0, 0] = 0
+
+    @property
+    def dev(self):
+        return self.buf.dev
+
+    def check(self, what="sampler"):
+        if self.buf.np is not None and int(self.buf.np[0, 0]) != 0:
+            self.buf.np[0, 0] = 0
+            raise RuntimeError(f"{what}: a logits row holds NaN / inf (probability tensor contains either inf, nan or "
+                               "element < 0 -- torch.multinomial raises on it in the reference)")
+
+    def free(self):
+        self.buf.free()
+
+
+_CHECKS = {}
+
+
+def sample_check(device):
+    """The default SampleCheck of a device (used when a sampler call passes none)."""
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    if idx not in _CHECKS:
+        _CHECKS[idx] = SampleCheck()
+    return _CHECKS[idx]
+
+
 def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None,
-           ban_id=-1, key=None):
-    """key: optional per-row int32 stream ids (defaults to the row index)."""
+           ban_id=-1, key=None, err=None, argmax_ws=False):
+    """key: optional per-row int32 stream ids (defaults to the row index).  err: SampleCheck (default: the
+    device's; read it with .check() after the work has completed).  argmax_ws=True: every row is top_k == 1,
+    so large-vocabulary rows take the split arg-max (scratch at the tail of the stream's Runtime workspace)."""
     B = logits.shape[0] if B is None else B
+    err = err or sample_check(logits.device)
+    ws, wsn = None, 0
+    if argmax_ws:
+        wsn = int(_lib.load().fo_sample_ws_floats(B, V))
+        rt = Runtime.get(logits.device)
+        ws = rt.ws[rt.ws.numel() - wsn:].data_ptr()
     _lib.call("fo_sample", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
               int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), ptr(out_max),
-              stream(logits.device))
+              err.dev, ws, wsn, stream(logits.device))
     return out_ids
 
 
 def sample_probs(logits, V, out_ids, probs, top_k=None, temperature=None, top_p=None, seed=0, step=None, B=None,
-                 ban_id=-1, key=None):
+                 ban_id=-1, key=None, err=None):
     """sample() that also writes each row's sampling distribution (the reference's pre-multinomial probs)
     into probs [B, >=V] fp32."""
     B = logits.shape[0] if B is None else B
     assert probs.dtype == F32 and probs.is_contiguous() and probs.shape[0] >= B and probs.shape[1] >= V
+    err = err or sample_check(logits.device)
     _lib.call("fo_sample_probs", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
               int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), probs.data_ptr(),
-              probs.stride(0), stream(logits.device))
+              probs.stride(0), err.dev, stream(logits.device))
     return out_ids
 
 
@@ -555,15 +601,16 @@ def penalty(logits, V, ids, win, step, penalty, B=None):
 
 def sample_embed(logits, V, out_ids, emb, x, gamma, eps, h, top_k=None, temperature=None, top_p=None, seed=0,
                  step=None, B=None, ban_id=-1, key=None, hist_ptr=None, hist_row=None, hist_ld=0, meta=None, maxb=0,
-                 PS=0):
+                 PS=0, err=None):
     """sample(), then the next decode step's input from the drawn ids: x[b] = emb[id_b] (fp32), h[b] =
     RMSNorm(x[b]) * gamma, and (hist_ptr) hist[hist_row[0] * hist_ld + b] = id_b -- one launch.  meta: the
     captured step's metadata block (step / key are its rows): it advances to the next step in the same launch."""
     B = logits.shape[0] if B is None else B
+    err = err or sample_check(logits.device)
     _lib.call("fo_sample_embed", logits.data_ptr(), logits.stride(0), B, V, ptr(top_k), ptr(temperature), ptr(top_p),
               int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(step), ptr(key), int(ban_id), out_ids.data_ptr(), hist_ptr,
               ptr(hist_row), hist_ld, emb.data_ptr(), emb.stride(0), emb.shape[1], x.data_ptr(), x.stride(0),
-              gamma.data_ptr(), float(eps), h.data_ptr(), h.stride(0), ptr(meta), int(maxb), int(PS),
+              gamma.data_ptr(), float(eps), h.data_ptr(), h.stride(0), ptr(meta), int(maxb), int(PS), err.dev,
               stream(logits.device))
     return out_ids
 

@@ -131,9 +131,11 @@ def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
         if pen:
             win = torch.tensor([penalty_ring([tts.sos] + states[i].all_ids, pen[0]) for i in live], dtype=I32).to(dev)
             ops.penalty(lg, tts.vocab + 4, cur, win, st, pen[1], B=len(live))
+        chk = ops.sample_check(dev)
         ops.sample(lg, tts.vocab if forced else tts.vocab + 4, out_ids, topk_d, None, None, seed=seed,
-                   step=st[:len(live)], B=len(live), key=st[len(live):])
+                   step=st[:len(live)], B=len(live), key=st[len(live):], err=chk)
         ids = out_ids[:len(live)].cpu().tolist()
+        chk.check("speech decode")
         step += 1
         finished, chunk_due = [], []
         for j, i in enumerate(live):
@@ -192,6 +194,7 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
             while pending:
                 st, batch, pg, ev = pending.popleft()
                 _lib.call("fo_event_sync", ev)
+                pg.check()
                 row = pg.hist.np[st].tolist()
                 fin2, due2 = [], []
                 for j, i in enumerate(batch):

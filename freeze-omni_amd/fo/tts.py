@@ -238,6 +238,7 @@ class DecodeGraph:
         self.logits = torch.empty(B, tts.vocab + 4, dtype=F32, device=dev)
         self.topk = torch.tensor([top_k] * B, dtype=I32).to(dev)
         self.ws = tts.main.workspace(B, ops.attn_nsplit(max_keys, B, tts.H), dev)
+        self.err = ops.SampleCheck()   # NaN / inf logits rows (the reference's multinomial raises on them)
         self.fused = tts.fused_step_args(self) if tts.fused else None
         self.events = []
         for _ in range(self.RING):
@@ -262,7 +263,7 @@ class DecodeGraph:
         ops.sample_embed(self.logits, self.V_sample, self.ids, t.embedding, self.x, t.main.layers[0].ln1, t.eps,
                          self.ws["h"], top_k=self.topk, seed=self.seed, step=self.meta.step, B=self.B,
                          key=self.meta.key, hist_ptr=self.hist.dev, hist_row=self.meta.hist_row, hist_ld=self.B,
-                         **(dict(meta=self.meta_d, maxb=self.maxb, PS=t.pool.PS) if self.advance else {}))
+                         err=self.err, **(dict(meta=self.meta_d, maxb=self.maxb, PS=t.pool.PS) if self.advance else {}))
 
     def prime(self):
         """Input rows of the next replay from self.ids (first step of a batch, or after the batch changed)."""
@@ -279,7 +280,9 @@ class DecodeGraph:
         self.ws["h"].copy_(other.ws["h"])
 
     def check(self):
-        """Raise if a fused step's device barrier ever timed out (it never blocks: it gives up and flags)."""
+        """After a step's event: raise if a logits row was NaN / inf (the reference's torch.multinomial raises,
+        decoder.py:355-359) or a fused step's device barrier timed out (it never blocks: it gives up and flags)."""
+        self.err.check("speech decode step")
         if self.fused is not None and int(self._err.np[0, 0]) != 0:
             raise RuntimeError("fo_tts_step: a device barrier timed out (workgroups not co-resident)")
 
@@ -358,5 +361,6 @@ class DecodeGraph:
             _lib.call("fo_event_destroy", e)
         self.events = []
         self.hist.free()
+        self.err.free()
         if self.fused is not None:
             self._err.free()

@@ -149,10 +149,13 @@ class AudioLLM:
             self._draws = getattr(self, "_draws", 0) + 1
             seed = self._draws
         out = torch.empty(1, dtype=I32, device=self.device)
+        chk = ops.sample_check(self.device)
         ops.sample(lg, V, out, torch.tensor([int(top_k)], dtype=I32).to(self.device),
                    torch.tensor([temperature], dtype=F32).to(self.device),
-                   torch.tensor([top_p], dtype=F32).to(self.device), seed=seed)
-        return out.view(1, 1).long()
+                   torch.tensor([top_p], dtype=F32).to(self.device), seed=seed, err=chk)
+        tok = out.view(1, 1).long().cpu()
+        chk.check("_post_decode")   # NaN / inf logits: the reference's torch.multinomial raises
+        return tok.to(self.device)
 
     # ------------------------------------------------------------------ A17: text decode step
     def generate_step(self, past_key_values, input_ids, top_k=None, top_p=None, temperature=None):

@@ -27,8 +27,10 @@ class LLM2TTSCodecAR:
                 if penalty_window_size > 0:   # decoder.py:348-351
                     win = torch.tensor([penalty_ring(generated, penalty_window_size)], dtype=torch.int32).to(dev)
                     ops.penalty(lg, e.vocab + 4, cur, win, step, penalty)
-                ops.sample(lg, e.vocab + 4, out, k, step=step)
+                chk = ops.sample_check(dev)
+                ops.sample(lg, e.vocab + 4, out, k, step=step, err=chk)
                 t = int(out.item())
+                chk.check("LLM2TTSCodecAR.infer")   # decoder.py:355-359: multinomial raises on NaN / inf
                 if t == e.eos:
                     break
                 generated.append(t)

@@ -233,16 +233,22 @@ int fo_vq_nearest(float* x, int B, int Ctot, int T, int ch0, int D, const float*
 
 /* ---------------------------------------------------------------- sampling (fo_sample.hip) */
 /* AudioLLM._post_decode (models/audioLLM.py:431-477) / decoder top-k (models/decoder/decoder.py:353-359).
- * Draws come from a counter stream keyed by (seed, key[row] or row, step[row]). */
+ * Draws come from a counter stream keyed by (seed, key[row] or row, step[row]).
+ * err (nullable, every sampler entry): set to 1, never cleared, when a row holds a NaN or +inf logit or
+ * only -inf ones -- the rows whose softmax torch.multinomial refuses (decoder.py:355-359 raises); the
+ * drawn id stays inside [0, V).  The caller raises on it (Python: RuntimeError).
+ * ws (nullable, >= fo_sample_ws_floats(B, V) floats): top_k == 1 rows over V >= 8192 take a split
+ * arg-max (one pass over the row by ~V/2048 workgroups, then the per-row reduction). */
+long long fo_sample_ws_floats(int B, int V);
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
               const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
-              int* out_ids, float* out_maxlogit, hipStream_t s);
+              int* out_ids, float* out_maxlogit, int* err, float* ws, long long ws_floats, hipStream_t s);
 /* fo_sample that also writes each row's sampling distribution -- the `probs` _post_decode hands to
  * torch.multinomial (models/audioLLM.py:455-476) -- to probs[row * ldp + i] (ldp >= V).  top_k 0 (no
  * top-k, the reference default) and top_k > 64 take a whole-vocabulary radix-select path. */
 int fo_sample_probs(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
-                    int* out_ids, float* probs, int ldp, hipStream_t s);
+                    int* out_ids, float* probs, int ldp, int* err, hipStream_t s);
 /* fo_sample fused with the next AR decode step's input (models/decoder/decoder.py:341-346: embed(id) ->
  * first LlamaRMSNorm): hist[hist_row[0] * hist_ld + row] = id (hist nullable), x[row] = emb[id] (bf16
  * table -> fp32), h[row] = RMSNorm(x[row]) * gamma.  meta (nullable): the captured step's metadata block
@@ -252,7 +258,7 @@ int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k,
                     const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id,
                     int* out_ids, int* hist, const int* hist_row, int hist_ld, const void* emb, long long emb_ld,
                     int D, float* x, int ldx, const float* gamma, float eps, float* h, int ldh, int* meta, int maxb,
-                    int PS, hipStream_t s);
+                    int PS, int* err, hipStream_t s);
 /* Repetition penalty of the AR decode loop (models/decoder/decoder.py:348-351), applied before the
  * draw: win[row][step[row] % W] = ids[row], then logits[row][t] /= penalty for every entry t of the
  * last min(step+1, W) ids -- once per occurrence, as the reference's set() of 0-d tensors does. */

@@ -52,18 +52,38 @@ def bf16_round(a):
     return (u.astype(np.uint32) << np.uint32(16)).view(np.float32).reshape(a.shape)
 
 
-def hash_uniform(seed, name, shape, center=0.0, scale=1.0, out_bf16=True):
+def hash_uniform(seed, name, shape, center=0.0, scale=1.0, out_bf16=True, chunk=1 << 24):
+    """Elementwise, so it is evaluated in chunks of `chunk` elements: a 545M-element Qwen2-7B embedding
+    table then needs ~0.3 GB of uint64 temporaries instead of ~15 GB."""
     n = int(np.prod(shape)) if len(shape) else 1
     key = np.uint64(tensor_key(seed, name))
-    idx = np.arange(n, dtype=np.uint64)
+    out = np.empty(n, dtype=np.float32)
+    for i0 in range(0, n, chunk):
+        idx = np.arange(i0, min(n, i0 + chunk), dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            v = _splitmix64_np(key + idx)
+        u = (v >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+        w = (np.float32(2.0) * u - np.float32(1.0)) * np.float32(scale) + np.float32(center)
+        w = w.astype(np.float32)
+        out[i0:i0 + len(w)] = bf16_round(w) if out_bf16 else w
+    return out.reshape(shape)
+
+
+def synth_rows(seed, name, shape, rows, overrides=None):
+    """Rows `rows` of the 2-D parameter synth_param(seed, name, shape) without materialising the rest
+    (e.g. a few embedding rows or lm_head rows of the 152,064 x 3584 Qwen2 tables)."""
+    c, s = init_spec(name, tuple(shape), overrides)
+    rows = np.asarray(rows, dtype=np.int64)
+    K = int(shape[1])
+    if s == 0.0:
+        return np.full((len(rows), K), c, dtype=np.float32)
+    key = np.uint64(tensor_key(seed, name))
+    idx = (rows[:, None] * K + np.arange(K)[None, :]).astype(np.uint64)
     with np.errstate(over="ignore"):
         v = _splitmix64_np(key + idx)
     u = (v >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
-    w = (np.float32(2.0) * u - np.float32(1.0)) * np.float32(scale) + np.float32(center)
-    w = w.astype(np.float32)
-    if out_bf16:
-        w = bf16_round(w)
-    return w.reshape(shape)
+    w = ((np.float32(2.0) * u - np.float32(1.0)) * np.float32(s) + np.float32(c)).astype(np.float32)
+    return bf16_round(w).reshape(len(rows), K)
 
 
 def init_spec(name, shape, overrides=None):

@@ -615,6 +615,121 @@ def gold_real_t2(seed=7):
     print("T2 codec: pcm", tuple(pcm.shape))
 
 
+REAL_QWEN2_SETTINGS = [(1.0, k, p) for k in (0, 1, 20, 100) for p in (0.0, 0.8)]   # (temperature, top_k, top_p)
+
+
+def gold_real_qwen2(seed=7, n_layers=2, n_sess=8):
+    """Qwen2-7B at REAL geometry (hidden 3584, 28 q / 4 kv heads of 128, intermediate 18944, rope_theta 1e6,
+    vocab 152064, untied lm_head), n_layers of the 28 layers, counter-hash weights (configs 'real'), run
+    through the reference's own AudioLLM methods on a Qwen2ForCausalLM (models/audioLLM.py:70-74):
+    _llm_forward_core (:479-484, inputs_embeds.half() and the all-True [past | new] mask of recognize,
+    :409-419), _prediction_head_forward (:486-493) and _post_decode (:431-477).
+    n_sess ragged sessions, each its own DynamicCache (the reference serves one session per call):
+      step 0   prefill of 9 + 2b rows (fp16-valued random embeds: the batched GPU prefill is M = 128),
+      step 1-2 two-row chunks (a listen chunk, M = 16 batched),
+      step 3-5 text steps: lm_head on the last hidden row, _post_decode(top_k=1) -> that token's
+               embedding (wte(tok).half()) is the next step's input (a text step, M = 8 batched).
+    Stored (I/O only, weights regenerate from the hash): the input embeds, hidden rows (last row of the
+    prefill, every row of the other steps), state probs, the lm_head logits of the 4 decision rows per
+    session reduced to (argmax, top-2 margin, top-32 ids / values, logsumexp, 1024 fixed-index values)
+    plus 2 full 152,064-wide rows, and _post_decode's pre-multinomial probs on those 2 rows for
+    top_k in {0, 1, 20, 100} x top_p in {0, 0.8}."""
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    sys.argv = ["golden"]
+    from models.audioLLM import AudioLLM
+    cfg = C.get("real")
+    assert cfg["seed"] == seed
+    lc = dict(cfg["llm"], num_hidden_layers=n_layers)
+    qc = Qwen2Config(**lc, torch_dtype="float32")
+    m = Qwen2ForCausalLM(qc)
+    for k, v in m.state_dict().items():   # one tensor at a time (6 GB of fp32 weights at 2 layers)
+        v.copy_(torch.from_numpy(synth_param(seed, k, tuple(v.shape), cfg["overrides"])))
+    m.eval()
+    D, V = lc["hidden_size"], lc["vocab_size"]
+    head = torch.nn.Linear(D, 4)
+    init_module(head, seed, "predictor_head.", cfg["overrides"])
+    obj = types.SimpleNamespace(llm_decoder=m, predictor_head=head)
+    wte = m.model.embed_tokens
+    rng = np.random.default_rng(1234)
+    rows0 = [9 + 2 * b for b in range(n_sess)]
+    emb_in = {0: [(rng.standard_normal((r, D)) * 0.5).astype(np.float16) for r in rows0]}
+    for s in (1, 2):
+        emb_in[s] = [(rng.standard_normal((2, D)) * 0.5).astype(np.float16) for _ in range(n_sess)]
+    fixed_idx = np.sort(np.random.default_rng(99).choice(V, 1024, replace=False))
+    out = {"rows0": np.array(rows0, np.int64), "fixed_idx": fixed_idx.astype(np.int64)}
+    for s in (0, 1, 2):
+        out[f"emb{s}"] = np.concatenate(emb_in[s])
+    hid = {s: [] for s in range(6)}
+    probs = np.zeros((6, n_sess, 3), np.float32)
+    toks = np.zeros((4, n_sess), np.int64)           # token fed at text steps 3..5 (toks[0..2]) + last pick
+    dec = {k: [] for k in ("argmax", "margin", "top_ids", "top_vals", "lse", "fixed")}
+    full = {}
+
+    def reduce_logits(lg):
+        v, i = torch.topk(lg, 32)
+        dec["argmax"].append(int(i[0]))
+        dec["margin"].append(float(v[0] - v[1]))
+        dec["top_ids"].append(i.numpy().astype(np.int64))
+        dec["top_vals"].append(v.numpy().astype(np.float32))
+        dec["lse"].append(float(torch.logsumexp(lg.double(), 0)))
+        dec["fixed"].append(lg.numpy()[fixed_idx].astype(np.float32))
+
+    for b in range(n_sess):
+        pkv = None
+        tok = None
+        for s in range(6):
+            if s < 3:
+                e = torch.from_numpy(emb_in[s][b].astype(np.float32)).unsqueeze(0)
+            else:
+                e = wte(torch.tensor([[tok]]))
+            past = 0 if pkv is None else pkv.get_seq_length()
+            mask = torch.full([1, past + e.shape[1]], True)
+            h, pkv = AudioLLM._llm_forward_core(obj, {"inputs_embeds": e.half(), "attention_mask": mask,
+                                                      "past_key_values": pkv})
+            hid[s].append(h[0, -1:].numpy().copy() if s == 0 else h[0].numpy().copy())
+            probs[s, b] = AudioLLM._prediction_head_forward(obj, h).numpy()
+            if s >= 2:
+                lg = m.lm_head(h[:, -1:])
+                reduce_logits(lg[0, 0])
+                if (b, s) in ((0, 2), (1, 3)):
+                    full[f"full_b{b}_s{s}"] = lg[0, 0].numpy().copy()
+                tok = int(AudioLLM._post_decode(None, lg, temperature=1.0, top_k=1, top_p=0.0).reshape(-1)[0])
+                toks[s - 2, b] = tok
+        print(f"real qwen2 session {b}: rows {rows0[b]} kv {pkv.get_seq_length()} tokens {toks[:, b].tolist()} "
+              f"margins {[round(x, 4) for x in dec['margin'][-4:]]}", flush=True)
+    for s in range(6):
+        out[f"hid{s}"] = np.concatenate(hid[s]).astype(np.float32)
+    out["probs"] = probs
+    out["toks"] = toks
+    for k, v in dec.items():
+        out["dec_" + k] = np.array(v)
+    out.update(full)
+    # _post_decode's pre-multinomial probs at V = 152,064 (multinomial captured, argmax returned)
+    orig = torch.multinomial
+    rows = [full["full_b0_s2"], full["full_b1_s3"]]
+    sp = np.zeros((len(rows), len(REAL_QWEN2_SETTINGS), V), np.float32)
+    try:
+        for ri, lg in enumerate(rows):
+            for si, (T, k, p) in enumerate(REAL_QWEN2_SETTINGS):
+                cap = {}
+
+                def mn(pr, n, **kw):
+                    cap["p"] = pr.detach().clone()
+                    return torch.argmax(pr).view(1)
+
+                torch.multinomial = mn
+                AudioLLM._post_decode(None, torch.from_numpy(lg).view(1, 1, -1), temperature=T, top_k=k, top_p=p)
+                sp[ri, si] = cap["p"].numpy()
+    finally:
+        torch.multinomial = orig
+    out["sampler_probs"] = sp
+    out["sampler_settings"] = np.array(REAL_QWEN2_SETTINGS, np.float64)
+    np.savez_compressed(os.path.join(HERE, "real_qwen2_t2.npz"), **out)
+    print("real qwen2: kept counts", [[int((sp[r, s] > 0).sum()) for s in range(len(REAL_QWEN2_SETTINGS))]
+                                      for r in range(len(rows))],
+          f"fixture {os.path.getsize(os.path.join(HERE, 'real_qwen2_t2.npz')) / 1e6:.2f} MB")
+
+
 ADAPTER_VARIANTS = [  # CNNSubsampling(enc_out_dim, llm_embed_dim, kernel_size, activation_func, norm)
     {"enc_out_dim": 16, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "relu", "norm": "batch"},
     {"enc_out_dim": 32, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "gelu", "norm": "layer"},
@@ -832,6 +947,7 @@ def main():
     gold_audiollm_b(cfg)
     gold_llm_text(cfg)
     gold_real_t2()
+    gold_real_qwen2()
     gold_adapter_variants(cfg["seed"])
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
         json.dump(SHAPES, f)
@@ -858,5 +974,8 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["real_t2"]:
         install_shims()
         gold_real_t2()
+    elif sys.argv[1:] == ["real_qwen2"]:
+        install_shims()
+        gold_real_qwen2()
     else:
         main()
