@@ -7,9 +7,10 @@ One "step" = one full dialogue turn for every user on every rank (SURVEY.md §8(
   listen : 10 s of synthetic 16 kHz PCM per user streamed in 160 ms chunks (framing A, 63 chunks);
            each chunk = fbank -> speech encoder -> adapter -> Qwen2-7B chunk prefill (per-user paged KV
            forked from a shared system prompt) -> dialog-state head (host read each chunk, as the reference)
-  speak  : dialog_ss -> assistant-prefix prefill + 8 text tokens (benchmark policy: one sentence of 8
-           tokens) -> AR speech decoder (EOS masked until 400 codec tokens = 10 s of 24 kHz audio) ->
-           TiCodec vocoder per 40(+10+10) tokens -> silence-cut emission.
+  speak  : dialog_ss -> assistant-prefix prefill + 32 text tokens (benchmark policy, SURVEY §8(d): a sentence
+           boundary every 8 tokens) -> per sentence, started at its boundary beside the text decode
+           (bin/inference.py:152-183): AR speech decoder (EOS masked until 100 codec tokens; 400 = 10 s of
+           24 kHz audio per response) -> TiCodec vocoder per 40(+10+10) tokens -> silence-cut emission.
 value = seconds of 24 kHz speech emitted by all users on all ranks / max-over-ranks wall seconds
 (aggregate real-time factor, higher is better).  Also reported: per-user RTF (audio / (dialog_ss ->
 last PCM)), p50/p90 first-audio latency (dialog_ss -> PCM of the first vocoder chunk known on the host,
@@ -55,8 +56,13 @@ def parse():
     ap.add_argument("--users", type=int, default=8, help="concurrent users per GPU")
     ap.add_argument("--config", default="real", choices=["real", "tiny"])
     ap.add_argument("--input-sec", type=float, default=10.0)
-    ap.add_argument("--text-tokens", type=int, default=8)
-    ap.add_argument("--codec-tokens", type=int, default=400)
+    ap.add_argument("--text-tokens", type=int, default=32, help="text tokens per response (bin/inference.py caps 128)")
+    ap.add_argument("--sentence-tokens", type=int, default=8,
+                    help="benchmark policy: a sentence boundary every N text tokens (SURVEY §8(d))")
+    ap.add_argument("--codec-tokens", type=int, default=400, help="codec tokens per response (10 s of 24 kHz speech)")
+    ap.add_argument("--no-concurrent-tts", dest="concurrent_tts", action="store_false",
+                    help="speak each sentence inside the text loop, as bin/inference.py does (default: a worker "
+                         "thread on its own streams, beside the text decode)")
     ap.add_argument("--top-k", type=int, default=1, help="speech decoder top_k (1 = parity/greedy)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
@@ -95,7 +101,6 @@ class Turn:
 
 def run_turn(engine, base_kv, pcms, args, sync):
     import torch
-    from fo.speak import speak
     B = len(pcms)
     t_begin = time.perf_counter()
     turns = [Turn(engine, base_kv, p) for p in pcms]
@@ -136,44 +141,203 @@ def run_turn(engine, base_kv, pcms, args, sync):
     t_ss = time.perf_counter()
     eod = engine.tokenizer.eod_id
     pre = engine.prefix_ids["system"]
+    T, S = args.text_tokens, args.sentence_tokens
+    n_sent = (T + S - 1) // S
+    # 400 codec tokens per response (EOS masked until then), dealt over the sentences
+    codec_per = [args.codec_tokens // n_sent + (1 if s < args.codec_tokens % n_sent else 0) for s in range(n_sent)]
+    rec = SpeechRecorder(B)
+    tts = SentenceTTS(engine, args, rec) if args.concurrent_tts else None
     text_ids = [[] for _ in turns]
     hiddens = []
     nxt, hid = engine.text_step([(t.kv, pre) for t in turns])
-    for _ in range(args.text_tokens):
+    s0 = 0
+    for j in range(T):
         hiddens.append(hid)
         for b in range(B):
             text_ids[b].append(nxt[b] if nxt[b] != eod else 0)
-        if len(hiddens) == args.text_tokens:
+        if (j + 1) % S == 0 or j == T - 1:
+            # sentence boundary (benchmark policy: every S tokens; bin/inference.py:160-173 cuts at punctuation):
+            # this sentence's speech starts now, while the text decode goes on (bin/inference.py:82-92)
+            job = (hiddens[s0:j + 1], [ids[s0:j + 1] for ids in text_ids], codec_per[len(rec.sentences)])
+            rec.sentences.append(time.perf_counter())
+            if tts is not None:
+                tts.submit(job)
+            else:
+                run_sentence(engine, args, rec, *job)
+            s0 = j + 1
+        if j == T - 1:
             break
         nxt, hid = engine.text_step([(t.kv, [text_ids[b][-1]]) for b, t in enumerate(turns)])
     t_text = time.perf_counter()   # the last text step's ids were read back: the text stage is done
-    D = engine.llm.D
-    idim = engine.cfg["decoder_json"][0]
-    items = []
-    ids_d = torch.tensor(text_ids, dtype=torch.int32).to(engine.device)
-    emb = engine.llm.embed(ids_d.view(-1))
-    hs = torch.stack(hiddens, 1)  # [B, T', D]
-    for b in range(B):
-        e = emb[b * args.text_tokens:(b + 1) * args.text_tokens].reshape(-1, idim).contiguous()
-        p = hs[b].reshape(-1, idim).contiguous()
-        items.append((e, p))
-    first = [None] * B
-    last = [None] * B
-    samples = [0] * B
-    states = []
-    for i, seg in speak(engine, items, top_k=args.top_k, min_tokens=args.codec_tokens,
-                        max_tokens=args.codec_tokens, states_out=states):
-        now = time.perf_counter()  # the segment's length is known on the host: the cut index was read back
-        if first[i] is None:
-            first[i] = now
-        last[i] = now
-        samples[i] += seg.numel()
+    if tts is not None:
+        tts.join()
     t_end = time.perf_counter()
     for t in turns:
         t.kv.free()
-    stage = {"listen": (t_ss - t_begin) * 1e3, "text": (t_text - t_ss) * 1e3, "speak": (t_end - t_text) * 1e3}
-    return dict(t_ss=t_ss, first=first, last=last, samples=samples, first_pcm=[s.t_first_pcm for s in states],
-                stage=stage)
+    stage = {"listen": (t_ss - t_begin) * 1e3, "text": (t_text - t_ss) * 1e3, "speak": (t_end - t_ss) * 1e3,
+             "speak_after_text": (t_end - t_text) * 1e3}
+    return dict(t_ss=t_ss, first=rec.first, last=rec.last, samples=rec.samples, first_pcm=rec.first_pcm,
+                stage=stage, n_sent=n_sent, codec_tokens=rec.codec_tokens)
+
+
+class SpeechRecorder:
+    """Per-user timing of the speech of one turn, over all its sentences."""
+
+    def __init__(self, B):
+        self.first = [None] * B        # first PCM segment released by the silence gate
+        self.first_pcm = [None] * B    # first vocoder chunk's PCM known on the host (before the gate)
+        self.last = [None] * B
+        self.samples = [0] * B
+        self.codec_tokens = [0] * B
+        self.sentences = []            # host time of each sentence boundary
+
+    def segment(self, i, seg):
+        now = time.perf_counter()      # the segment's length is known on the host: the cut index was read back
+        if self.first[i] is None:
+            self.first[i] = now
+        self.last[i] = now
+        self.samples[i] += seg.numel()
+
+
+def run_sentence(engine, args, rec, hiddens, ids, n_codec, stream=None, voc=None):
+    """llm2TTS.run for one sentence of every user (bin/inference.py:82-92): the sentence's text-token
+    embeddings and LLM hidden rows, each reshaped to [-1, 896] sub-tokens, through the AR decoder (EOS masked
+    until n_codec tokens) and the vocoder with silence-cut emission.  stream / voc: the AR
+    decode's and the vocoder's streams (None: the engine's own); the inputs are gathered on `stream` too, so
+    nothing of the sentence touches the legacy default stream (which would order it against the text decode)."""
+    import contextlib
+
+    import torch
+    from fo.speak import speak
+    B, n = len(ids), len(ids[0])
+    idim = engine.cfg["decoder_json"][0]
+    with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
+        ids_d = torch.tensor(ids, dtype=torch.int32).to(engine.device)
+        emb = engine.llm.embed(ids_d.view(-1))
+        hs = torch.stack(hiddens, 1)  # [B, n, D]
+        items = [(emb[b * n:(b + 1) * n].reshape(-1, idim).contiguous(), hs[b].reshape(-1, idim).contiguous())
+                 for b in range(B)]
+        states = []
+        for i, seg in speak(engine, items, top_k=args.top_k, min_tokens=n_codec, max_tokens=n_codec,
+                            states_out=states, stream=stream, voc_stream=voc):
+            rec.segment(i, seg)
+    for i, st in enumerate(states):
+        if rec.first_pcm[i] is None:
+            rec.first_pcm[i] = st.t_first_pcm
+        rec.codec_tokens[i] += len(st.all_ids)
+
+
+class SentenceTTS:
+    """The speech of each sentence generated on its own pair of streams (AR decode + vocoder) by a worker
+    thread, while the main thread keeps decoding text on the engine stream: a sentence's speech depends only
+    on its own text tokens and hidden rows, and the text decode never reads the speech, so the ids and PCM
+    are those of the reference's sequential loop (bin/inference.py:152-183, which pauses the text decode for
+    each sentence).  Sentences are spoken in order (one user's audio is a sequence)."""
+
+    def __init__(self, engine, args, rec):
+        import queue
+        import threading
+        from fo import ops
+        self.q = queue.Queue()
+        self.err = None
+        self.stream = ops.engine_stream(engine.device, name="tts")
+        self.voc = ops.engine_stream(engine.device, name="voc")
+
+        def work():
+            import torch
+            torch.cuda.set_device(engine.device)
+            while True:
+                job = self.q.get()
+                if job is None:
+                    return
+                if self.err is None:
+                    try:
+                        run_sentence(engine, args, rec, *job, stream=self.stream, voc=self.voc)
+                    except BaseException as e:  # re-raised in the main thread by join()
+                        self.err = e
+
+        self.t = threading.Thread(target=work, daemon=True)
+        self.t.start()
+
+    def submit(self, job):
+        self.q.put(job)
+
+    def join(self):
+        self.q.put(None)
+        self.t.join()
+        if self.err is not None:
+            raise self.err
+
+
+def vocoder_calls(n, chunk=40, pad=10):
+    """Token counts of the vocoder calls llm2TTS.run makes for n codec tokens (models/decoder/llm2tts.py:
+    122-160): a call when the buffer holds left + chunk + pad tokens (left 0, then pad), the final flush."""
+    calls, left, have = [], 0, 0
+    for _ in range(n):
+        have += 1
+        if have == left + chunk + pad:
+            calls.append(have)
+            left = pad
+            have = left + pad
+    if have > 0:
+        calls.append(have)
+    return calls
+
+
+def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.0e12, mfma=2.5e15):
+    """Speed-of-light time of one turn's work (each stage against its own bound, the turn as
+    Σ max(bytes / HBM BW, flops / dense bf16 MFMA peak)).  Algorithmic bytes of this implementation's
+    layouts: bf16 weights streamed once per batched step, fp32 paged KV read per token
+    (Qwen2 114,688 B, AR decoder 28,672 B), vocoder as 2*Cin*Cout*K*Tout FLOPs.  ctx0: per-user LLM context
+    when the listen starts (system prompt)."""
+    llm = eng.llm
+    kv_llm = llm.stack.n * llm.KVH * llm.hd * 2 * 4
+    kv_tts = eng.tts.main.n * eng.tts.H * eng.tts.hd * 2 * 4
+    w_listen = eng.enc["user"].weight_bytes + eng.ada["user"].weight_bytes + llm.stack.weight_bytes
+    rows = 2   # LLM tokens per 160 ms chunk (framing A)
+    listen_b = 0.0
+    L = ctx0
+    for c in range(n_chunks):
+        L += rows + (len(eng.prefix_ids["user"]) if c == 0 else 0)
+        listen_b += w_listen + B * L * kv_llm
+    text_b = 0.0
+    L += len(eng.prefix_ids["system"])
+    for t in range(text_tokens):
+        text_b += llm.stack.weight_bytes + llm.lm_head.nbytes + B * L * kv_llm
+        L += 1
+    speak_b, speak_f = 0.0, 0.0
+    pre_w = eng.tts.pre.weight_bytes + eng.tts.main.weight_bytes + (eng.tts.prefix.weight_bytes if eng.tts.prefix else 0)
+    for n in codec_per_sentence:
+        speak_b += pre_w
+        P = 2 * 4 * (text_tokens // max(1, len(codec_per_sentence)))   # prefix + prefill rows (4 sub-tokens each)
+        for i in range(n):
+            speak_b += eng.tts.weight_bytes_per_step + B * (P + i) * kv_tts
+        speak_f += B * sum(eng.codec.flops(T) for T in vocoder_calls(n))
+    ms = {"listen": listen_b / bw * 1e3, "text": text_b / bw * 1e3,
+          "speak": max(speak_b / bw, 0.0) * 1e3 + speak_f / mfma * 1e3}
+    return ms, {"listen_GB": listen_b / 1e9, "text_GB": text_b / 1e9, "speak_GB": speak_b / 1e9,
+                "vocoder_TFLOP": speak_f / 1e12}
+
+
+def codec_ids_check(eng):
+    """The product AR decoder + sampler on the reference's real-geometry golden (tests/golden/real_tts_t2.npz:
+    LLM2TTSCodecAR.infer at 896 / 14 heads / 4864, 4 layers, top_k = 1, 48 ids; configs/real's weights are the
+    golden's).  Returns (matching ids in order, total) -- the codec-token exact match of SURVEY §8(d)."""
+    import torch
+    from fo.speak import speak
+    path = os.path.join(ROOT, "tests", "golden", "real_tts_t2.npz")
+    if not os.path.exists(path):
+        return None, None
+    g = np.load(path)
+    items = [(torch.from_numpy(g["hidden"]).to(eng.device), torch.from_numpy(g["prefix"]).to(eng.device))]
+    states = []
+    for _ in speak(eng, items, top_k=1, max_tokens=len(g["ids"]), states_out=states):
+        pass
+    got, want = states[0].all_ids, g["ids"].tolist()
+    n = 0
+    while n < min(len(got), len(want)) and got[n] == want[n]:
+        n += 1
+    return n, len(want)
 
 
 def cpu_model():
@@ -186,39 +350,58 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(cfg_name, threads, seconds_audio, n_chunks, text_tokens, codec_tokens):
-    """Oracle (numpy fp32 port of the reference path, oracle/nets.py) timed on host cores at REAL geometry,
-    one unit of each kind at FULL depth: U1 = one 160 ms chunk through the 24-block encoder, the adapter
-    and all 28 Qwen2 layers + state head; U2 = one text token through the 28 layers + lm_head; U3 = one
-    codec token through the 4 AR layers + out_fnn; U4 = one 60-token vocoder call.  Only chunk / token /
-    call COUNTS are extrapolated to the turn (no layer extrapolation).  Weights: one random array per
-    parameter shape, shared by every layer of that shape (the GEMMs still stream their operands from DRAM:
-    each shape's array is far beyond the last-level cache), so the sample needs ~3 GB of host RAM, not
-    the 30 GB of distinct fp32 Qwen2 weights.  BLAS threads are set before numpy is imported
-    (_blas_threads_from_argv) and verified with threadpoolctl."""
+def cpu_quota():
+    """CPUs this process may use: the cgroup's cpu.max quota (the GPU box grants 16 of its 256), else the
+    affinity mask."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(cfg_name, threads, text_tokens, sentence_tokens, codec_tokens):
+    """The reference's CPU path restated in numpy fp32 (oracle/nets.py, pinned to the reference's own outputs at
+    real geometry by tests/test_oracle_real_qwen2.py and the T2 goldens), timed on this host's cores:
+      * config 1 END TO END (bin/inference.py:94-187 on assets/question.wav, top_k = 1): the system-role
+        prefill, the 13 framing-A chunks of question.wav (their fbank is the committed fixture
+        tests/golden/fbank.npz A_feats, the reference's own features of that file) through the 24-block
+        encoder, the adapter, all 28 Qwen2 layers and the state head; dialog_ss: the assistant prefix and
+        `text_tokens` greedy text tokens (lm_head over 152,064); per sentence of `sentence_tokens` tokens, the
+        AR decoder's prefill and codec tokens (EOS masked, as the GPU bench) and every vocoder call
+        llm2TTS.run makes (models/decoder/llm2tts.py:122-160);
+      * one unit of each kind at full depth (U1 chunk, U2 text token, U3 codec token, U4 60-token vocoder
+        call), and from them the config-2 turn (10 s input) by counts.
+    Weights: distinct fp32 arrays for every parameter (copies of one random array per shape: the values do
+    not matter for time, distinct memory does -- each layer streams its own ~0.9 GB from DRAM), ~32 GB of
+    host RAM.  BLAS threads are set before numpy is imported (_blas_threads_from_argv) and verified with
+    threadpoolctl; the cgroup quota is reported beside them."""
     sys.path.insert(0, ROOT)
     from oracle import configs, nets, params
     cfg = configs.get(cfg_name)
     rng = np.random.default_rng(0)
+    base = {}
 
-    class Shared(dict):
+    class Distinct(dict):
         def __init__(self, shapes):
             super().__init__()
-            self.shapes, self.by_shape = shapes, {}
+            self.shapes = shapes
 
         def __missing__(self, k):
             shp = tuple(self.shapes[k])
             pos = k.endswith(("norm.weight", "norm1.weight", "norm2.weight", "layernorm.weight")) or \
                 "running_var" in k or "istd" in k
             key = (shp, pos)
-            if key not in self.by_shape:
+            if key not in base:
                 v = (rng.standard_normal(shp, dtype=np.float32) * np.float32(0.02 if len(shp) > 1 else 0.1))
-                self.by_shape[key] = (np.abs(v) + np.float32(1.0)) if pos else v
-            self[k] = self.by_shape[key]
+                base[key] = (np.abs(v) + np.float32(1.0)) if pos else v
+            self[k] = base[key].copy()
             return self[k]
 
-    W = Shared(params.all_shapes(cfg))
-    for k in W.shapes:   # generate (and first-touch) every shared array before anything is timed
+    W = Distinct(params.all_shapes(cfg))
+    for k in W.shapes:   # materialise (and first-touch) every array before anything is timed
         W[k]
     try:
         from threadpoolctl import threadpool_info, threadpool_limits
@@ -228,57 +411,96 @@ def cpu_baseline(cfg_name, threads, seconds_audio, n_chunks, text_tokens, codec_
         blas_lib = ",".join(sorted({d.get("internal_api", "?") for d in blas}))
     except Exception:   # threadpoolctl missing: the env vars set before the numpy import still hold
         limiter, used, blas_lib = None, threads, "unknown"
+    n_layers = cfg["llm"]["num_hidden_layers"]
+    D = cfg["llm"]["hidden_size"]
+    idim = cfg["decoder_json"][0]
+    n_codes = cfg["codec_json"]["n_codes"]
     try:
         enc, ada = nets.Encoder(W, cfg, "user"), nets.Adapter(W, cfg, "user")
         llm = nets.Qwen2(W, cfg)
-        D = cfg["llm"]["hidden_size"]
-        feats = rng.standard_normal((19, 80)).astype(np.float32) * 3 + 8
-        kv = nets.KV(cfg["llm"]["num_hidden_layers"])
-        llm.forward(rng.standard_normal((40, D)).astype(np.float32), kv)   # system prompt context
-        est = nets.new_encoder_state(enc.nb)
-        ac = None
-        enc.infer(feats, est)   # warm (first-touch page faults of the shared arrays)
+        tts = nets.TTSDecoder(W, cfg)
+        codec = nets.Codec(W, cfg)
+        # ---------------------------------------------------------------- config 1, end to end
+        feats = np.load(os.path.join(ROOT, "tests", "golden", "fbank.npz"))["A_feats"]
+        n_sent = (text_tokens + sentence_tokens - 1) // sentence_tokens
+        per = [codec_tokens // n_sent] * n_sent
+        t0 = time.perf_counter()
+        kv = nets.KV(n_layers)
+        V = cfg["llm"]["vocab_size"]
+
+        def emb(ids):   # Qwen2-7B-Instruct chat-template ids (configs.QWEN2_IDS), folded into a smaller vocabulary
+            return llm.embed([i % V for i in ids])
+
+        llm.forward(emb(list(range(1, 16))), kv)                    # 'pre': the system role (15 tokens)
+        est, ac = nets.new_encoder_state(enc.nb), None
+        for c in range(len(feats)):                                 # listen: 13 chunks
+            e = enc.infer(feats[c], est)
+            a, ac = ada(e, ac)
+            if c == 0:
+                a = np.concatenate([emb([151645, 198, 151644, 872, 198]), a])   # user chat prefix
+            h = llm.forward(a, kv)
+            nets.state_probs(W, h)
+        t_listen = time.perf_counter() - t0
+        h = llm.forward(emb([151645, 198, 151644, 77091, 198]), kv)   # dialog_ss: assistant prefix
+        toks, hids = [], []
+        for j in range(text_tokens):
+            hids.append(h[-1])
+            tok = int(np.argmax(llm.logits(h[-1:])[0]))
+            toks.append(tok)
+            if j < text_tokens - 1:
+                h = llm.forward(llm.embed([tok]), kv)
+        for si in range(n_sent):                                    # speak, sentence by sentence
+            sl = slice(si * sentence_tokens, (si + 1) * sentence_tokens)
+            kvt, P = tts.prefill(llm.embed(toks[sl]).reshape(-1, idim), np.stack(hids[sl]).reshape(-1, idim))
+            cur, ids = tts.vocab + 1, []
+            for _ in range(per[si]):
+                lg = tts.step(cur, kvt, P)
+                cur = int(np.argmax(lg[:n_codes]))                  # EOS masked (benchmark policy)
+                ids.append(cur)
+            for T in vocoder_calls(per[si]):                     # the calls' token counts (which ids: immaterial)
+                codec(np.asarray(ids[:T]))
+        config1 = time.perf_counter() - t0
+        # ---------------------------------------------------------------- units
+        e = enc.infer(feats[0], est)
         t = time.perf_counter()
-        e = enc.infer(feats, est)
+        e = enc.infer(feats[1], est)
         a, ac = ada(e, ac)
         h = llm.forward(a, kv)
         nets.state_probs(W, h)
         u1 = time.perf_counter() - t
         t = time.perf_counter()
-        h = llm.forward(rng.standard_normal((1, D)).astype(np.float32), kv)
+        h = llm.forward(llm.embed([toks[-1]]), kv)
         llm.logits(h)
         u2 = time.perf_counter() - t
-        tts = nets.TTSDecoder(W, cfg)
-        idim = cfg["decoder_json"][0]
         kvt, P = tts.prefill(rng.standard_normal((32, idim)).astype(np.float32),
                              rng.standard_normal((32, idim)).astype(np.float32))
         tts.step(4, kvt, P)
         t = time.perf_counter()
-        n3 = 5
-        for i in range(n3):
+        for i in range(5):
             tts.step(5 + i, kvt, P)
-        u3 = (time.perf_counter() - t) / n3
-        codec = nets.Codec(W, cfg)
+        u3 = (time.perf_counter() - t) / 5
         t = time.perf_counter()
-        codec(rng.integers(0, cfg["codec_json"]["n_codes"], 60))
+        codec(rng.integers(0, n_codes, 60))
         u4 = time.perf_counter() - t
     finally:
         if limiter is not None:
             limiter.restore_original_limits()
-    n_voc = 1 + max(0, (codec_tokens - 50 + 39) // 40)
-    turn = n_chunks * u1 + text_tokens * u2 + codec_tokens * u3 + n_voc * u4
-    speak = text_tokens * u2 + codec_tokens * u3 + n_voc * u4
-    return {"value": round(seconds_audio / turn, 4), "unit": "x real-time (1 user, 1 turn)", "cores": used,
-            "kind": "port",
-            "sample": (f"numpy fp32 oracle (oracle/nets.py) at REAL geometry, {used} BLAS threads ({blas_lib}) of "
-                       f"{os.cpu_count()} host CPUs ({cpu_model()}); one unit of each kind at full depth (24 encoder "
-                       f"blocks, 28 Qwen2 layers, 4 AR layers): U1 chunk {u1 * 1e3:.1f} ms, U2 text token "
-                       f"{u2 * 1e3:.1f} ms, U3 codec token {u3 * 1e3:.2f} ms, U4 vocoder {u4 * 1e3:.1f} ms; "
-                       f"turn = {n_chunks} U1 + {text_tokens} U2 + {codec_tokens} U3 + {n_voc} U4 for "
-                       f"{seconds_audio:.0f} s of speech (counts extrapolated, layers not)"),
-            "speak_rtf_per_user": round(seconds_audio / speak, 4),
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
-            "units_ms": {"U1": u1 * 1e3, "U2": u2 * 1e3, "U3": u3 * 1e3, "U4": u4 * 1e3}}
+    audio1 = codec_tokens * 600 / 24000.0
+    n_voc = n_sent * len(vocoder_calls(codec_tokens // n_sent))
+    turn2 = 63 * u1 + text_tokens * u2 + codec_tokens * u3 + n_voc * u4
+    return {"value": round(audio1 / config1, 4),
+            "unit": f"x real-time (config 1: 1 user, question.wav 2.0 s in, {audio1:.0f} s of speech out)",
+            "cores": used, "kind": "port",
+            "sample": (f"config 1 end to end on the numpy fp32 oracle (oracle/nets.py) at REAL geometry with distinct "
+                       f"weights per layer: {len(feats)} question.wav chunks (listen {t_listen:.2f} s), assistant prefix "
+                       f"+ {text_tokens} text tokens, {n_sent} sentences x {per[0]} codec tokens, {n_voc} vocoder calls"
+                       f" = {config1:.2f} s; {used} BLAS threads ({blas_lib}) within a cgroup quota of {cpu_quota()} "
+                       f"CPUs of {os.cpu_count()} ({cpu_model()})"),
+            "config1_s": round(config1, 3), "config1_listen_s": round(t_listen, 3),
+            "config2_rtf_from_units": round(10.0 / turn2, 4),
+            "host_cpus": os.cpu_count(), "cpu_quota": cpu_quota(), "cpu_model": cpu_model(),
+            "units_ms": {"U1": round(u1 * 1e3, 2), "U2": round(u2 * 1e3, 2), "U3": round(u3 * 1e3, 3),
+                         "U4": round(u4 * 1e3, 2)}}
 
 
 def gather_list(dist, vals, world, dev):
@@ -567,6 +789,10 @@ def main():
                   "first_emit_gated_ms": round((s1["first"][0] - s1["t_ss"]) * 1e3, 2),
                   "rtf_per_user": round(a1 / (s1["last"][0] - s1["t_ss"]), 3)}
     probe = gemm_probe(eng, 2 * args.users)
+    codec_ok, codec_n = codec_ids_check(eng)
+    n_chunks = int(math.ceil(n_samp / 2560))
+    roof_ms, roof_units = turn_roofline(eng, args.users, n_chunks, args.text_tokens,
+                                        [args.codec_tokens // stats[0]["n_sent"]] * stats[0]["n_sent"], base_kv.length)
     if dist is not None:
         t = torch.tensor([wall, audio], dtype=torch.float64, device=dev)
         allw = [torch.zeros_like(t) for _ in range(world)]
@@ -585,8 +811,8 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args.config, args.cpu_threads, args.codec_tokens / 40.0,
-                                   int(math.ceil(n_samp / 2560)), args.text_tokens, args.codec_tokens)
+                cpu = cpu_baseline(args.config, args.cpu_threads, args.text_tokens, args.sentence_tokens,
+                                   args.codec_tokens)
             except Exception as e:  # the baseline is reported, never required for the GPU number
                 cpu = {"value": None, "unit": "x real-time", "cores": args.cpu_threads, "kind": "port",
                        "sample": f"failed: {type(e).__name__}: {e}"}
@@ -599,7 +825,13 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16w-fp32a",
             "data": "synthetic (counter-hash weights at Qwen2-7B + paper geometry; synthetic 16 kHz PCM)",
             "config": {"workload": f"config 3: {args.users} users/GPU, {args.input_sec:.0f} s input (160 ms chunks) "
-                                   f"+ {args.text_tokens} text tokens + {args.codec_tokens} codec tokens per turn",
+                                   f"+ {args.text_tokens} text tokens in {stats[0]['n_sent']} sentences of "
+                                   f"{args.sentence_tokens} + {args.codec_tokens} codec tokens per turn "
+                                   f"({args.codec_tokens // stats[0]['n_sent']} per sentence); each sentence's speech "
+                                   + ("starts at its boundary beside the text decode" if args.concurrent_tts else
+                                      "runs inside the text loop (bin/inference.py order)"),
+                       "text_tokens": args.text_tokens, "sentences": stats[0]["n_sent"],
+                       "codec_tokens": args.codec_tokens,
                        "model": f"Freeze-Omni ({args.config}): speech encoder + adapter + Qwen2-7B + AR decoder + "
                                 "TiCodec", "users_per_gpu": args.users, "global_users": args.users * world,
                        "parallelism": f"dp{world} (session-pinned replicas)"},
@@ -621,12 +853,25 @@ def main():
                          "rocprof_avg_launch_us": None if rp_us is None else round(rp_us, 2),
                          "rocprof_calls": rp_calls,
                          "rocprof_frac": None if rp_us is None else round(probe["bytes"] / (rp_us * 1e-6) / 1e9 / peak, 4),
-                         "rocprof_source": rp_src},
+                         "rocprof_source": rp_src,
+                         # the whole turn against its speed of light: Σ over the turn's units of
+                         # max(bytes / 8 TB/s, FLOPs / 2.5 PF) vs the measured ms per turn, and each stage vs its
+                         # own wall window (text and speak overlap: speak's window starts at dialog_ss too)
+                         "turn_roofline_ms": round(sum(roof_ms.values()), 2),
+                         "turn_frac": round(sum(roof_ms.values()) / (wall / args.steps * 1e3), 4),
+                         "stages": {k: {"ms": round(float(np.median([s["stage"][k] for s in stats])), 2),
+                                        "roofline_ms": round(roof_ms[k], 2),
+                                        "frac": round(roof_ms[k] / float(np.median([s["stage"][k] for s in stats])), 4)}
+                                    for k in ("listen", "text", "speak")},
+                         "units": {k: round(v, 3) for k, v in roof_units.items()}},
+            "codec_ids_exact": {"matched": codec_ok, "total": codec_n,
+                                "source": "tests/golden/real_tts_t2.npz (reference LLM2TTSCodecAR.infer, top_k=1, "
+                                          "real geometry, the bench's own decoder weights)"},
             # wall ms per stage of a timed turn (median over the timed turns): listen = 63 chunks through
             # fbank / encoder / adapter / Qwen2 / state head (pipelined), text = dialog_ss -> the last text
             # token's id on the host, speak = TTS prefill + AR decode + vocoder until the last PCM segment
             "stage_ms": {k: round(float(np.median([s["stage"][k] for s in stats])), 2)
-                         for k in ("listen", "text", "speak")},
+                         for k in ("listen", "text", "speak", "speak_after_text")},
             "single_user": single,
             "cpu_baseline": cpu,
         }

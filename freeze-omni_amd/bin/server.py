@@ -14,10 +14,13 @@ client -> server
                   "time_stamp": float}                               enqueue_audio_data (:330-400)
     prompt       {"text": str}                                       set_prompt (:290-300)
     reset        {}                                                  reset_context (:170-238)
-    register_tm  {"sid": int}       this connection receives that session's 'tm_audio_chunk' stream
+    register_tm  {"sid": int, "token": str}  this connection receives that session's 'tm_audio_chunk' stream;
+                 the token is the one 'started' returned to the session's own connection (a guessed sid
+                 alone is refused), and a session's stream, once registered, is not taken over
     stop         {}                                                  release the session
 server -> client
-    connected {"sid"}, started {"sid"}, error {"message"}, timeout {"sid"}, stopped {"sid"}, and the
+    connected {"sid"}, started {"sid", "token"}, registered {"sid"}, error {"message"}, timeout {"sid"},
+    stopped {"sid"}, and the
     session's emits: vad_state_update, vad_event, dialog_ss, dialog_state_update, tm_audio_chunk.
 
 Sessions are not threads here: one worker thread ticks every replica's DuplexScheduler, which batches
@@ -31,6 +34,7 @@ import base64
 import itertools
 import json
 import os
+import secrets
 import socket
 import socketserver
 import sys
@@ -103,6 +107,7 @@ class DialogServer:
         self.factory, self.max_users, self.timeout, self.tick_sleep = session_factory, max_users, timeout, tick_sleep
         self.hub = Hub()
         self.sessions, self.last_active = {}, {}
+        self.tokens = {}     # sid -> the secret 'started' returned (register_tm must present it)
         self.schedulers = {}
         self.lock = threading.RLock()
         self._sids = itertools.count(1)
@@ -130,7 +135,8 @@ class DialogServer:
             self.schedulers[key].add(s)
             self.sessions[sid] = s
             self.last_active[sid] = time.monotonic()
-        self.hub.emit("started", {"sid": sid}, to=sid)
+            self.tokens[sid] = token = secrets.token_hex(16)
+        self.hub.emit("started", {"sid": sid, "token": token}, to=sid)
 
     def stop(self, sid, event="stopped", drain=False):
         """Release a session; drain=True first prefills everything it has received (a client 'stop')."""
@@ -147,6 +153,7 @@ class DialogServer:
                     sch.tick()
             self.sessions.pop(sid, None)
             self.last_active.pop(sid, None)
+            self.tokens.pop(sid, None)
             if sch is not None:
                 sch.sessions.remove(s)
             s.release()
@@ -164,10 +171,15 @@ class DialogServer:
             return
         if event == "register_tm":
             with self.lock:
-                target = self.sessions.get(int(data["sid"]))
-                if target is None:
-                    raise ValueError(f"no session {data['sid']}")
+                tsid = int(data["sid"])
+                target = self.sessions.get(tsid)
+                token = str(data.get("token", ""))
+                if target is None or not secrets.compare_digest(token, self.tokens.get(tsid, "")):
+                    raise ValueError("register_tm: unknown session or wrong token")   # no hint which
+                if getattr(target, "tm_sid", None) not in (None, sid):
+                    raise ValueError(f"register_tm: session {tsid}'s stream is already registered")
                 target.tm_sid = sid
+            self.hub.emit("registered", {"sid": tsid}, to=sid)
             return
         with self.lock:
             s = self.sessions.get(sid)
@@ -191,9 +203,20 @@ class DialogServer:
 
     # ---------------------------------------------------------------- worker
     def tick(self):
-        """One batched prefill per replica; the sessions emit their results.  Returns the work count."""
+        """One batched prefill per replica; the sessions emit their results.  Returns the work count.  A
+        replica whose prefill fails reports it to the sessions of that batch only (the others go on)."""
+        n = 0
         with self.lock:
-            return sum(len(sch.tick()) for sch in list(self.schedulers.values()) if sch.sessions)
+            for sch in list(self.schedulers.values()):
+                if not sch.sessions:
+                    continue
+                try:
+                    n += len(sch.tick())
+                except Exception as e:
+                    members = [sid for sid, s in self.sessions.items() if s in sch.sessions]
+                    for sid in members:
+                        self.hub.emit("error", {"message": f"prefill failed: {e}"}, to=sid)
+        return n
 
     def _reap(self):
         now = time.monotonic()
@@ -208,14 +231,7 @@ class DialogServer:
 
     def _run(self):
         while not self._stop.is_set():
-            try:
-                n = self.tick()
-            except Exception as e:   # a failing prefill must not kill the transport: report it
-                n = 0
-                with self.hub.lock:
-                    sids = list(self.hub.conns)
-                for sid in sids:
-                    self.hub.emit("error", {"message": f"prefill failed: {e}"}, to=sid)
+            n = self.tick()   # a failing prefill is reported to its batch's sessions, never kills the transport
             self._reap()
             if n == 0:
                 time.sleep(self.tick_sleep)

@@ -65,16 +65,29 @@ def make_source(cfg, synth, device, model_path=None, llm_path=None, receive=Fals
 
 class FreezeOmniEngine:
     def __init__(self, model_path, llm_path=None, device="cuda:0", max_sessions=64, llm_kv_tokens=None,
-                 tts_kv_tokens=None, source=None, receive_weights=False):
+                 tts_kv_tokens=None, source=None, receive_weights=False, train_yaml=None):
         """receive_weights=True: allocate every packed layout without reading or generating weights; the
-        caller fills them with fo.replica.broadcast_frozen(engine, dist) from rank 0 before any use."""
+        caller fills them with fo.replica.broadcast_frozen(engine, dist) from rank 0 before any use.
+        train_yaml: the parsed audiollm/train.yaml as a dict (models/utils.py:init_encoder_llm's configs) in
+        place of the file; its cmvn_file, when present on disk, supplies the CMVN statistics
+        (models/utils.py:31-38)."""
         if not torch.cuda.is_available():
             raise RuntimeError("FreezeOmniEngine needs an MI355X (gfx950) device: there is no CPU fallback")
         self.device = torch.device(device)
         torch.cuda.set_device(self.device)
         self.cfg, self.synth, self.llm_path = load_model_dir(model_path, llm_path)
+        if train_yaml is not None:
+            self.cfg["train_yaml"] = train_yaml
         src = source or make_source(self.cfg, self.synth, self.device, model_path, self.llm_path,
                                     receive=receive_weights)
+        cmvn = (train_yaml or {}).get("cmvn_file")
+        if cmvn and os.path.exists(cmvn) and not receive_weights:
+            from .checkpoint import load_cmvn
+            from .weights import CheckpointSource, OverlaySource
+            mean, istd = load_cmvn(cmvn, bool(self.cfg["train_yaml"].get("is_json_cmvn", True)))
+            st = {f"encoder_{i}.global_cmvn.{n}": torch.from_numpy(np.asarray(v, np.float32))
+                  for i in ("user", "system") for n, v in (("mean", mean), ("istd", istd))}
+            src = OverlaySource(CheckpointSource(st, self.device), src)
         self.src = src
         self.max_sessions = max_sessions
         ty = self.cfg["train_yaml"]

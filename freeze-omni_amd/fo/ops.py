@@ -24,14 +24,15 @@ def stream(device=None):
 _ENGINE_STREAMS = {}
 
 
-def engine_stream(device, side=False):
+def engine_stream(device, side=False, name=None):
     """A blocking HIP stream per device (fo_stream_create) wrapped for torch: it orders against the
     legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it.
-    side=True: a second such stream, for work that overlaps the main one (pipelined listen stages)."""
+    side=True: a second such stream, for work that overlaps the main one (pipelined listen stages).
+    name: further named streams ("tts", "voc": speech generation running beside the text decode)."""
     import ctypes
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
-    key = (idx, bool(side))
+    key = (idx, name if name is not None else bool(side))
     if key not in _ENGINE_STREAMS:
         h = ctypes.c_void_p()
         with torch.cuda.device(idx):

@@ -7,10 +7,14 @@ point-to-point: large messages keep every ring link busy) instead of hundreds of
 """
 import torch
 
-# per-session / scratch state that must not be broadcast (it is replica-local by design)
-_SKIP_CLASSES = {"KVPool", "KVSeq", "Runtime", "SlotPool", "EncoderCache", "AdapterCache", "Framer"}
+# per-session / scratch state that must not be broadcast (it is replica-local by design), including the
+# captured-graph caches a warm-up fills lazily (decode / text / listen graphs, vocoder buffers, fbank tables),
+# so a replica that has run work before the broadcast walks the same storage list as one that has not
+_SKIP_CLASSES = {"KVPool", "KVSeq", "Runtime", "SlotPool", "EncoderCache", "AdapterCache", "Framer", "DecodeGraph",
+                 "TextGraph", "ListenGraph", "ListenPipe", "FbankGPU", "HostBuffer", "SampleCheck", "_HostRing"}
 _FOREIGN = {"torch", "numpy", "builtins", "ctypes", "transformers", "tokenizers", "threading", "logging"}
-_SKIP_ATTRS = {"ws", "counters", "part_ml", "part_o", "scratch", "src"}
+_SKIP_ATTRS = {"ws", "counters", "part_ml", "part_o", "scratch", "src", "_graphs", "_lgraphs", "_tgraphs", "_fbank",
+               "host", "meta_d", "hist", "err"}
 
 
 def frozen_tensors(root):
@@ -101,3 +105,23 @@ def frozen_checksum(root):
         tail = int(b[n4:].to(torch.int64).sum().item()) if b.numel() > n4 else 0
         acc = (acc * 1000003 + w + tail + i) & ((1 << 63) - 1)
     return acc
+
+
+def copy_frozen(src_root, dst_root):
+    """Fill a receive-only replica in the SAME process (fo.weights.ReceiveSource layouts, e.g. on another GPU
+    of the node) from a loaded one: every frozen storage copied device to device (a peer copy over xGMI
+    between GPUs), in the walk order broadcast_frozen uses, then checked by frozen_checksum.  The in-process
+    form of the start-up broadcast (bin/pool.py's `devices` replicas), so one design serves both.
+    Returns the bytes copied."""
+    src, dst = frozen_storages(src_root), frozen_storages(dst_root)
+    if len(src) != len(dst) or any(a.numel() != b.numel() for a, b in zip(src, dst)):
+        raise RuntimeError(f"copy_frozen: the replicas' frozen layouts differ ({len(src)} vs {len(dst)} storages)")
+    total = 0
+    for a, b in zip(src, dst):
+        b.copy_(a)
+        total += a.numel()
+    for r in {t.device for t in src} | {t.device for t in dst}:
+        torch.cuda.synchronize(r)
+    if frozen_checksum(src_root) != frozen_checksum(dst_root):
+        raise RuntimeError("copy_frozen: replica weights differ from the source after the copy")
+    return total

@@ -47,7 +47,7 @@ def silence_cut(buffer, syn, N, threshold, res, r=None):
 
 def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
           max_tokens=1000, min_tokens=0, states_out=None, seed=0, graph=True, window=32, penalty_window_size=-1,
-          penalty=1.1):
+          penalty=1.1, stream=None, voc_stream=None):
     """items: list of (hidden [T1, D] device, prefix [T2, D] device or None).
     min_tokens > 0 masks EOS until that many tokens (benchmark policy).
     Yields (session index, pcm segment device 1-D) as segments become available; the per-session
@@ -55,9 +55,12 @@ def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=
     graph=True replays a captured decode step (fo.tts.DecodeGraph) and reads sampled ids back lazily,
     up to `window` steps behind the GPU; graph=False is the step-by-step eager loop.  Both produce the
     same ids (same kernels, same RNG stream).
-    penalty_window_size > 0 applies the reference's repetition penalty (decoder.py:348-351, fo_penalty)."""
+    penalty_window_size > 0 applies the reference's repetition penalty (decoder.py:348-351, fo_penalty).
+    stream / voc_stream: the streams of the AR decode and of the vocoder (default: the engine's main and side
+    streams); the bench's concurrent speech generation runs on its own pair beside the text decode."""
     pen = (int(penalty_window_size), float(penalty)) if penalty_window_size and penalty_window_size > 0 else None
-    es = ops.engine_stream(engine.device)
+    es = stream if stream is not None else ops.engine_stream(engine.device)
+    vs = voc_stream if voc_stream is not None else ops.engine_stream(engine.device, side=True)
     with torch.cuda.stream(es):
         seqs = engine.tts.start(items)
     states = [SpeakState(sq, top_k, max_tokens, min_tokens) for sq in seqs]
@@ -65,7 +68,7 @@ def speak(engine, items, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=
         states_out.extend(states)
     run = _speak_graph if graph else _speak_eager
     gen = run(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens, min_tokens,
-              seed, window, pen)
+              seed, window, pen, voc=vs)
     try:
         while True:
             with torch.cuda.stream(es):  # the engine stream is current only while engine code runs
@@ -94,25 +97,25 @@ def _after_token(states, i, t, eos, chunk_due, finished, codec_chunk_size, codec
         finished.append(i)
 
 
-def _emit(engine, states, chunk_due, finished, up, pad, N, thr, res):
+def _emit(engine, states, chunk_due, finished, up, pad, N, thr, res, voc):
     segs = []
     if chunk_due:
-        segs += list(_vocode(engine, states, chunk_due, up, pad, N, thr, res, final=False))
+        segs += list(_vocode(engine, states, chunk_due, up, pad, N, thr, res, voc, final=False))
     if finished:
-        segs += list(_vocode(engine, states, [i for i in finished if states[i].tokens], up, pad, N, thr, res,
+        segs += list(_vocode(engine, states, [i for i in finished if states[i].tokens], up, pad, N, thr, res, voc,
                              final=True))
     return segs
 
 
 def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
-                 min_tokens, seed, window, pen=None):
+                 min_tokens, seed, window, pen=None, voc=None):
     tts = engine.tts
     if tts.fused:
         # the fused step (fo_tts_step) launched directly, one step at a time with an id read-back each: the
         # eager form of the captured graph path (same kernel; steps outside its contract fall back to the
         # multi-kernel body inside DecodeGraph)
         yield from _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold,
-                                max_tokens, min_tokens, seed, 1, pen, capture=False)
+                                max_tokens, min_tokens, seed, 1, pen, capture=False, voc=voc)
         return
     dev = engine.device
     up = engine.codec.upsample
@@ -140,7 +143,7 @@ def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
         finished, chunk_due = [], []
         for j, i in enumerate(live):
             _after_token(states, i, ids[j], tts.eos, chunk_due, finished, codec_chunk_size, codec_padding_size)
-        segs = _emit(engine, states, chunk_due, finished, up, codec_padding_size, N, seg_threshold, res)
+        segs = _emit(engine, states, chunk_due, finished, up, codec_padding_size, N, seg_threshold, res, voc)
         live = [i for i in live if not states[i].done]
         if live:
             cur = torch.tensor([states[i].all_ids[-1] for i in live], dtype=I32).to(dev)
@@ -149,7 +152,7 @@ def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
 
 
 def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
-                 min_tokens, seed, window, pen=None, capture=True):
+                 min_tokens, seed, window, pen=None, capture=True, voc=None):
     tts = engine.tts
     dev = engine.device
     up = engine.codec.upsample
@@ -187,7 +190,7 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
         for j, i in enumerate(batch):
             if not states[i].done:
                 _after_token(states, i, row[j], tts.eos, chunk_due, finished, codec_chunk_size, codec_padding_size)
-        segs = _emit(engine, states, chunk_due, finished, up, codec_padding_size, N, seg_threshold, res)
+        segs = _emit(engine, states, chunk_due, finished, up, codec_padding_size, N, seg_threshold, res, voc)
         if finished:
             # the batch shrinks: drain what was launched with the old batch (finished rows are ignored),
             # then continue with a graph for the survivors, seeded with their last ids
@@ -200,7 +203,7 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
                 for j, i in enumerate(batch):
                     if not states[i].done:
                         _after_token(states, i, row[j], tts.eos, due2, fin2, codec_chunk_size, codec_padding_size)
-                segs += _emit(engine, states, due2, fin2, up, codec_padding_size, N, seg_threshold, res)
+                segs += _emit(engine, states, due2, fin2, up, codec_padding_size, N, seg_threshold, res, voc)
             live = [i for i in live if not states[i].done]
             g = None
         if step >= max_tokens and not pending:
@@ -209,18 +212,18 @@ def _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N,
             for i in rest:
                 states[i].done = True
             segs += _emit(engine, states, [], [i for i in rest if states[i].tokens], up, codec_padding_size, N,
-                          seg_threshold, res)
+                          seg_threshold, res, voc)
             live = []
         if segs:
             yield segs
 
 
-def _vocode(engine, states, idx, up, pad, N, thr, res, final):
-    """One batched vocoder call for sessions idx (equal token counts share a launch), on the engine's
-    side stream: the MFMA-bound vocoder overlaps the launch-bound AR decode steps already queued on
-    the engine stream instead of stalling them (the side stream is blocking w.r.t. the legacy default
-    stream, so callers reading the yielded PCM there are ordered after it)."""
-    with torch.cuda.stream(ops.engine_stream(engine.device, side=True)):
+def _vocode(engine, states, idx, up, pad, N, thr, res, voc, final):
+    """One batched vocoder call for sessions idx (equal token counts share a launch), on the vocoder stream
+    (the engine's side stream by default): the MFMA-bound vocoder overlaps the launch-bound AR decode steps
+    already queued on the decode stream instead of stalling them (the stream is blocking w.r.t. the legacy
+    default stream, so callers reading the yielded PCM there are ordered after it)."""
+    with torch.cuda.stream(voc if voc is not None else ops.engine_stream(engine.device, side=True)):
         yield from _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final)
 
 
@@ -243,7 +246,7 @@ def _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final):
             syn = pcm[j]
             if final:
                 if s.t_first_pcm is None:
-                    torch.cuda.synchronize(engine.device)
+                    torch.cuda.current_stream(engine.device).synchronize()   # this call's PCM (not the other streams)
                     s.t_first_pcm = time.perf_counter()
                 syn = syn[s.left * up:]
                 seg = syn if s.buffer is None or s.buffer.numel() == 0 else torch.cat([s.buffer, syn])

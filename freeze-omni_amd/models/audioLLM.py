@@ -59,17 +59,6 @@ class _LLMDecoder:
         self.transformer.wte = self.model.embed_tokens
 
 
-class _EncoderView:
-    def __init__(self, eng):
-        self.num_blocks = eng.nb
-
-
-class _Encoder:
-    def __init__(self, eng):
-        self.engine = eng
-        self.enc = [None, _EncoderView(eng)]
-
-
 class AudioLLM:
     def __init__(self, engine: FreezeOmniEngine, top_k=1, top_p=0.0, temperature=1.0):
         self.engine = engine
@@ -78,8 +67,7 @@ class AudioLLM:
         self.chat_template = None if engine.chat_template is None else {
             k: torch.tensor([v]) for k, v in engine.chat_template.items()}
         self.llm_decoder = _LLMDecoder(engine)
-        self.encoder_user = _Encoder(engine.enc["user"])
-        self.encoder_system = _Encoder(engine.enc["system"])
+        self._views()
         self.predictor_head = engine.llm.head_w
         self.top_k, self.top_p, self.temperature = top_k, top_p, temperature
         self.logger = None
@@ -87,15 +75,24 @@ class AudioLLM:
     def rebind(self, loaded=None):
         """Refresh the views on the engine after models.utils.load_checkpoint re-packed weights."""
         eng = self.engine
-        self.encoder_user = _Encoder(eng.enc["user"])
-        self.encoder_system = _Encoder(eng.enc["system"])
+        self._views()
         self.predictor_head = eng.llm.head_w
         self.llm_decoder = _LLMDecoder(eng)
         return loaded
 
+    def _views(self):
+        """encoder_user / encoder_system / adpter_user / adpter_system as the reference names them
+        (models/audioLLM.py:67-68,159-166): speechEncoder / CNNSubsampling facades over the engine's own."""
+        from models.adapter import CNNSubsampling
+        from models.encoder.encoder import speechEncoder
+        for i in ("user", "system"):
+            setattr(self, f"encoder_{i}", speechEncoder(self.engine.enc[i]))
+            setattr(self, f"adpter_{i}", CNNSubsampling(self.engine.ada[i]))
+
     @classmethod
-    def from_model_dir(cls, model_path, llm_path=None, device="cuda:0", **kw):
-        return cls(FreezeOmniEngine(model_path, llm_path, device=device), **kw)
+    def from_model_dir(cls, model_path, llm_path=None, device="cuda:0", train_yaml=None, receive_weights=False, **kw):
+        return cls(FreezeOmniEngine(model_path, llm_path, device=device, train_yaml=train_yaml,
+                                    receive_weights=receive_weights), **kw)
 
     def setup_logger(self, parent_logger=None):
         if parent_logger is not None:

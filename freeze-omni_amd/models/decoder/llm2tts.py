@@ -14,17 +14,21 @@ from fo.tts import TTSEngine
 
 
 class _SpeechEngine:
-    def __init__(self, model_path, device):
+    def __init__(self, model_path, device, receive=False):
         self.device = torch.device(device)
         self.cfg, synth, _ = load_model_dir(model_path)
-        src = make_source(self.cfg, synth, self.device)
+        src = make_source(self.cfg, synth, self.device, model_path, receive=receive)
         self.tts = TTSEngine(src, self.cfg["decoder_json"], self.device)
         self.codec = CodecEngine(src, self.cfg["codec_json"], self.device)
 
 
 class llm2TTS:
-    def __init__(self, model_path, device="cuda:0"):
-        self.engine = _SpeechEngine(model_path, device)
+    def __init__(self, model_path, device="cuda:0", weights_from=None):
+        """weights_from: another llm2TTS whose frozen weights this one copies (fo.replica.copy_frozen)."""
+        self.engine = _SpeechEngine(model_path, device, receive=weights_from is not None)
+        if weights_from is not None:
+            from fo.replica import copy_frozen
+            copy_frozen(weights_from.engine, self.engine)
         self.model = self.engine.tts          # .vocab_size mirrors LLM2TTSCodecAR.vocab_size
         self.model.vocab_size = self.engine.tts.vocab
         self.codec_model = self.engine.codec

@@ -39,3 +39,15 @@ def load_kaldi_cmvn(path):
 
 def load_cmvn(cmvn_file, is_json):
     return load_json_cmvn(cmvn_file) if is_json else load_kaldi_cmvn(cmvn_file)
+
+
+class GlobalCMVN:
+    """GlobalCMVN(mean, istd, norm_var=True) (reference: models/encoder/cmvn.py:7-35): the statistics a
+    speechEncoder folds into its first kernel ((x - mean) * istd; norm_var=False subtracts the mean only).
+    It is a parameter holder here: the normalisation runs inside the encoder's im2col on the device."""
+
+    def __init__(self, mean, istd, norm_var=True):
+        import torch
+        self.mean = torch.as_tensor(mean).float()
+        self.istd = torch.as_tensor(istd).float() if norm_var else torch.ones_like(self.mean)
+        self.norm_var = norm_var

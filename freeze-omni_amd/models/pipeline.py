@@ -24,7 +24,10 @@ _UPSTREAM_TO_STATUS = {"dialog_sl": "ipu_sl", "dialog_cl": "ipu_cl", "dialog_el"
 
 
 class inferencePipeline:
-    def __init__(self, args):
+    def __init__(self, args, weights_from=None):
+        """weights_from: another inferencePipeline (any device) whose frozen weights this replica copies
+        instead of reading / generating its own (fo.replica.copy_frozen: the in-process form of the
+        start-up broadcast, bin/pool.py's `devices` replicas)."""
         if isinstance(args, argparse.Namespace):
             args = vars(args)
         self.args = args
@@ -35,7 +38,12 @@ class inferencePipeline:
         self.model = AudioLLM.from_model_dir(args["model_path"], args.get("llm_path"), device=self.device,
                                              top_k=top_k if top_k is not None else 1,
                                              top_p=args.get("top_p", 0.0) or 0.0,
-                                             temperature=args.get("temperature", 1.0) or 1.0)
+                                             temperature=args.get("temperature", 1.0) or 1.0,
+                                             receive_weights=weights_from is not None)
+        if weights_from is not None:
+            from fo.replica import copy_frozen
+            copy_frozen(weights_from.model.engine, self.model.engine)
+            self.model.rebind()
         self.model.init_template_compilation()
         self.logger = None
 

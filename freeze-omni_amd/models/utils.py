@@ -5,14 +5,20 @@ from models.audioLLM import AudioLLM
 
 
 def init_encoder_llm(configs, device="cuda:0", model_path=None, llm_path=None):
-    """Build the AudioLLM for a model directory.  `configs` is the parsed train.yaml as in the
-    reference; the MI355X engine reads the same files itself, so model_path must be given (or
-    configs['model_path'])."""
-    mp = model_path or configs.get("model_path")
+    """models/utils.py:30-49 with the reference's `configs`: the parsed train.yaml carrying the cmvn_file and
+    model_conf.llm_path that inferencePipeline injects (models/pipeline.py:21-24).  The model directory is the
+    one cmvn_file sits in (<model_path>/audiollm/global_cmvn) unless model_path is given; its decoder and codec
+    configs and weights (or synthetic.json) load with it, the CMVN statistics come from cmvn_file when it
+    exists, and the train.yaml settings are the dict's (not the file's)."""
+    import copy
+    configs = copy.deepcopy(configs)
+    cmvn = configs.get("cmvn_file")
+    mp = model_path or configs.get("model_path") or (os.path.dirname(os.path.dirname(cmvn)) if cmvn else None)
     if mp is None:
-        raise ValueError("init_encoder_llm: pass model_path (directory holding audiollm/train.yaml)")
+        raise ValueError("init_encoder_llm: configs carry no cmvn_file (models/pipeline.py:23 sets "
+                         "<model_path>/audiollm/global_cmvn); pass model_path")
     lp = llm_path or configs.get("model_conf", {}).get("llm_path") or os.path.join(mp, "llm")
-    return AudioLLM.from_model_dir(mp, lp, device=device)
+    return AudioLLM.from_model_dir(mp, lp, device=device, train_yaml=configs)
 
 
 def load_checkpoint(model, path):

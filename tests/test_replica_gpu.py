@@ -77,3 +77,24 @@ def test_receive_only_replica_matches_after_broadcast(dev):
     assert pa == pb
     assert ia == ib and len(ia) >= 45
     assert torch.equal(wa, wb)
+
+
+def test_pool_devices_replicas_copy_the_first_replicas_weights(dev):
+    """bin/pool.py's `devices` mode: the first replica loads, the others are receive-only and filled by
+    fo.replica.copy_frozen (device-to-device; here both on cuda:0), checksum-verified, and serve the same
+    results; a warm-up run on the source before the copy (graph caches filled) does not change the walk."""
+    from bin.pool import pipelineObjectPool
+    from fo.replica import copy_frozen, frozen_checksum
+    from fo.engine import FreezeOmniEngine
+    a = FreezeOmniEngine(TINY, device=dev, max_sessions=4)
+    pa, ia, wa = _run(a, dev)                       # warm: decode / listen / vocoder graphs exist now
+    b = FreezeOmniEngine(TINY, device=dev, max_sessions=4, receive_weights=True)
+    assert copy_frozen(a, b) > 0 and frozen_checksum(a) == frozen_checksum(b)
+    pb, ib, wb = _run(b, dev)
+    assert (pa, ia) == (pb, ib) and torch.equal(wa, wb)
+    pool = pipelineObjectPool(2, {"model_path": TINY, "llm_path": os.path.join(TINY, "llm"),
+                                  "devices": [str(dev), str(dev)], "top_k": 1})
+    e0, e1 = (o.pipeline_proc.model.engine for o in pool.pool)
+    assert frozen_checksum(e0) == frozen_checksum(e1)
+    assert _run(e0, dev)[:2] == _run(e1, dev)[:2]
+    assert pool.acquire() is not pool.acquire()   # least-loaded: the two sessions land on different replicas

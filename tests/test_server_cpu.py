@@ -75,8 +75,17 @@ def test_server_streams_session_events_and_tm_chunks():
     try:
         # user speech from 0.3 s to 1.5 s (chunk centres 0.112, 0.336, ... step 0.224)
         c.send("start", {"vad_intervals": [[0.3, 1.5]]})
-        assert c.wait("started")["sid"] == c.sid
+        st = c.wait("started")
+        assert st["sid"] == c.sid
+        # a guessed sid without the session's token is refused, and so is a second registration
         tm.send("register_tm", {"sid": c.sid})
+        assert "wrong token" in tm.wait("error")["message"]
+        tm.send("register_tm", {"sid": c.sid, "token": st["token"]})
+        assert tm.wait("registered")["sid"] == c.sid
+        spy = DialogClient(host, port)
+        spy.send("register_tm", {"sid": c.sid, "token": st["token"]})
+        assert "already registered" in spy.wait("error")["message"]
+        spy.close()
         n = 9
         for k in range(n):
             c.send_audio("user", _pcm(0.2, k), k * CH / 16000)
