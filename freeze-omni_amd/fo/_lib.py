@@ -20,20 +20,6 @@ c_ll = ctypes.c_longlong
 c_float = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-TTS_MAXL = 8   # FO_TTS_MAXL
-
-
-class FoTtsStep(ctypes.Structure):
-    """include/fo_hip.h FoTtsStep: the arguments of one fused AR speech-decoder step (fo_tts_step)."""
-    _fields_ = ([(n, c_int) for n in ("B", "D", "H", "hd", "F", "nl", "V", "V_sample", "PS", "maxb", "S")] +
-                [(n, c_float) for n in ("eps", "scale", "penalty")] + [("W", c_int), ("seed", ctypes.c_ulonglong)] +
-                [(n, c_vp * TTS_MAXL) for n in ("wqkv", "wo", "wgu", "wdown", "ln1", "ln2", "kc", "vc")] +
-                [(n, c_vp) for n in ("norm", "wout", "bout", "emb")] + [("emb_ld", c_ll)] +
-                [(n, c_vp) for n in ("cos_t", "sin_t", "tok_pos", "tok_slot", "tok_nvis", "step", "key", "hist_row",
-                                     "block_table", "top_k", "win", "x", "ids", "hist")] + [("hist_ld", c_int)] +
-                [(n, c_vp) for n in ("logits", "ws", "bar", "err", "trace")])
-
-
 # name -> (restype, argtypes)
 _SIGS = {
     "fo_version": (c_int, []),
@@ -58,8 +44,6 @@ _SIGS = {
     "fo_gemm_set_xs": (c_int, [c_int]),
     "fo_gemm_set_merge": (c_int, [c_int]),
     "fo_gemm_set_trace": (c_int, [c_vp]),
-    "fo_tts_step_ws_floats": (c_ll, [c_int, c_int, c_int, c_int, c_int]),
-    "fo_tts_step": (c_int, [ctypes.POINTER(FoTtsStep), c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),

@@ -110,13 +110,6 @@ def _emit(engine, states, chunk_due, finished, up, pad, N, thr, res, voc):
 def _speak_eager(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold, max_tokens,
                  min_tokens, seed, window, pen=None, voc=None):
     tts = engine.tts
-    if tts.fused:
-        # the fused step (fo_tts_step) launched directly, one step at a time with an id read-back each: the
-        # eager form of the captured graph path (same kernel; steps outside its contract fall back to the
-        # multi-kernel body inside DecodeGraph)
-        yield from _speak_graph(engine, states, top_k, codec_chunk_size, codec_padding_size, N, seg_threshold,
-                                max_tokens, min_tokens, seed, 1, pen, capture=False, voc=voc)
-        return
     dev = engine.device
     up = engine.codec.upsample
     res = torch.empty(2, dtype=F32, device=dev)

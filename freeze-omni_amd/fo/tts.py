@@ -103,61 +103,6 @@ class TTSEngine:
             s.generated += 1
         return self.out_fnn(ws["xg"][:B], norm=(ws["sA"], self.eps))
 
-    # the fused one-launch decode step (fo_tts_step) where its contract holds, opt-in (FO_TTS_FUSED=1):
-    # measured at real geometry, 8 sessions, 285 keys (scripts/tts_step_time.py, profiles/r02m_*): 257 us per
-    # step against 181 us for the multi-kernel step -- each device barrier still ends ~2.8 us after its last
-    # arrival and every phase that reads another workgroup's output pays a 2-3 us memory round trip first
-    # (q|k|v staging 6 us, down 10 us), so the 21-barrier step does not beat ~27 graph nodes of ~5-7 us
-    # yet.  Correct (tests/test_tts_step_gpu.py), not the default.
-    fused = os.environ.get("FO_TTS_FUSED", "0") == "1"
-    FUSED_KMAX = 64
-
-    def fused_step_args(self, g):
-        """FoTtsStep for DecodeGraph g, or None when the step is outside the fused kernel's contract
-        (then the graph keeps the multi-kernel body)."""
-        L = self.main.layers
-        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-        S = max(1, -(-g.max_keys // 1024))
-        while S < 4 and g.B * self.H * (S + 1) <= ncu and g.max_keys > 256 * S:
-            S += 1
-        top_k = int(g.topk[0].item())
-        ok = (self.hd in (32, 64) and self.D % 128 == 0 and self.D <= 1024 and len(L) <= _lib.TTS_MAXL and g.B <= 16 and
-              1 <= top_k <= self.FUSED_KMAX and L[0].qkv.bias is None and g.B * self.H * S <= ncu and
-              -(-g.max_keys // S) <= 1024 and max(3 * self.D // 32, (self.D // 16) * 2, (self.vocab + 19) // 16) <= ncu
-              and (L[0].gu.N // 32) % 2 == 0)
-        if not ok:
-            return None
-        a = _lib.FoTtsStep()
-        a.B, a.D, a.H, a.hd, a.F, a.nl = g.B, self.D, self.H, self.hd, L[0].gu.N, len(L)
-        a.V, a.V_sample = g.logits.shape[1], g.V_sample
-        a.PS, a.maxb, a.S = self.pool.PS, g.maxb, S
-        a.eps, a.scale = self.eps, self.hd ** -0.5
-        a.penalty, a.W = (float(g.pen[1]), int(g.pen[0])) if g.pen else (1.0, 0)
-        a.seed = int(g.seed) & 0xFFFFFFFFFFFFFFFF
-        for i, ly in enumerate(L):
-            a.wqkv[i], a.wo[i] = ly.qkv.packed.data_ptr(), ly.o.packed.data_ptr()
-            a.wgu[i], a.wdown[i] = ly.gu.packed.data_ptr(), ly.down.packed.data_ptr()
-            a.ln1[i], a.ln2[i] = ly.ln1.data_ptr(), ly.ln2.data_ptr()
-            a.kc[i], a.vc[i] = self.pool.k[self.main.kv_layer0 + i].data_ptr(), self.pool.v[self.main.kv_layer0 + i].data_ptr()
-        a.norm, a.wout = self.norm.data_ptr(), self.out_fnn.packed.data_ptr()
-        a.bout = self.out_fnn.bias.data_ptr() if self.out_fnn.bias is not None else None
-        a.emb, a.emb_ld = self.embedding.data_ptr(), self.embedding.stride(0)
-        a.cos_t, a.sin_t = self.main.cos.data_ptr(), self.main.sin.data_ptr()
-        m = g.meta
-        a.tok_pos, a.tok_slot, a.tok_nvis = m.tok_pos.data_ptr(), m.tok_slot.data_ptr(), m.tok_nvis.data_ptr()
-        a.step, a.key, a.hist_row = m.step.data_ptr(), m.key.data_ptr(), m.hist_row.data_ptr()
-        a.block_table, a.top_k = m.block_table.data_ptr(), g.topk.data_ptr()
-        a.win = g.win.data_ptr() if g.win is not None else None
-        a.x, a.ids, a.logits = g.x.data_ptr(), g.ids.data_ptr(), g.logits.data_ptr()
-        a.hist, a.hist_ld = g.hist.dev, g.B
-        g._fws = torch.empty(_lib.load().fo_tts_step_ws_floats(self.D, self.H, self.hd, a.F, S), dtype=F32,
-                             device=self.device)
-        g._bar = torch.zeros(256, dtype=I32, device=self.device)
-        g._err = ops.HostBuffer(1, 1)   # host-mapped: read after a step's event, no device sync
-        g._err.np[0, 0] = 0
-        a.ws, a.bar, a.err = g._fws.data_ptr(), g._bar.data_ptr(), g._err.dev
-        return a
-
     def embed_input(self, tokens, ws, B, x=None):
         """x = embedding[tokens] (fp32) and ws["h"] = the first layer's RMSNorm of it: the decode step's
         input, as fo_sample_embed writes it for the next step inside the captured graph."""
@@ -168,8 +113,8 @@ class TTSEngine:
     def decode_graph(self, B, V_sample, top_k, seed, max_keys, hist_rows, pen=None, capture=True):
         """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows).
         pen = (window, penalty) adds the repetition penalty before the draw (None: off).
-        capture=False: the same step body launched directly each step (the eager loop of the fused path)."""
-        key = (B, V_sample, top_k, seed, pen, bool(self.fused), capture)
+        capture=False: the same step body launched directly each step (no graph)."""
+        key = (B, V_sample, top_k, seed, pen, capture)
         g = self._graphs.get(key) if hasattr(self, "_graphs") else None
         if g is None or g.max_keys < max_keys or g.hist_rows < hist_rows:
             if not hasattr(self, "_graphs"):
@@ -215,7 +160,7 @@ class DecodeGraph:
         self.pen = pen
         # the captured step advances its own metadata for the next step (inside the sampler launch); the host
         # uploads a fresh block only when the batch, its RNG keys or a session's page list changed
-        self.advance = capture and not tts.fused
+        self.advance = capture
         self._uploaded = None
         self.win = torch.full((B, pen[0]), -1, dtype=I32, device=dev) if pen else None
         PS = tts.pool.PS
@@ -239,7 +184,6 @@ class DecodeGraph:
         self.topk = torch.tensor([top_k] * B, dtype=I32).to(dev)
         self.ws = tts.main.workspace(B, ops.attn_nsplit(max_keys, B, tts.H), dev)
         self.err = ops.SampleCheck()   # NaN / inf logits rows (the reference's multinomial raises on them)
-        self.fused = tts.fused_step_args(self) if tts.fused else None
         self.events = []
         for _ in range(self.RING):
             e = ctypes.c_void_p()
@@ -252,9 +196,6 @@ class DecodeGraph:
     def _body(self):
         # x / ws["h"] hold this step's input (prime() or the previous replay's sampler); the sampler
         # records the drawn ids and writes the next step's input rows (fo_sample_embed)
-        if self.fused is not None:   # the whole step as one persistent kernel (fo_tts_step)
-            _lib.call("fo_tts_step", ctypes.byref(self.fused), ops.stream(self.tts.device))
-            return
         t = self.tts
         t.main.forward(self.x, self.meta, self.ws, pre_normed=True, final_norm=t.norm)
         t.out_fnn(self.ws["xg"], out=self.logits, norm=(self.ws["sA"], t.eps))
@@ -281,10 +222,8 @@ class DecodeGraph:
 
     def check(self):
         """After a step's event: raise if a logits row was NaN / inf (the reference's torch.multinomial raises,
-        decoder.py:355-359) or a fused step's device barrier timed out (it never blocks: it gives up and flags)."""
+        decoder.py:355-359)."""
         self.err.check("speech decode step")
-        if self.fused is not None and int(self._err.np[0, 0]) != 0:
-            raise RuntimeError("fo_tts_step: a device barrier timed out (workgroups not co-resident)")
 
     def _capture(self):
         s = ops.stream(self.tts.device)
@@ -362,5 +301,3 @@ class DecodeGraph:
         self.events = []
         self.hist.free()
         self.err.free()
-        if self.fused is not None:
-            self._err.free()

@@ -265,58 +265,6 @@ int fo_sample_embed(const float* logits, int ld, int B, int V, const int* top_k,
 int fo_penalty(float* logits, int ld, int B, int V, const int* ids, int* win, int W, const int* step, float penalty,
                hipStream_t s);
 
-/* ---------------------------------------------------------------- AR speech-decoder step, one launch
- * One decode step of LLM2TTSCodecAR (models/decoder/decoder.py:341-367: embed -> layers -> norm -> out_fnn
- * -> [repetition penalty] -> top-k draw) for a batch of B <= 16 sessions as ONE persistent kernel: every
- * phase (q|k|v + RoPE + paged-KV append, split-key attention, o, gate/up + SwiGLU, down, output head,
- * draw + next input) is separated by a device-wide barrier, each workgroup's next weights are loaded
- * while it waits there, and the activations (a few KB per phase) stay in L2.  Replaces the ~27 launches
- * of the multi-kernel step; same C contract as the rest of the library (plain pointers, no torch). */
-#define FO_TTS_MAXL 8
-typedef struct {
-  int B, D, H, hd, F, nl;        /* sessions, model width, heads (= kv heads), head dim (32 | 64), FFN width, layers */
-  int V, V_sample;               /* logits columns (vocab + 4), ids drawn from [0, V_sample) */
-  int PS, maxb, S;               /* KV page size, block-table stride, attention key splits */
-  float eps, scale, penalty;     /* RMSNorm eps, attention scale, repetition penalty (used when win) */
-  int W;                         /* penalty window (win [B][W] device ring), 0 = off */
-  unsigned long long seed;
-  const void* wqkv[FO_TTS_MAXL]; /* fo_pack_weight layouts: q|k|v rope-paired, o, gate/up interleaved, down */
-  const void* wo[FO_TTS_MAXL];
-  const void* wgu[FO_TTS_MAXL];
-  const void* wdown[FO_TTS_MAXL];
-  const float* ln1[FO_TTS_MAXL];
-  const float* ln2[FO_TTS_MAXL];
-  float* kc[FO_TTS_MAXL];        /* per-layer paged caches [page][H][PS][hd] */
-  float* vc[FO_TTS_MAXL];
-  const float* norm;             /* final RMSNorm weight */
-  const void* wout;              /* out_fnn packed, bias bout [V] */
-  const float* bout;
-  const void* emb;               /* bf16 embedding [vocab][emb_ld] */
-  long long emb_ld;
-  const float* cos_t;            /* RoPE tables [pos][hd/2] */
-  const float* sin_t;
-  const int* tok_pos;            /* per-step metadata [B] (device): RoPE position, cache slot, visible keys, */
-  const int* tok_slot;           /* draw step, RNG stream id; hist_row [1]; block_table [B][maxb] */
-  const int* tok_nvis;
-  const int* step;
-  const int* key;
-  const int* hist_row;
-  const int* block_table;
-  const int* top_k;              /* [B] */
-  int* win;                      /* penalty rings [B][W] or null */
-  float* x;                      /* [16][D] this step's input rows (embedding of the current ids); the draw writes
-                                    the next step's */
-  int* ids;                      /* [B] current ids in, drawn ids out */
-  int* hist;                     /* host-mapped [*][hist_ld] id history or null */
-  int hist_ld;
-  float* logits;                 /* [16][V] */
-  float* ws;                     /* scratch, fo_tts_step_ws_floats() */
-  unsigned* bar;                 /* 256 zeroed words, owned by this step (re-armed by the kernel) */
-  int* err;                      /* set non-zero if a barrier timed out */
-  unsigned long long* trace;     /* optional [grid][64] wall clocks: phase work done / barrier passed (profiling) */
-} FoTtsStep;
-long long fo_tts_step_ws_floats(int D, int H, int hd, int F, int S);
-int fo_tts_step(const FoTtsStep* a, hipStream_t s);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,5 @@
 """Device time of one AR speech-decoder step at real geometry (896 / 14 heads / 4864, 4 layers, 8 sessions,
-~300 cached keys): the fused one-launch step (fo_tts_step) against the multi-kernel step, each replayed as
+~300 cached keys): the multi-kernel step replayed as
 the decode graph the benchmark uses, event-timed over 200 steps (host meta preparation included: the
 number is the step rate the speak loop can reach).  python scripts/tts_step_time.py [B] (GPU only)."""
 import ctypes
@@ -27,9 +27,7 @@ e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
 lib.fo_event_create(ctypes.byref(e0))
 lib.fo_event_create(ctypes.byref(e1))
 gen = torch.Generator().manual_seed(0)
-modes = (False, False) if "multi" in sys.argv[2:] else (True, False, True, False)
-for fused in modes:
-    tts.fused = fused
+for fused in (False, False):
     es = ops.engine_stream(dev)
     with torch.cuda.stream(es):
         items = [((torch.randn(40, 896, generator=gen) * 0.5).to(dev), (torch.randn(24, 896, generator=gen) * 0.5).to(dev))
@@ -51,9 +49,9 @@ for fused in modes:
         g.check()
         ms = ctypes.c_float()
         lib.fo_event_elapsed_ms(e0, e1, ctypes.byref(ms))
-        print(f"{'fused' if fused else 'multi'} step, {B} sessions, keys {seqs[0].kv.length}: "
+        print(f"multi step, {B} sessions, keys {seqs[0].kv.length}: "
               f"{ms.value / n * 1e3:7.1f} us per step", flush=True)
-        if not fused and g.exec is not None:
+        if g.exec is not None:
             # the same graph replayed with no host work at all (the captured step advances its own metadata;
             # the pages of the n positions are reserved and uploaded first by one regular launch)
             for q in seqs:
