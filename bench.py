@@ -134,6 +134,8 @@ def run_turn(engine, base_kv, pcms, args, sync):
         else:
             for t, r in zip(turns, engine.listen(items)):
                 t.enc_cache, t.ada_cache, t.pe = r["enc_cache"], r["ada_cache"], r["pe_index"]
+        if c == 0:
+            t_c0 = time.perf_counter()   # chunk 0 (chat prefix, eager) has been read back
     if pipe is not None:
         pipe.flush()
     # ---- dialog_ss (benchmark policy forces it at end of input, as bin/inference.py:138 does)
@@ -175,7 +177,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
     for t in turns:
         t.kv.free()
     stage = {"listen": (t_ss - t_begin) * 1e3, "text": (t_text - t_ss) * 1e3, "speak": (t_end - t_ss) * 1e3,
-             "speak_after_text": (t_end - t_text) * 1e3}
+             "speak_after_text": (t_end - t_text) * 1e3, "listen_chunk0": (t_c0 - t_begin) * 1e3}
     return dict(t_ss=t_ss, first=rec.first, last=rec.last, samples=rec.samples, first_pcm=rec.first_pcm,
                 stage=stage, n_sent=n_sent, codec_tokens=rec.codec_tokens)
 
@@ -871,7 +873,7 @@ def main():
             # fbank / encoder / adapter / Qwen2 / state head (pipelined), text = dialog_ss -> the last text
             # token's id on the host, speak = TTS prefill + AR decode + vocoder until the last PCM segment
             "stage_ms": {k: round(float(np.median([s["stage"][k] for s in stats])), 2)
-                         for k in ("listen", "text", "speak", "speak_after_text")},
+                         for k in ("listen", "text", "speak", "speak_after_text", "listen_chunk0")},
             "single_user": single,
             "cpu_baseline": cpu,
         }

@@ -46,34 +46,47 @@ class KVPool:
 
 
 class KVSeq:
-    """One sequence's view of a KVPool (block list + length)."""
+    """One sequence's view of a KVPool (block list + length).  `version` changes whenever the block list
+    does (pages added, a shared page copied on write, truncation), so a device-side copy of the block table
+    can tell whether it is still current."""
 
     def __init__(self, pool):
         self.pool = pool
         self.pages = []
         self.length = 0
+        self.version = 0
 
     def reserve(self, new_len):
-        """Make room for new_len tokens; the page about to be written is made private (COW)."""
+        """Make room for new_len tokens.  Every page that will be written and is shared with another
+        sequence is made private first (copy on write): the partial tail page and any page past the
+        current length (pages reserved ahead are never shared by fork(), this is the safety net)."""
         PS = self.pool.PS
-        if new_len > self.length and self.length % PS:
-            li = (self.length - 1) // PS  # page holding the partial tail that is about to grow
-            last = self.pages[li]
-            if self.pool.ref[last] > 1:
-                fresh = self.pool.alloc()
-                self.pool.copy_page(last, fresh)
-                self.pool.release(last)
-                self.pages[li] = fresh
+        if new_len > self.length:
+            first = self.length // PS   # first page the new tokens touch (the partial tail if length % PS)
+            last_pg = min(len(self.pages), (new_len + PS - 1) // PS)
+            for li in range(first, last_pg):
+                pg = self.pages[li]
+                if self.pool.ref[pg] > 1:
+                    fresh = self.pool.alloc()
+                    if li * PS < self.length:   # holds live keys: keep them
+                        self.pool.copy_page(pg, fresh)
+                    self.pool.release(pg)
+                    self.pages[li] = fresh
+                    self.version += 1
         while len(self.pages) * PS < new_len:
             self.pages.append(self.pool.alloc())
+            self.version += 1
 
     def slot(self, pos):
         PS = self.pool.PS
         return self.pages[pos // PS] * PS + pos % PS
 
     def fork(self):
+        """A sequence sharing this one's keys copy-on-write: only the pages that hold keys (< length) are
+        shared; pages reserved ahead stay this sequence's own."""
         n = KVSeq(self.pool)
-        n.pages = list(self.pages)
+        used = (self.length + self.pool.PS - 1) // self.pool.PS
+        n.pages = list(self.pages[:used])
         n.length = self.length
         for p in n.pages:
             self.pool.ref[p] += 1
@@ -84,6 +97,8 @@ class KVSeq:
         keep = (new_len + PS - 1) // PS
         for p in self.pages[keep:]:
             self.pool.release(p)
+        if keep < len(self.pages):
+            self.version += 1
         self.pages = self.pages[:keep]
         self.length = new_len
 
@@ -92,6 +107,7 @@ class KVSeq:
             self.pool.release(p)
         self.pages = []
         self.length = 0
+        self.version += 1
 
     def __del__(self):
         try:

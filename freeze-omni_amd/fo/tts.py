@@ -261,9 +261,13 @@ class DecodeGraph:
                 raise RuntimeError("decode graph block table too small")
         if self.advance and slot != step:
             raise ValueError("decode graph: the history row is the step when the step advances its own metadata")
-        sig = (tuple(id(s) for s in seqs), tuple(int(k) for k in keys), tuple(len(s.kv.pages) for s in seqs))
+        # the device-advanced block is current only for the same sequences, RNG keys and block lists (version:
+        # any page added, copied on write or dropped) and lengths exactly one step on
+        sig = (tuple(id(s) for s in seqs), tuple(int(k) for k in keys), tuple(s.kv.version for s in seqs))
+        lens = tuple(s.kv.length for s in seqs)
         up = self._uploaded
-        if not (self.advance and up is not None and up[0] == sig and step == up[1] + 1 and slot == up[2] + 1):
+        if not (self.advance and up is not None and up[0] == sig and step == up[1] + 1 and slot == up[2] + 1
+                and lens == tuple(n + 1 for n in up[3])):
             # the device-advanced block is not this step's: upload it from the host
             h = self.host_np[slot % self.RING]
             h[4 * B:5 * B] = keys
@@ -279,7 +283,7 @@ class DecodeGraph:
                 bt[b, :len(kv.pages)] = kv.pages
                 bt[b, len(kv.pages):] = kv.pages[-1]   # defensive: never a foreign page past the list
             self.meta_d.copy_(self.host[slot % self.RING], non_blocking=True)
-        self._uploaded = (sig, step, slot)
+        self._uploaded = (sig, step, slot, lens)
         for s in seqs:
             s.kv.length += 1
             s.generated += 1
