@@ -89,6 +89,16 @@ int fo_stream_create(void** s_out) {
   *s_out = (void*)s;
   return 0;
 }
+// A blocking stream at the device's greatest scheduling priority when high != 0 (the speech streams: a
+// sentence's first audio is latency-critical while the text decode beside it is throughput work).
+int fo_stream_create_prio(void** s_out, int high) {
+  int lo = 0, hi = 0;
+  FO_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  hipStream_t s;
+  FO_HIP(hipStreamCreateWithPriority(&s, hipStreamDefault, high ? hi : lo));
+  *s_out = (void*)s;
+  return 0;
+}
 // Order stream s after event ev (cross-stream dependency of the pipelined listen stages).
 int fo_stream_wait_event(hipStream_t s, void* ev) {
   FO_HIP(hipStreamWaitEvent(s, (hipEvent_t)ev, 0));

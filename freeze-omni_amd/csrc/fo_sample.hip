@@ -699,7 +699,8 @@ long long fo_sample_ws_floats(int B, int V) {
 int fo_sample(const float* logits, int ld, int B, int V, const int* top_k, const float* temperature,
               const float* top_p, unsigned long long seed, const int* step, const int* key, int ban_id, int* out_ids,
               float* out_maxlogit, int* err, float* ws, long long ws_floats, hipStream_t s) {
-  FO_REQUIRE(B > 0 && V > 0 && ld >= V, "fo_sample: bad shape B=%d V=%d ld=%d", B, V, ld);
+  FO_REQUIRE(B > 0 && V > 0 && (ld >= V || ld == 0), "fo_sample: bad shape B=%d V=%d ld=%d (0: one row for all)", B, V,
+             ld);
   NextInput nx{};
   AmaxPart* parts = nullptr;
   const int nc = (V + AMAX_CH - 1) / AMAX_CH;

@@ -105,6 +105,7 @@ class FreezeOmniEngine:
         self._fbank = {}
         self._lgraphs = {}
         self._tgraphs = {}
+        self._prefix_kv = {}   # shared-context chat-prefix KV (listen: _apply_cached_prefixes)
         self.use_graphs = True
         self.predict_usr_state = ty["model_conf"].get("predict_usr_state", 0)
         self._chat_template(ty["model_conf"].get("chat_template"))
@@ -187,9 +188,47 @@ class FreezeOmniEngine:
         ListenGraph; everything else runs the eager launch sequence.  hidden_row = (buffer, row):
         the buffer is reused by the next listen call."""
         with torch.cuda.stream(ops.engine_stream(self.device)):
+            items = self._apply_cached_prefixes(items)
             if graph and self._graphable(items):
                 return self._listen_graph(items)
             return self._listen_eager(items)
+
+    PREFIX_CACHE = 8
+    use_prefix_cache = True
+
+    def _apply_cached_prefixes(self, items):
+        """Shared-context prefix caching for the first chunk of a turn (status 'ipu_sl' with the chat
+        template): when a session's KV is still exactly the context it was forked from (e.g. the system role
+        every session starts from, bin/dialog_state_pred.py:110,218), the chat-prefix rows it is about to
+        append (models/audioLLM.py:404-406) are the same tokens on the same keys for every such session, so
+        they are computed once per (context, identity), kept as a cached KV extension, and each session
+        becomes a copy-on-write fork of it; the chunk then carries only its adapter rows and runs as a
+        steady-state (captured) step.  Causal attention makes this exact: the prefix rows never see the audio
+        rows.  Sessions with history of their own take the ordinary path."""
+        if not self.chat_template or not self.use_prefix_cache:
+            return items
+        out = []
+        for it in items:
+            kv = it.get("kv")
+            if (it.get("status") == "ipu_sl" and not it.get("prefix_applied") and kv is not None and
+                    it.get("identity") in ("user", "system") and kv.pristine()):
+                key = (kv.content_key(), it["identity"])
+                ext = self._prefix_kv.pop(key, None)
+                if ext is None:
+                    if len(self._prefix_kv) >= self.PREFIX_CACHE:   # least recently used goes
+                        self._prefix_kv.pop(next(iter(self._prefix_kv))).free()
+                    ids = self.prefix_ids[it["identity"]]
+                    ext = kv.fork()
+                    self.llm.forward(self.llm.embed(ids, round_fp16=True), [(ext, len(ids))])
+                self._prefix_kv[key] = ext
+                kv.adopt(ext)
+                it = dict(it, prefix_applied=True)
+                if it.get("enc_cache") is None:
+                    it["enc_cache"] = self.enc[it["identity"]].new_cache()
+                if it.get("ada_cache") is None:
+                    it["ada_cache"] = self.ada[it["identity"]].new_cache()
+            out.append(it)
+        return out
 
     def _graphable(self, items):
         if not items or not self.use_graphs:
@@ -199,7 +238,8 @@ class FreezeOmniEngine:
         for it in items:
             if it["identity"] != ident or it["kv"] is None or it["enc_cache"] is None or it["ada_cache"] is None:
                 return False
-            if it["feats"].shape[0] != R or (self.chat_template and it["status"] == "ipu_sl"):
+            if it["feats"].shape[0] != R or (self.chat_template and it["status"] == "ipu_sl" and
+                                              not it.get("prefix_applied")):
                 return False
         if ident not in ("user", "system"):
             return False
@@ -254,7 +294,8 @@ class FreezeOmniEngine:
         r = 0
         for i, it in enumerate(items):
             emb, r0, To = rows[i]
-            p = self.prefix_ids[it["identity"]] if (self.chat_template and it["status"] == "ipu_sl") else []
+            p = self.prefix_ids[it["identity"]] if (self.chat_template and it["status"] == "ipu_sl" and
+                                                    not it.get("prefix_applied")) else []
             pre_ids += p
             pre_pos += list(range(r, r + len(p)))
             r += len(p)

@@ -90,7 +90,30 @@ class KVSeq:
         n.length = self.length
         for p in n.pages:
             self.pool.ref[p] += 1
+        n.origin = (tuple(n.pages), n.length)
         return n
+
+    origin = None   # (pages, length) at fork time: the content it was forked with
+
+    def pristine(self):
+        """Still exactly the content it was forked with (nothing appended, no page changed)?"""
+        return self.origin is not None and self.length == self.origin[1] and tuple(self.pages) == self.origin[0]
+
+    def content_key(self):
+        """Identity of a pristine fork's content: the shared pages (held by every holder of the key, so they
+        cannot be reused for other keys meanwhile) and the length."""
+        return self.origin
+
+    def adopt(self, other):
+        """Become a copy-on-write fork of `other` (this sequence's own pages are released)."""
+        self.free()
+        used = (other.length + self.pool.PS - 1) // self.pool.PS
+        self.pages = list(other.pages[:used])
+        for p in self.pages:
+            self.pool.ref[p] += 1
+        self.length = other.length
+        self.version += 1
+        self.origin = None
 
     def truncate(self, new_len):
         PS = self.pool.PS

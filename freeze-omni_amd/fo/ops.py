@@ -24,11 +24,16 @@ def stream(device=None):
 _ENGINE_STREAMS = {}
 
 
+HIGH_PRIORITY_STREAMS = ("tts", "voc")
+
+
 def engine_stream(device, side=False, name=None):
     """A blocking HIP stream per device (fo_stream_create) wrapped for torch: it orders against the
     legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it.
     side=True: a second such stream, for work that overlaps the main one (pipelined listen stages).
-    name: further named streams ("tts", "voc": speech generation running beside the text decode)."""
+    name: further named streams ("tts", "voc": speech generation running beside the text decode; those two
+    are created at the device's greatest priority, HIGH_PRIORITY_STREAMS, so a sentence's audio is not
+    queued behind the text decode's weight streams)."""
     import ctypes
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
@@ -36,7 +41,10 @@ def engine_stream(device, side=False, name=None):
     if key not in _ENGINE_STREAMS:
         h = ctypes.c_void_p()
         with torch.cuda.device(idx):
-            _lib.call("fo_stream_create", ctypes.byref(h))
+            if name in HIGH_PRIORITY_STREAMS:
+                _lib.call("fo_stream_create_prio", ctypes.byref(h), 1)
+            else:
+                _lib.call("fo_stream_create", ctypes.byref(h))
         _ENGINE_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
     return _ENGINE_STREAMS[key]
 
@@ -357,7 +365,9 @@ def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS
               stream(qkv.device))
 
 
-ATTN_KEYS_PER_SPLIT = 256
+# keys per split of the decode attention: r03c's sweep (scripts/attn_kps_sweep.py, Qwen2 28/4 heads, 8 sessions
+# x 1-2 new tokens) puts 128 first or tied at every context from 100 to 800 keys (800 keys: 21.7 us vs 24.2 at 256)
+ATTN_KEYS_PER_SPLIT = 128
 
 
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,

@@ -171,3 +171,27 @@ def test_text_graph_matches_eager(eng, top_k):
     for (ie, he), (ig, hg) in zip(eager, graph):
         assert ie == ig
         np.testing.assert_allclose(hg, he, atol=2e-5, rtol=1e-5)
+
+
+def test_shared_context_prefix_cache_matches_uncached(eng, dev):
+    """First chunk (ipu_sl, chat prefix) of sessions forked from one system role: the cached prefix KV
+    (computed once, each session a copy-on-write fork of it, the chunk then a captured steady-state step)
+    gives the state probs, hidden rows and KV lengths of the per-session prefill that appends the prefix rows
+    in the chunk's own forward (models/audioLLM.py:404-419), and later chunks agree too."""
+    g = np.load(os.path.join(G, "fbank.npz"))
+    n_users = 3
+    feats = torch.from_numpy(g["A_feats"]).to(dev)
+    seq = [torch.stack([feats[(c + 5 * u) % 13] for u in range(n_users)]) for c in range(4)]
+    eng.use_prefix_cache = False
+    try:
+        plain = _session_run(eng, seq, True, n_users)
+    finally:
+        eng.use_prefix_cache = True
+    n0 = len(eng._prefix_kv)
+    cached = _session_run(eng, seq, True, n_users)
+    assert len(eng._prefix_kv) >= max(1, n0)                  # the cache really served chunk 0
+    for (pp, hp, lp, qp), (pc, hc, lc, qc) in zip(plain, cached):
+        assert lp == lc and qp == qc
+        np.testing.assert_allclose(np.array(pc), np.array(pp), atol=2e-5)
+        for a, b in zip(hc, hp):
+            np.testing.assert_allclose(a, b, atol=5e-5, rtol=1e-5)
