@@ -728,9 +728,26 @@ thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
 
 // forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
 thread_local int g_force_nw = 0, g_force_nt = 0;
+// k-steps in flight per wave of the one-row-tile fp32-X grid kernel: 4 (default), 7 on 16 waves or 8 on 8
+// waves (every k-step of a wave's K range in one round when waves x U covers K: the Qwen2 o / q|k|v
+// projections, K = 3584 = 16 x 7 x 32); 0 = the policy in gemm_impl
+thread_local int g_force_u = 0;
+thread_local int g_launch_u = 4;
 
 template <int NT, int RB, bool SW>
 void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
+  if constexpr (RB == 1 && NT <= 2) {
+    if (g_launch_u != 4 && x_f32 && !g_launch_pipe) {
+      if constexpr (NT == 1) {  // (2 tiles x 7 k-steps on 16 waves spill past the 128-VGPR budget: 8 x 8 instead)
+        if (g_launch_u == 7) {
+          hipLaunchKernelGGL((k_gemm<1, 1, true, 16, 7, SW>), grid, dim3(1024), 0, s, a);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((k_gemm<NT, 1, true, 8, 8, SW>), grid, dim3(512), 0, s, a);
+      return;
+    }
+  }
   if constexpr (NT == 8) {  // 8 tiles x 16 waves exceeds the 128-VGPR budget of a 1024-thread group
     if (nw == 16) nw = 8;
   } else if (nw == 16) {
@@ -1206,6 +1223,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (nw_pref) nw = nw_pref;
     if (g_force_nw) nw = g_force_nw;
     g_launch_pipe = launch_pipe;
+    g_launch_u = g_force_u ? g_force_u : 4;
     if (swiglu) {
       if (NT == 8) launch_nw<8, 1, true>(nw, wstream, x_f32, grid, a, stream);
       else if (NT == 4) launch_nw<4, 1, true>(nw, wstream, x_f32, grid, a, stream);
@@ -1235,6 +1253,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     }
   }
   g_launch_pipe = 0;
+  g_launch_u = 4;
   if (S > 1 && !merged) {
     int rc = fo::check_launch("fo_gemm/split");
     if (rc) return rc;
@@ -1326,6 +1345,12 @@ int fo_gemm_set_merge(int on) {
 
 int fo_gemm_set_trace(void* trace) {
   g_trc = reinterpret_cast<unsigned long long*>(trace);
+  return 0;
+}
+
+int fo_gemm_set_u(int u) {
+  FO_REQUIRE(u == 0 || u == 4 || u == 7 || u == 8, "fo_gemm_set_u: u must be 0/4/7/8");
+  g_force_u = u;
   return 0;
 }
 

@@ -42,6 +42,7 @@ _SIGS = {
     "fo_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
     "fo_event_destroy": (c_int, [c_vp]),
     "fo_gemm_tune": (c_int, [c_int, c_int]),
+    "fo_gemm_set_u": (c_int, [c_int]),
     "fo_gemm_set_xs": (c_int, [c_int]),
     "fo_gemm_set_merge": (c_int, [c_int]),
     "fo_gemm_set_trace": (c_int, [c_vp]),

@@ -79,6 +79,8 @@ int fo_gemm_rowstats(const void* X, int x_f32, int ldx, int M, int K, const void
                      int splitk, float* rsum, float* rsumsq, int* sgroups, hipStream_t stream);
 /* sweep hook: force (waves, 16-column tiles per workgroup) of the M <= 16 GEMM kernels; 0 = automatic */
 int fo_gemm_tune(int nw, int nt);
+/* sweep hook: k-steps in flight per wave of the one-row-tile fp32-X grid kernel (0 = policy, 4, 7 on 16 waves, 8 on 8 waves) */
+int fo_gemm_set_u(int u);
 /* X-stationary persistent weight stream (k_gemm_xs) for the M <= 16 fp32-X GEMMs with K = 3584 (Qwen2 q|k|v,
  * o, gate/up, lm_head): 0 off, 1 on (default; FO_GEMM_XS=0 turns it off).  Process-global; returns the
  * previous setting. */

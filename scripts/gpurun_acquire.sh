@@ -4,7 +4,7 @@
 log=$1; lim=$2; cmd=$3
 for attempt in $(seq 1 20); do
   timeout $((lim + 1500)) /usr/local/graft/bin/gpurun --timeout $lim -- "$cmd" > $log 2>&1
-  if grep -q "no free box\|backing off\|stopped responding while being prepared\|slot(s) on this pod are busy\|retry in a few minutes" $log && ! grep -q "status=ok\|status=fail\|EXIT" $log; then
+  if grep -q "no free box\|backing off\|stopped responding while being prepared\|slot(s) on this pod are busy\|retry in a few minutes\|taken away by the GPU service" $log && ! grep -q "status=ok\|status=fail\|EXIT" $log; then
     sleep 120
     continue
   fi

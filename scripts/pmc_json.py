@@ -1,0 +1,96 @@
+"""Condense two rocprofv3 --pmc passes of the same command (pass 1: SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES
+SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16; pass 2: GRBM_GUI_ACTIVE GRBM_COUNT) and, optionally, a kernel-trace
+run into one JSON per (kernel, grid): dispatches, mean counters, MfmaUtil and the MFMA rate.
+
+  MfmaUtil %   = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs) * 100
+                 (rocprofv3's MfmaUtil; GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+  TFLOP/s      = SQ_INSTS_VALU_MFMA_MOPS_BF16 * 512 / (GRBM_GUI_ACTIVE / 8 / 2.4 GHz)
+                 (counts every MFMA issued: the fp32-activation hi/lo split issues two per weight fragment)
+
+usage: python scripts/pmc_json.py <out.json> <pass1 dir> <pass2 dir> [<kernel-trace dir>] [--note TEXT]"""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+CLK = 2.4e9
+
+
+def short(name):
+    return re.sub(r"\(anonymous namespace\)::|void ", "", name).split("(")[0]
+
+
+def passes(d):
+    """{(kernel, grid threads, wg): {counter: [per-dispatch values]}}"""
+    out = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        per = defaultdict(float)
+        meta = {}
+        for r in csv.DictReader(open(f)):
+            k = r["Dispatch_Id"]
+            per[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+            meta[k] = (short(r["Kernel_Name"]), int(r["Grid_Size"]), int(r["Workgroup_Size"]))
+        for (k, c), v in per.items():
+            out[meta[k]][c].append(v)
+    return out
+
+
+def trace(d):
+    out = defaultdict(list)
+    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            key = (short(r["Kernel_Name"]), int(r["Grid_Size"]) if "Grid_Size" in r else
+                   int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]),
+                   int(r["Workgroup_Size"]) if "Workgroup_Size" in r else
+                   int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"]))
+            out[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return out
+
+
+def main():
+    args = sys.argv[1:]
+    note = None
+    if "--note" in args:
+        i = args.index("--note")
+        note = args[i + 1]
+        del args[i:i + 2]
+    out, p1, p2 = args[:3]
+    tr = trace(args[3]) if len(args) > 3 else {}
+    a, b = passes(p1), passes(p2)
+    rows = []
+    for key in sorted(set(a) | set(b)):
+        ca, cb = a.get(key, {}), b.get(key, {})
+        mean = {c: sum(v) / len(v) for c, v in list(ca.items()) + list(cb.items())}
+        n = max([len(v) for v in list(ca.values()) + list(cb.values())] or [0])
+        row = {"kernel": key[0], "grid_threads": key[1], "wg": key[2], "dispatches": n,
+               "counters": {c: round(v, 1) for c, v in sorted(mean.items())}}
+        ga = mean.get("GRBM_GUI_ACTIVE")
+        if ga:
+            cyc = ga / 8
+            row["active_us"] = round(cyc / CLK * 1e6, 2)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in mean:
+                row["mfma_util_pct"] = round(mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024) * 100, 2)
+            if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in mean:
+                row["mfma_tflops_incl_hilo"] = round(mean["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / (cyc / CLK) / 1e12, 1)
+        if key in tr:
+            row["trace_avg_us"] = round(sum(tr[key]) / len(tr[key]), 2)
+            row["trace_dispatches"] = len(tr[key])
+        rows.append(row)
+    rows.sort(key=lambda r: -(r.get("trace_avg_us", r.get("active_us", 0)) * r["dispatches"]))
+    doc = {"command_passes": [p1, p2] + ([args[3]] if len(args) > 3 else []),
+           "formulas": {"mfma_util_pct": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) * 100",
+                        "mfma_tflops_incl_hilo": "SQ_INSTS_VALU_MFMA_MOPS_BF16 * 512 / (GRBM_GUI_ACTIVE/8 / 2.4 GHz)"},
+           "kernels": rows}
+    if note:
+        doc["note"] = note
+    json.dump(doc, open(out, "w"), indent=1)
+    for r in rows[:25]:
+        print(f'{r["kernel"][:44]:44s} grid {r["grid_threads"]:8d} wg {r["wg"]:4d} n {r["dispatches"]:5d} '
+              f'{r.get("trace_avg_us", r.get("active_us", 0)):8.2f} us  util {r.get("mfma_util_pct", 0):6.2f}%  '
+              f'{r.get("mfma_tflops_incl_hilo", 0):7.1f} TF/s')
+
+
+if __name__ == "__main__":
+    main()
