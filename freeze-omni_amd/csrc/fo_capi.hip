@@ -89,14 +89,20 @@ int fo_stream_create(void** s_out) {
   *s_out = (void*)s;
   return 0;
 }
-// A blocking stream at the device's greatest scheduling priority when high != 0 (the speech streams: a
-// sentence's first audio is latency-critical while the text decode beside it is throughput work).
-int fo_stream_create_prio(void** s_out, int high) {
+// A blocking stream at the device's greatest scheduling priority when level > 0 (the speech streams: a
+// sentence's first audio is latency-critical while the text decode beside it is throughput work), at its
+// least priority when level < 0, at the default (0, clamped into the range) otherwise.
+int fo_stream_create_prio(void** s_out, int level) {
   int lo = 0, hi = 0;
   FO_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   hipStream_t s;
-  FO_HIP(hipStreamCreateWithPriority(&s, hipStreamDefault, high ? hi : lo));
+  FO_HIP(hipStreamCreateWithPriority(&s, hipStreamDefault, level > 0 ? hi : (level < 0 ? lo : 0)));
   *s_out = (void*)s;
+  return 0;
+}
+// The device's stream priority range (least, greatest; lower numbers are greater priorities).
+int fo_stream_priority_range(int* least, int* greatest) {
+  FO_HIP(hipDeviceGetStreamPriorityRange(least, greatest));
   return 0;
 }
 // Order stream s after event ev (cross-stream dependency of the pipelined listen stages).

@@ -1117,7 +1117,13 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     // tiles per workgroup; long-K layers (Qwen2 down) 4 tiles and a 4-way K split; mid-size grids
     // (> 256 tiles: Qwen2 qkv) 2 tiles; small ones 1
     if (a.ntiles >= 1024) NT = 4;
-    else if (KS >= 256 && a.ntiles >= 128) { NT = 4; S_auto = 4; }
+    // Qwen2 down (592 k-steps, 224 tiles): 8 tiles x 8-way K split, pipelined (28 x 8 = 224 workgroups): the
+    // activation rows are read by a quarter as many column groups as with 4 tiles x 4 ways; 31.7 -> 29.7 us at 16
+    // rows, 29.7 -> 28.7 us at 8, reduce launch included (profiles/r03g_down_sweep.txt)
+    else if (KS >= 256 && a.ntiles >= 128) {
+      NT = a.ntiles % 8 == 0 ? 8 : 4;
+      S_auto = NT == 8 ? 8 : 4;
+    }
     else if (KS >= 128 && a.ntiles <= 64) S_auto = 4;  // narrow long-K (TTS down): 10.9 -> 8.2 us in a graph
     else if (a.ntiles > 256) NT = 2;
     // small SwiGLU pairs over 512+ tiles (the TTS gate/up, 608 tiles, 17.4 MB): 2 pairs per workgroup on 8
@@ -1229,7 +1235,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       else if (NT == 4) launch_nw<4, 1, true>(nw, wstream, x_f32, grid, a, stream);
       else launch_nw<2, 1, true>(nw, wstream, x_f32, grid, a, stream);
     } else {
-      if (NT == 4) launch_nw<4, 1, false>(nw, wstream, x_f32, grid, a, stream);
+      if (NT == 8) launch_nw<8, 1, false>(nw, wstream, x_f32, grid, a, stream);
+      else if (NT == 4) launch_nw<4, 1, false>(nw, wstream, x_f32, grid, a, stream);
       else if (NT == 2) launch_nw<2, 1, false>(nw, wstream, x_f32, grid, a, stream);
       else launch_nw<1, 1, false>(nw, wstream, x_f32, grid, a, stream);
     }

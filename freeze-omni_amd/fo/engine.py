@@ -455,7 +455,7 @@ class ListenGraph:
         self.side = ops.engine_stream(dev, side=True) if slots > 1 else self.main
         # the encoder stage is captured on the stream it replays on, so its split-K scratch (ops.Runtime)
         # is not the LLM stage's while the two overlap
-        self.enc_exec = [self._capture(self.side, lambda k=k: self._enc_body(k)) for k in range(slots)]
+        self.enc_exec = [self._capture(self.side, lambda k=k: self._enc_body(k), ENC_GEMM_TUNE) for k in range(slots)]
         self.llm_exec = [self._capture(self.main, lambda k=k: self._llm_body(k)) for k in range(slots)]
         self.ev_enc = [self._event() for _ in range(slots)]
         self.ev_llm = [self._event() for _ in range(slots)]
@@ -469,8 +469,11 @@ class ListenGraph:
         return e
 
     @staticmethod
-    def _capture(stream, body):
+    def _capture(stream, body, tune=None):
+        """tune: (waves, tiles per workgroup) forced on the GEMMs captured in body (fo_gemm_tune; probes)."""
         s = stream.cuda_stream
+        if tune:
+            _lib.call("fo_gemm_tune", *tune)
         _lib.call("fo_graph_begin", s)
         try:
             with torch.cuda.stream(stream):
@@ -478,6 +481,8 @@ class ListenGraph:
         finally:
             ex = ctypes.c_void_p()
             _lib.call("fo_graph_end", s, ctypes.byref(ex))
+            if tune:
+                _lib.call("fo_gemm_tune", 0, 0)
         return ex
 
     def _enc_body(self, k):
@@ -665,6 +670,11 @@ class TextGraph:
             self.ring.destroy()
             self.err.free()
             self.exec = None
+
+
+# probe knob: FO_ENC_TUNE="waves,tiles" forces the GEMM shape of the pipelined encoder stage's graph (the stage
+# beside the Qwen2 stage, off the critical path: fewer, wider workgroups re-read its activations less often)
+ENC_GEMM_TUNE = tuple(int(v) for v in os.environ["FO_ENC_TUNE"].split(",")) if os.environ.get("FO_ENC_TUNE") else None
 
 
 class ListenPipe:

@@ -3,6 +3,7 @@
 torch is used only for device memory and the current stream (plumbing); every computation
 below is a hand-written gfx950 kernel in libfo_hip.so.
 """
+import os
 import torch
 
 from . import _lib
@@ -25,6 +26,11 @@ _ENGINE_STREAMS = {}
 
 
 HIGH_PRIORITY_STREAMS = ("tts", "voc")
+# priority level of the side stream (the pipelined listen's encoder stage, the vocoder when no "voc" stream is
+# given): 0 default, -1 the device's least (FO_SIDE_PRIORITY, A/B probes)
+SIDE_STREAM_PRIORITY = int(os.environ.get("FO_SIDE_PRIORITY", "0"))
+# and of the engine stream (the Qwen2 stages, the text decode): FO_MAIN_PRIORITY, 0 default, 1 greatest
+MAIN_STREAM_PRIORITY = int(os.environ.get("FO_MAIN_PRIORITY", "0"))
 
 
 def engine_stream(device, side=False, name=None):
@@ -43,6 +49,10 @@ def engine_stream(device, side=False, name=None):
         with torch.cuda.device(idx):
             if name in HIGH_PRIORITY_STREAMS:
                 _lib.call("fo_stream_create_prio", ctypes.byref(h), 1)
+            elif name is None and side and SIDE_STREAM_PRIORITY:
+                _lib.call("fo_stream_create_prio", ctypes.byref(h), SIDE_STREAM_PRIORITY)
+            elif name is None and not side and MAIN_STREAM_PRIORITY:
+                _lib.call("fo_stream_create_prio", ctypes.byref(h), MAIN_STREAM_PRIORITY)
             else:
                 _lib.call("fo_stream_create", ctypes.byref(h))
         _ENGINE_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))

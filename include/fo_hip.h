@@ -25,8 +25,10 @@ int fo_graph_end(hipStream_t s, void** exec_out);
 int fo_graph_launch(void* exec, hipStream_t s);
 int fo_graph_destroy(void* exec);
 int fo_stream_create(void** s_out);
-// high != 0: the device's greatest stream priority (the speech streams, fo/ops.py engine_stream)
-int fo_stream_create_prio(void** s_out, int high);
+// level > 0: the device's greatest stream priority (the speech streams, fo/ops.py engine_stream);
+// level < 0: its least; 0: the default
+int fo_stream_create_prio(void** s_out, int level);
+int fo_stream_priority_range(int* least, int* greatest);
 int fo_stream_destroy(void* s);
 int fo_stream_wait_event(hipStream_t s, void* ev);
 int fo_host_alloc(long long bytes, void** host_ptr, void** dev_ptr);

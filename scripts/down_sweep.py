@@ -52,6 +52,7 @@ for M in (16, 8):
                     except RuntimeError as e:
                         res.append((1e9, f"pipe{pipe} nw{nw} nt{nt} S{S} failed: {e}"))
                         continue
+                    ops.Runtime.get(dev).ws.zero_()   # no stale split-K slabs from an earlier configuration
                     run(0, S)
                     torch.cuda.synchronize()
                     err = (outs[0] - ref).abs().max().item() / scale
