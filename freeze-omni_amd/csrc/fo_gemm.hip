@@ -567,14 +567,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     for (int rr = wave; rr < ROWS; rr += NW) {
       const int m = m0 + rr;
       if (m >= a.M) break;
-      const float v = lane < cnt ? red[0][lane >> 4][rr][lane & 15] : 0.f;
-      const float ss = wave_sum(v * v);
+      // the workgroup's LT * 16 columns in 64-lane passes (one pass up to 4 tiles; 8-tile groups take two)
+      float sq = 0.f, sm = 0.f;
+#pragma unroll
+      for (int c0 = 0; c0 < LT * 16; c0 += 64) {
+        const int c = c0 + lane;
+        const float v = c < cnt ? red[0][c >> 4][rr][c & 15] : 0.f;
+        sq += v * v;
+        sm += v;
+        if (a.yg && c < cnt) a.yg[(size_t)m * a.ldy + n0 + c] = v * (EPRE ? p_gn : a.gnext[n0 + c]);
+      }
+      const float ss = wave_sum(sq);
       if (lane == 0) a.sout[(size_t)m * gridDim.x + tg] = ss;
       if (a.sout1) {
-        const float s1 = wave_sum(v);
+        const float s1 = wave_sum(sm);
         if (lane == 0) a.sout1[(size_t)m * gridDim.x + tg] = s1;
       }
-      if (a.yg && lane < cnt) a.yg[(size_t)m * a.ldy + n0 + lane] = v * (EPRE ? p_gn : a.gnext[n0 + lane]);
     }
   }
   if (trc && threadIdx.x == 0) trc[18] = wall_clock64();

@@ -286,7 +286,18 @@ inline int grid_for(long long n) {
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
-inline int pick_ck(int Cin) { return Cin >= 64 ? 64 : Cin; }
+// Channels per staged Cin chunk: 64 by default; FO_CONV_CK=32 halves every workgroup's LDS (window and weight
+// buffers), so two or three workgroups share a CU and one stages while another computes (A/B probe; the packing
+// reads the same value, so weights packed in a process match its launches).
+int g_ck_max = 0;
+inline int pick_ck(int Cin) {
+  if (!g_ck_max) {
+    const char* e = getenv("FO_CONV_CK");
+    g_ck_max = (e && (e[0] == '1' || e[0] == '3')) ? atoi(e) : 64;
+    if (g_ck_max != 16 && g_ck_max != 32) g_ck_max = 64;
+  }
+  return Cin >= g_ck_max ? g_ck_max : Cin;
+}
 
 
 }  // namespace
@@ -340,6 +351,7 @@ int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const fl
   }
   dim3 grid((Tq + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B);
   if (MTW == 2 && NTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 2, 64>), grid, dim3(256), 0, s, a);
+  else if (MTW == 2 && NTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 2, 32>), grid, dim3(256), 0, s, a);
   else if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, a);
   else if (MTW == 2 && NTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, a);
   else if (MTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 4, 32>), grid, dim3(256), 0, s, a);

@@ -269,7 +269,7 @@ def test_gemm_split_merge_in_launch_bit_exact(dev, M, N, K):
 
     def run():
         y = res0.clone()
-        yg = torch.empty_like(y)
+        yg = torch.full_like(y, float("nan"))   # every column must be written (no stale memory passes)
         st = RowStats(M, dev).set(gamma, yg)
         lin(x, out=y, residual=True, splitk=4, stats_out=st)
         ss = st.buf[:M * st.groups].view(M, st.groups).sum(1)
@@ -289,3 +289,4 @@ def test_gemm_split_merge_in_launch_bit_exact(dev, M, N, K):
     ref = x.cpu().double() @ w.double().t() + res0.cpu().double()
     torch.testing.assert_close(y0.double(), ref, rtol=5e-5, atol=5e-5)
     torch.testing.assert_close(s0.double(), (ref ** 2).sum(1), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(g0.double(), ref * gamma.cpu().double(), rtol=5e-5, atol=5e-5)
