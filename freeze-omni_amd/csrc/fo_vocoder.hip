@@ -13,6 +13,7 @@
 // ConvTranspose1d (stride u) is u polyphase convolutions: output phase r only meets taps
 // j = j0(r) + u*m, i.e. a 2-tap stride-1 conv with its own packed weights writing every u-th step.
 #include "fo_common.h"
+#include "fo_hip.h"
 
 namespace {
 
@@ -38,13 +39,25 @@ struct ConvArgs {
   const float* gadd;   // [B][Cout] or null
 };
 
+// Up to CONV_MAXG convolutions of one shape class (same Cin / Cout) in one launch: blockIdx.z = b + B * g
+// runs conv g on batch row b (the u polyphase components of a ConvTranspose1d; the independent dilated
+// ResBlock1 chains of a stage, models/decoder/ticodec/models.py:221-238); sum != 0: every workgroup runs ALL G
+// convs of its output tile into one accumulator and stores (sum_g (conv_g + bias_g + res_g + res2_g)) *
+// oscale + gadd (the resblocks' last convs, whose outputs the reference averages) -- out / oscale / gadd /
+// the output geometry are a[0]'s.
+constexpr int CONV_MAXG = 5;
+struct ConvMulti {
+  ConvArgs a[CONV_MAXG];
+  int B, G, sum;
+};
+
 constexpr int CONV_KMAX = 11;
 // k-steps per Cin chunk, rounded up to even (padding k-steps carry zero weights)
 __host__ __device__ constexpr int nks_per_chunk(int K, int CK) { return ((K * CK + 31) / 32 + 1) & ~1; }
 __host__ __device__ constexpr int conv_wmax(int CK) { return nks_per_chunk(CONV_KMAX, CK); }
 
 template <int MTW, int NTW, int CK>
-__global__ __launch_bounds__(256) void k_conv_cl(ConvArgs a) {
+__global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
   constexpr int TW = 64 * NTW;     // time steps per workgroup (4 waves x 16*NTW)
   constexpr int ROWS = TW + HALO;
   constexpr int LP = CK + 8;       // padded bf16 row (16 B): 16 lanes of different rows hit distinct banks
@@ -56,10 +69,10 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t0 = blockIdx.x * TW;
   const int ct0 = blockIdx.y * MTW;  // first 16-channel output tile
-  const int b = blockIdx.z;
-  const int nks = (a.Cin / CK) * a.nks_c;
-  const int span = TW + a.dil * (a.K - 1);
-  const float* xb = a.x + (size_t)b * a.Tin * a.Cin;
+  const int g0 = mc.sum ? 0 : (int)blockIdx.z / mc.B;
+  const int b = mc.sum ? (int)blockIdx.z : (int)blockIdx.z % mc.B;
+  const int g1 = mc.sum ? mc.G : g0 + 1;
+  if (t0 >= mc.a[g0].Tq) return;  // (polyphase components: the shorter phases' last time tile)
 
   f32x4 acc[MTW][NTW];
 #pragma unroll
@@ -70,78 +83,85 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvArgs a) {
   const int tl = wave * 16 * NTW + (lane & 15);  // this lane's time row (tile n adds 16 n)
   const int kq = 8 * (lane >> 4);                 // this lane's 8-wide K slice inside a step
 
-  // A chunk's weight A-fragments (MTW tiles x nks_c k-steps, 1 KiB each) are copied global -> LDS
-  // with 16-B LDS-DMA loads (lane-linear, exactly one fragment per wave-instruction), issued with the
-  // activation loads: one memory latency per chunk, and the four waves share one copy.
-  // Staging: every thread issues all of its window loads for the chunk back to back (MAXL 16-B loads,
-  // one latency per chunk instead of one per loop trip), then splits them into LDS.
-  constexpr int MAXL = (ROWS * (CK / 4) + 255) / 256;
-  auto stage = [&](int c) {
-    __syncthreads();  // the previous chunk's reads are done
-    for (int f = wave; f < MTW * a.nks_c; f += 4) {
-      const int m = f / a.nks_c, st = f - m * a.nks_c;
-      const bf16_t* src = a.wp + ((size_t)(ct0 + m) * nks + c * a.nks_c + st) * 512 + lane * 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)&wl[f * 512], 16, 0, 0);
-    }
-    float4 v[MAXL];
-#pragma unroll
-    for (int i = 0; i < MAXL; ++i) {
-      const int e = threadIdx.x + 256 * i;
-      const int row = e / (CK / 4), c4 = e % (CK / 4);
-      const int ti = t0 - a.pad + row;
-      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < span * (CK / 4) && ti >= 0 && ti < a.Tin)
-        v[i] = *reinterpret_cast<const float4*>(xb + (size_t)ti * a.Cin + c * CK + c4 * 4);
-    }
-#pragma unroll
-    for (int i = 0; i < MAXL; ++i) {
-      const int e = threadIdx.x + 256 * i;
-      if (e >= span * (CK / 4)) break;
-      const int row = e / (CK / 4), c4 = e % (CK / 4);
-      float f[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-      __attribute__((ext_vector_type(4))) __bf16 h4, l4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (a.pre_act) f[q] = f[q] < 0.f ? f[q] * a.slope : f[q];
-        const __bf16 h = (__bf16)f[q];
-        h4[q] = h;
-        l4[q] = (__bf16)(f[q] - (float)h);
+  for (int g = g0; g < g1; ++g) {
+    const ConvArgs& a = mc.a[g];
+    const int nks = (a.Cin / CK) * a.nks_c;
+    const int span = TW + a.dil * (a.K - 1);
+    const float* xb = a.x + (size_t)b * a.Tin * a.Cin;
+    // A chunk's weight A-fragments (MTW tiles x nks_c k-steps, 1 KiB each) are copied global -> LDS
+    // with 16-B LDS-DMA loads (lane-linear, exactly one fragment per wave-instruction), issued with the
+    // activation loads: one memory latency per chunk, and the four waves share one copy.
+    // Staging: every thread issues all of its window loads for the chunk back to back (MAXL 16-B loads,
+    // one latency per chunk instead of one per loop trip), then splits them into LDS.
+    constexpr int MAXL = (ROWS * (CK / 4) + 255) / 256;
+    auto stage = [&](int c) {
+      __syncthreads();  // the previous chunk's (or convolution's) reads are done
+      for (int f = wave; f < MTW * a.nks_c; f += 4) {
+        const int m = f / a.nks_c, st = f - m * a.nks_c;
+        const bf16_t* src = a.wp + ((size_t)(ct0 + m) * nks + c * a.nks_c + st) * 512 + lane * 8;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)&wl[f * 512], 16, 0, 0);
       }
-      *reinterpret_cast<decltype(h4)*>(&xh[row][c4 * 4]) = h4;
-      *reinterpret_cast<decltype(l4)*>(&xl[row][c4 * 4]) = l4;
-    }
-    __builtin_amdgcn_s_waitcnt(0);  // the LDS-DMA copies (vmcnt) too
-    __syncthreads();
-  };
-  auto comp = [&](int s) {
-    const int kk = s * 32 + kq;
-    int j = kk / CK;
-    const int cil = kk - j * CK;
-    if (j > a.K - 1) j = a.K - 1;  // padded K: the packed weights are zero there
-    const int rb = tl + j * a.dil;
-    bf16x8 av[MTW];
+      float4 v[MAXL];
 #pragma unroll
-    for (int m = 0; m < MTW; ++m) av[m] = *reinterpret_cast<const bf16x8*>(&wl[(m * a.nks_c + s) * 512 + lane * 8]);
-#pragma unroll
-    for (int n = 0; n < NTW; ++n) {
-      const bf16x8 hi = *reinterpret_cast<const bf16x8*>(&xh[rb + 16 * n][cil]);
-      const bf16x8 lo = *reinterpret_cast<const bf16x8*>(&xl[rb + 16 * n][cil]);
-#pragma unroll
-      for (int m = 0; m < MTW; ++m) {
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], hi, acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], lo, acc[m][n], 0, 0, 0);
+      for (int i = 0; i < MAXL; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        const int row = e / (CK / 4), c4 = e % (CK / 4);
+        const int ti = t0 - a.pad + row;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < span * (CK / 4) && ti >= 0 && ti < a.Tin)
+          v[i] = *reinterpret_cast<const float4*>(xb + (size_t)ti * a.Cin + c * CK + c4 * 4);
       }
+#pragma unroll
+      for (int i = 0; i < MAXL; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        if (e >= span * (CK / 4)) break;
+        const int row = e / (CK / 4), c4 = e % (CK / 4);
+        float f[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        __attribute__((ext_vector_type(4))) __bf16 h4, l4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (a.pre_act) f[q] = f[q] < 0.f ? f[q] * a.slope : f[q];
+          const __bf16 h = (__bf16)f[q];
+          h4[q] = h;
+          l4[q] = (__bf16)(f[q] - (float)h);
+        }
+        *reinterpret_cast<decltype(h4)*>(&xh[row][c4 * 4]) = h4;
+        *reinterpret_cast<decltype(l4)*>(&xl[row][c4 * 4]) = l4;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // the LDS-DMA copies (vmcnt) too
+      __syncthreads();
+    };
+    auto comp = [&](int s) {
+      const int kk = s * 32 + kq;
+      int j = kk / CK;
+      const int cil = kk - j * CK;
+      if (j > a.K - 1) j = a.K - 1;  // padded K: the packed weights are zero there
+      const int rb = tl + j * a.dil;
+      bf16x8 av[MTW];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) av[m] = *reinterpret_cast<const bf16x8*>(&wl[(m * a.nks_c + s) * 512 + lane * 8]);
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) {
+        const bf16x8 hi = *reinterpret_cast<const bf16x8*>(&xh[rb + 16 * n][cil]);
+        const bf16x8 lo = *reinterpret_cast<const bf16x8*>(&xl[rb + 16 * n][cil]);
+#pragma unroll
+        for (int m = 0; m < MTW; ++m) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], hi, acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], lo, acc[m][n], 0, 0, 0);
+        }
+      }
+    };
+    const int nchunks = a.Cin / CK;
+    for (int c = 0; c < nchunks; ++c) {
+      stage(c);
+      for (int s = 0; s < a.nks_c; ++s) comp(s);
     }
-  };
-  const int nchunks = a.Cin / CK;
-  for (int c = 0; c < nchunks; ++c) {
-    stage(c);
-    for (int s = 0; s < a.nks_c; ++s) comp(s);
   }
   // C layout: row (output channel) = 4*(lane>>4) + i, column (time) = lane & 15.  Every epilogue
   // operand is loaded for all tiles first (one memory latency, not one per tile), rows past Tq read
   // row Tq - 1 and are not stored.
+  const ConvArgs& a = mc.a[g0];
   float4 add[NTW][MTW];
 #pragma unroll
   for (int n = 0; n < NTW; ++n)
@@ -153,27 +173,39 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvArgs a) {
     const int q = min(t0 + tl + 16 * n, a.Tq - 1);
     off[n] = ((size_t)b * a.Tout_total + (size_t)q * a.ostride + a.ooff) * a.Cout + (ct0 * 16 + kq / 2);
   }
-  const float* rs[2] = {a.res, a.res2};
+  float4 bb[MTW];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    if (!rs[r]) continue;
-    float4 v[NTW][MTW];
+  for (int m = 0; m < MTW; ++m) bb[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g = g0; g < g1; ++g) {
+    const ConvArgs& ag = mc.a[g];
+    const float* rs[2] = {ag.res, ag.res2};
 #pragma unroll
-    for (int n = 0; n < NTW; ++n)
+    for (int r = 0; r < 2; ++r) {
+      if (!rs[r]) continue;
+      float4 v[NTW][MTW];
 #pragma unroll
-      for (int m = 0; m < MTW; ++m) v[n][m] = *reinterpret_cast<const float4*>(rs[r] + off[n] + m * 16);
+      for (int n = 0; n < NTW; ++n)
 #pragma unroll
-    for (int n = 0; n < NTW; ++n)
+        for (int m = 0; m < MTW; ++m) v[n][m] = *reinterpret_cast<const float4*>(rs[r] + off[n] + m * 16);
+#pragma unroll
+      for (int n = 0; n < NTW; ++n)
+#pragma unroll
+        for (int m = 0; m < MTW; ++m) {
+          add[n][m].x += v[n][m].x; add[n][m].y += v[n][m].y; add[n][m].z += v[n][m].z; add[n][m].w += v[n][m].w;
+        }
+    }
+    if (ag.bias) {
 #pragma unroll
       for (int m = 0; m < MTW; ++m) {
-        add[n][m].x += v[n][m].x; add[n][m].y += v[n][m].y; add[n][m].z += v[n][m].z; add[n][m].w += v[n][m].w;
+        const float4 v = *reinterpret_cast<const float4*>(ag.bias + (ct0 + m) * 16 + kq / 2);
+        bb[m].x += v.x; bb[m].y += v.y; bb[m].z += v.z; bb[m].w += v.w;
       }
+    }
   }
-  float4 bb[MTW], gg[MTW];
+  float4 gg[MTW];
 #pragma unroll
   for (int m = 0; m < MTW; ++m) {
     const int co = (ct0 + m) * 16 + kq / 2;
-    bb[m] = a.bias ? *reinterpret_cast<const float4*>(a.bias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
     gg[m] = a.gadd ? *reinterpret_cast<const float4*>(a.gadd + (size_t)b * a.Cout + co) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
@@ -286,15 +318,16 @@ inline int grid_for(long long n) {
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
-// Channels per staged Cin chunk: 64 by default; FO_CONV_CK=32 halves every workgroup's LDS (window and weight
-// buffers), so two or three workgroups share a CU and one stages while another computes (A/B probe; the packing
-// reads the same value, so weights packed in a process match its launches).
+// Channels per staged Cin chunk: 32, half the LDS of a 64-channel chunk (window and weight buffers), so two or
+// three workgroups share a CU and one stages its chunk while another computes: 8-user call 2.11 -> 1.93 ms
+// (16: 2.58 ms; profiles/r03i_vocoder_ck_ab.txt).  FO_CONV_CK=16/64 for A/B; the packing reads the same value,
+// so weights packed in a process match its launches.
 int g_ck_max = 0;
 inline int pick_ck(int Cin) {
   if (!g_ck_max) {
     const char* e = getenv("FO_CONV_CK");
-    g_ck_max = (e && (e[0] == '1' || e[0] == '3')) ? atoi(e) : 64;
-    if (g_ck_max != 16 && g_ck_max != 32) g_ck_max = 64;
+    g_ck_max = e ? atoi(e) : 32;
+    if (g_ck_max != 16 && g_ck_max != 64) g_ck_max = 32;
   }
   return Cin >= g_ck_max ? g_ck_max : Cin;
 }
@@ -329,40 +362,83 @@ int fo_pack_conv(const void* W, int src_bf16, int Cout, int Cin, int K, int tran
 // q * ostride + ooff for q < Tq (Tq = Tin + 2 pad - dil (K-1) for a plain conv), with the fused
 // epilogue out = (conv + bias + res + res2) * oscale + gadd[b] (res, res2, gadd optional).
 // out must not alias x (other workgroups still read the input window).
-int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const float* bias, int Cout, int K, int dil,
-               int pad, int Tq, int ostride, int ooff, int Tout_total, int pre_leaky, float slope, float* out,
-               const float* res, const float* res2, float oscale, const float* gadd, hipStream_t s) {
-  FO_REQUIRE(Cout % 16 == 0 && Cin % 16 == 0 && Cin >= 16, "fo_conv_cl: Cout=%d Cin=%d", Cout, Cin);
-  FO_REQUIRE(K >= 1 && K <= CONV_KMAX && dil >= 1 && dil * (K - 1) <= HALO,
-             "fo_conv_cl: K=%d dil=%d beyond the LDS halo / weight buffer", K, dil);
-  FO_REQUIRE(Tq > 0 && (long long)(Tq - 1) * ostride + ooff < Tout_total, "fo_conv_cl: output range");
-  FO_REQUIRE((const void*)x != (const void*)out, "fo_conv_cl: out aliases the input");
+static int conv_check(const ConvArgs& a) {
+  FO_REQUIRE(a.Cout % 16 == 0 && a.Cin % 16 == 0 && a.Cin >= 16, "fo_conv_cl: Cout=%d Cin=%d", a.Cout, a.Cin);
+  FO_REQUIRE(a.K >= 1 && a.K <= CONV_KMAX && a.dil >= 1 && a.dil * (a.K - 1) <= HALO,
+             "fo_conv_cl: K=%d dil=%d beyond the LDS halo / weight buffer", a.K, a.dil);
+  FO_REQUIRE(a.Tq > 0 && (long long)(a.Tq - 1) * a.ostride + a.ooff < a.Tout_total, "fo_conv_cl: output range");
+  FO_REQUIRE((const void*)a.x != (const void*)a.out, "fo_conv_cl: out aliases the input");
+  return 0;
+}
+
+// One launch of mc.G convolutions (all Cin -> Cout); Tq_max: the longest output range among them.
+static int conv_launch(ConvMulti& mc, int Tq_max, hipStream_t s) {
+  const int B = mc.B, Cin = mc.a[0].Cin, Cout = mc.a[0].Cout;
   const int CK = pick_ck(Cin);
-  ConvArgs a{x, (const bf16_t*)wp, bias, out, Cin, Tin, Cout, K, dil, pad, Tq, ostride, ooff, Tout_total,
-             nks_per_chunk(K, CK), pre_leaky, slope, res, res2, oscale, gadd};
+  const int zg = mc.sum ? 1 : mc.G;
   int MTW = Cout >= 64 ? 4 : Cout / 16;
   int NTW = 8 / MTW;
   // short, wide stages (the first upsampling stages: Tq of a few hundred, 256-512 channels) would put
   // only ~100 workgroups on 256 CUs: take 2 x 2 tiles per wave there (more workgroups, less reuse of
   // the L2-resident weights, which costs little at these sizes)
-  if (MTW == 4 && (long long)((Tq + 127) / 128) * (Cout / 64) * B < 256) {
+  if (MTW == 4 && (long long)((Tq_max + 127) / 128) * (Cout / 64) * B * zg < 256) {
     MTW = 2;
     NTW = 2;
   }
-  dim3 grid((Tq + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B);
-  if (MTW == 2 && NTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 2, 64>), grid, dim3(256), 0, s, a);
-  else if (MTW == 2 && NTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 2, 32>), grid, dim3(256), 0, s, a);
-  else if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, a);
-  else if (MTW == 2 && NTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, a);
-  else if (MTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 4, 32>), grid, dim3(256), 0, s, a);
-  else if (MTW == 1 && CK == 32) hipLaunchKernelGGL((k_conv_cl<1, 8, 32>), grid, dim3(256), 0, s, a);
-  else if (MTW == 1 && CK == 16) hipLaunchKernelGGL((k_conv_cl<1, 8, 16>), grid, dim3(256), 0, s, a);
-  else if (MTW == 4 && CK == 32) hipLaunchKernelGGL((k_conv_cl<4, 2, 32>), grid, dim3(256), 0, s, a);
-  else if (MTW == 4 && CK == 16) hipLaunchKernelGGL((k_conv_cl<4, 2, 16>), grid, dim3(256), 0, s, a);
-  else if (MTW == 2 && CK == 16) hipLaunchKernelGGL((k_conv_cl<2, 4, 16>), grid, dim3(256), 0, s, a);
-  else if (MTW == 1 && CK == 64) hipLaunchKernelGGL((k_conv_cl<1, 4, 64>), dim3((Tq + 255) / 256, Cout / 16, B), dim3(256), 0, s, a);
+  dim3 grid((Tq_max + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B * zg);
+  if (MTW == 1 && CK == 64) grid.x = (Tq_max + 255) / 256;
+  if (MTW == 2 && NTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 2, 64>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 2 && NTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 2, 32>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 2 && NTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 4, 32>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 1 && CK == 32) hipLaunchKernelGGL((k_conv_cl<1, 8, 32>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 1 && CK == 16) hipLaunchKernelGGL((k_conv_cl<1, 8, 16>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 4 && CK == 32) hipLaunchKernelGGL((k_conv_cl<4, 2, 32>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 4 && CK == 16) hipLaunchKernelGGL((k_conv_cl<4, 2, 16>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 2 && CK == 16) hipLaunchKernelGGL((k_conv_cl<2, 4, 16>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 1 && CK == 64) hipLaunchKernelGGL((k_conv_cl<1, 4, 64>), grid, dim3(256), 0, s, mc);
   else FO_REQUIRE(false, "fo_conv_cl: no variant for Cout=%d Cin=%d", Cout, Cin);
   return fo::check_launch("fo_conv_cl");
+}
+
+int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const float* bias, int Cout, int K, int dil,
+               int pad, int Tq, int ostride, int ooff, int Tout_total, int pre_leaky, float slope, float* out,
+               const float* res, const float* res2, float oscale, const float* gadd, hipStream_t s) {
+  ConvMulti mc{};
+  mc.a[0] = ConvArgs{x, (const bf16_t*)wp, bias, out, Cin, Tin, Cout, K, dil, pad, Tq, ostride, ooff, Tout_total,
+                     nks_per_chunk(K, pick_ck(Cin)), pre_leaky, slope, res, res2, oscale, gadd};
+  mc.B = B;
+  mc.G = 1;
+  mc.sum = 0;
+  if (int rc = conv_check(mc.a[0])) return rc;
+  return conv_launch(mc, Tq, s);
+}
+
+int fo_conv_cl_multi(const FoConvDesc* d, int G, int B, int Cin, int Cout, int sum, hipStream_t s) {
+  FO_REQUIRE(d && G >= 1 && G <= CONV_MAXG && B >= 1, "fo_conv_cl_multi: G=%d (1..%d) B=%d", G, CONV_MAXG, B);
+  ConvMulti mc{};
+  mc.B = B;
+  mc.G = G;
+  mc.sum = sum ? 1 : 0;
+  int tqmax = 0;
+  for (int g = 0; g < G; ++g) {
+    const FoConvDesc& e = d[g];
+    mc.a[g] = ConvArgs{e.x, (const bf16_t*)e.wp, e.bias, e.out, Cin, e.Tin, Cout, e.K, e.dil, e.pad, e.Tq, e.ostride,
+                       e.ooff, e.Tout_total, nks_per_chunk(e.K, pick_ck(Cin)), e.pre_leaky, e.slope, e.res, e.res2,
+                       e.oscale, e.gadd};
+    if (int rc = conv_check(mc.a[g])) return rc;
+    for (int h = 0; h < G; ++h)  // another member's output must not be this one's input (no order inside a launch)
+      FO_REQUIRE(h == g || (const void*)d[h].out != (const void*)e.x, "fo_conv_cl_multi: conv %d reads conv %d's output",
+                 g, h);
+    if (sum) FO_REQUIRE(e.Tq == d[0].Tq, "fo_conv_cl_multi: summed convs need one output range");
+    tqmax = e.Tq > tqmax ? e.Tq : tqmax;
+  }
+  if (!sum)
+    for (int g = 0; g < G; ++g)
+      for (int h = g + 1; h < G; ++h)
+        FO_REQUIRE(d[g].out != d[h].out || d[g].ostride > 1, "fo_conv_cl_multi: convs %d and %d write one output", g, h);
+  return conv_launch(mc, tqmax, s);
 }
 
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s) {

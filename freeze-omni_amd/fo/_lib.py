@@ -20,6 +20,14 @@ c_ll = ctypes.c_longlong
 c_float = ctypes.c_float
 c_vp = ctypes.c_void_p
 
+class FoConvDesc(ctypes.Structure):
+    """include/fo_hip.h FoConvDesc (fo_conv_cl_multi)."""
+    _fields_ = [("x", c_vp), ("wp", c_vp), ("bias", c_vp), ("out", c_vp), ("Tin", c_int), ("K", c_int),
+                ("dil", c_int), ("pad", c_int), ("Tq", c_int), ("ostride", c_int), ("ooff", c_int),
+                ("Tout_total", c_int), ("pre_leaky", c_int), ("slope", c_float), ("res", c_vp), ("res2", c_vp),
+                ("oscale", c_float), ("gadd", c_vp)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "fo_version": (c_int, []),
@@ -97,6 +105,7 @@ _SIGS = {
     "fo_scale_add_channel": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_conv_pack_elems": (c_ll, [c_int, c_int, c_int]),
     "fo_pack_conv": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "fo_conv_cl_multi": (c_int, [ctypes.POINTER(FoConvDesc), c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fo_conv_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_int, c_int, c_float, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
     "fo_codec_embed_cl": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp]),

@@ -63,6 +63,13 @@ class CodecEngine:
                 phases.append((r, pc, pc.K - 1 - off))  # (phase, weights, pad of the equivalent conv)
             self.p_ups.append(phases)
         self.use_graphs = os.environ.get("FO_CODEC_GRAPH", "1") != "0"
+        # ResBlock1 stages as grouped launches (fo_conv_cl_multi): the u polyphase components of each upsampling
+        # in one launch, the stage's resblock chains side by side (one launch per conv position), their last
+        # convs summed into the stage output by one launch -- 7 launches a stage instead of u + 18.
+        # FO_CODEC_GROUPED=0: one launch per conv (A/B)
+        self.grouped = (h["resblock"] == "1" and os.environ.get("FO_CODEC_GROUPED", "1") != "0"
+                        and len({len(c) for _, c in self.res[0]}) == 1 and len(self.res[0]) <= 5
+                        and max(h["upsample_rates"]) <= 5)
         self._graphs = {}   # (B, T) -> static buffers (+ captured graph), least recently used first
         self.p_res = [[(k, [(ops.PackedConv(c1[0], c1[1]), c1[2], None if c2 is None else ops.PackedConv(c2[0], c2[1]))
                             for c1, c2 in convs]) for k, convs in stage] for stage in self.res]
@@ -92,8 +99,11 @@ class CodecEngine:
         C, L = self.U, T
         for w, b, u, k in self.ups:
             C, L = C // 2, (L - 1) * u - 2 * ((k - u) // 2) + k
-            bufs.stages.append(SimpleNamespace(C=C, L=L, up=torch.empty(B, L, C, **F), t1=torch.empty(B, L, C, **F),
-                                               ya=torch.empty(B, L, C, **F), yb=torch.empty(B, L, C, **F),
+            nb = len(self.res[0]) if self.grouped else 1   # one chain's buffers per resblock
+            bufs.stages.append(SimpleNamespace(C=C, L=L, up=torch.empty(B, L, C, **F),
+                                               t1=[torch.empty(B, L, C, **F) for _ in range(nb)],
+                                               ya=[torch.empty(B, L, C, **F) for _ in range(nb)],
+                                               yb=[torch.empty(B, L, C, **F) for _ in range(nb)],
                                                xs=torch.empty(B, L, C, **F)))
         bufs.out = torch.empty(B, L, **F)
         return bufs
@@ -110,12 +120,22 @@ class CodecEngine:
         x, C, L = bf.y0, self.U, T
         for i, (w, b, u, k) in enumerate(self.ups):
             S = bf.stages[i]
-            for r, pc, pad_r in self.p_ups[i]:  # leaky -> ConvTranspose1d as u polyphase convs
-                Tq = (S.L - r + u - 1) // u
-                ops.conv_cl(x, B, C, L, pc, 1, pad_r, S.up, Tq=Tq, ostride=u, ooff=r, Tout_total=S.L, pre_leaky=0.1)
+            if self.grouped:   # leaky -> ConvTranspose1d as u polyphase convs, one launch
+                ops.conv_cl_multi([ops.conv_desc(x, L, pc, 1, pad_r, S.up, Tq=(S.L - r + u - 1) // u, ostride=u, ooff=r,
+                                                 Tout_total=S.L, pre_leaky=0.1) for r, pc, pad_r in self.p_ups[i]],
+                                  B, C, S.C, self.device)
+            else:
+                for r, pc, pad_r in self.p_ups[i]:  # leaky -> ConvTranspose1d as u polyphase convs
+                    Tq = (S.L - r + u - 1) // u
+                    ops.conv_cl(x, B, C, L, pc, 1, pad_r, S.up, Tq=Tq, ostride=u, ooff=r, Tout_total=S.L,
+                                pre_leaky=0.1)
             C, L = S.C, S.L
             nk = len(self.p_res[i])
             gadd = bf.g if C == bf.g.shape[1] else None
+            if self.grouped:
+                self._stage_grouped(S, B, C, L, self.p_res[i], gadd)
+                x = S.xs
+                continue
             for j, (kk, convs) in enumerate(self.p_res[i]):
                 src, last_j = S.up, j == nk - 1
                 for m, (p1, d1, p2) in enumerate(convs):
@@ -123,18 +143,39 @@ class CodecEngine:
                         dst, res2 = S.xs, (S.xs if j > 0 else None)
                         osc, ga = (1.0 / nk, gadd) if last_j else (1.0, None)
                     else:
-                        dst, res2, osc, ga = (S.ya if src is not S.ya else S.yb), None, 1.0, None
+                        dst, res2, osc, ga = (S.ya[0] if src is not S.ya[0] else S.yb[0]), None, 1.0, None
                     if p2 is None:  # ResBlock2: y = y + conv(leaky(y))
                         ops.conv_cl(src, B, C, L, p1, d1, (kk * d1 - d1) // 2, dst, pre_leaky=0.1, res=src, res2=res2,
                                     oscale=osc, gadd=ga)
                     else:
-                        ops.conv_cl(src, B, C, L, p1, d1, (kk * d1 - d1) // 2, S.t1, pre_leaky=0.1)
-                        ops.conv_cl(S.t1, B, C, L, p2, 1, (kk - 1) // 2, dst, pre_leaky=0.1, res=src, res2=res2,
+                        ops.conv_cl(src, B, C, L, p1, d1, (kk * d1 - d1) // 2, S.t1[0], pre_leaky=0.1)
+                        ops.conv_cl(S.t1[0], B, C, L, p2, 1, (kk - 1) // 2, dst, pre_leaky=0.1, res=src, res2=res2,
                                     oscale=osc, gadd=ga)
                     src = dst
             x = S.xs
         w, b = self.conv_post
         ops.conv_post_cl(x, B, L, C, w, b, w.shape[-1], (w.shape[-1] - 1) // 2, 0.1, bf.out)
+
+    def _stage_grouped(self, S, B, C, L, res, gadd):
+        """The stage's ResBlock1 chains side by side (models.py:59-110, 221-238): for each dilation position m,
+        one launch of every chain's c1 and one of every chain's c2 (y_j = y_j + c2(leaky(c1(leaky(y_j))))); the
+        last c2 launch sums the chains into xs = (sum_j y_j) / num_kernels + g, so no chain's partial sum is
+        ever stored."""
+        dev, nk, nd = self.device, len(res), len(res[0][1])
+        src = [S.up] * nk
+        for m in range(nd):
+            ops.conv_cl_multi([ops.conv_desc(src[j], L, res[j][1][m][0], res[j][1][m][1],
+                                             (res[j][0] * res[j][1][m][1] - res[j][1][m][1]) // 2, S.t1[j],
+                                             pre_leaky=0.1) for j in range(nk)], B, C, C, dev)
+            if m < nd - 1:
+                dst = [S.ya[j] if src[j] is not S.ya[j] else S.yb[j] for j in range(nk)]
+                ops.conv_cl_multi([ops.conv_desc(S.t1[j], L, res[j][1][m][2], 1, (res[j][0] - 1) // 2, dst[j],
+                                                 pre_leaky=0.1, res=src[j]) for j in range(nk)], B, C, C, dev)
+                src = dst
+            else:
+                ops.conv_cl_multi([ops.conv_desc(S.t1[j], L, res[j][1][m][2], 1, (res[j][0] - 1) // 2, S.xs,
+                                                 pre_leaky=0.1, res=src[j], oscale=1.0 / nk, gadd=gadd)
+                                   for j in range(nk)], B, C, C, dev, summed=True)
 
     def __call__(self, ids):
         """ids: device int32 [B, T] codec token ids -> pcm [B, T*upsample] fp32 (tanh output).

@@ -469,6 +469,25 @@ def conv_cl(x, B, Cin, Tin, pc, dil, pad, out, Tq=None, ostride=1, ooff=0, Tout_
     return out
 
 
+def conv_desc(x, Tin, pc, dil, pad, out, Tq=None, ostride=1, ooff=0, Tout_total=None, pre_leaky=None, res=None,
+              res2=None, oscale=1.0, gadd=None):
+    """One member of a conv_cl_multi launch (arguments as conv_cl's); returns (descriptor, keep-alive refs)."""
+    Tq = Tin + 2 * pad - dil * (pc.K - 1) if Tq is None else Tq
+    Tout_total = Tq if Tout_total is None else Tout_total
+    d = _lib.FoConvDesc(x.data_ptr(), pc.packed.data_ptr(), ptr(pc.bias), out.data_ptr(), Tin, pc.K, dil, pad, Tq,
+                        ostride, ooff, Tout_total, 0 if pre_leaky is None else 1,
+                        0.0 if pre_leaky is None else float(pre_leaky), ptr(res), ptr(res2), float(oscale), ptr(gadd))
+    return d
+
+
+def conv_cl_multi(descs, B, Cin, Cout, device, summed=False):
+    """G = len(descs) convolutions in one launch (fo_conv_cl_multi): independent members (polyphase components,
+    parallel resblock chains), or summed=True: one output = (sum of the members' conv + bias + res) * oscale +
+    gadd of descs[0]."""
+    arr = (_lib.FoConvDesc * len(descs))(*descs)
+    _lib.call("fo_conv_cl_multi", arr, len(descs), B, Cin, Cout, 1 if summed else 0, stream(device))
+
+
 def codec_embed_cl(table, E, n_codes, ids, B, T, out):
     _lib.call("fo_codec_embed_cl", table.data_ptr(), E, n_codes, ids.data_ptr(), B, T, out.data_ptr(),
               stream(out.device))

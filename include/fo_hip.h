@@ -208,6 +208,25 @@ int fo_pack_conv(const void* W, int src_bf16, int Cout, int Cin, int K, int tran
 int fo_conv_cl(const float* x, int B, int Cin, int Tin, const void* wp, const float* bias, int Cout, int K, int dil,
                int pad, int Tq, int ostride, int ooff, int Tout_total, int pre_leaky, float slope, float* out,
                const float* res, const float* res2, float oscale, const float* gadd, hipStream_t s);
+/* One fo_conv_cl per descriptor, G (<= 5) of them in ONE launch, all Cin -> Cout over B batch rows: the u
+ * polyphase components of a ConvTranspose1d, or the independent ResBlock1 chains of a generator stage
+ * (models/decoder/ticodec/models.py:221-238: the resblocks of a stage all read the upsampled x and are
+ * averaged).  No descriptor may read another's output.  sum != 0: each output tile runs all G convs into one
+ * accumulator and stores (sum_g (conv_g + bias_g + res_g + res2_g)) * oscale + gadd with descriptor 0's out,
+ * oscale, gadd and output geometry (the resblocks' last convs and their mean, models.py:236-238). */
+typedef struct FoConvDesc {
+  const float* x;       /* [B][Tin][Cin] */
+  const void* wp;       /* fo_pack_conv output */
+  const float* bias;    /* [Cout] or NULL */
+  float* out;           /* [B][Tout_total][Cout] */
+  int Tin, K, dil, pad, Tq, ostride, ooff, Tout_total, pre_leaky;
+  float slope;
+  const float* res;     /* like out, or NULL */
+  const float* res2;
+  float oscale;
+  const float* gadd;    /* [B][Cout] or NULL */
+} FoConvDesc;
+int fo_conv_cl_multi(const FoConvDesc* descs, int G, int B, int Cin, int Cout, int sum, hipStream_t s);
 /* Quantizer.embed (models/decoder/ticodec/models.py:661-700), channel-last output */
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 /* xs / num_kernels (+ global feature, models.py:233-238), channel-last */
