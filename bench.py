@@ -28,8 +28,10 @@ import sys
 import time
 
 
-def _blas_threads_from_argv(default=16):
-    """--cpu-threads, read before numpy is imported so the BLAS pool is created at that size."""
+def _blas_threads_from_argv(default=64):
+    """--cpu-threads, read before numpy is imported so the BLAS pool is created at that size.  Default 64: one
+    socket of the GPU box's 2 x 64-core host (SURVEY §8(d) asks for os.cpu_count() threads or at least a socket);
+    the box's cgroup quota admits 16 CPUs of time, which the line states beside the thread count."""
     n = default
     for i, a in enumerate(sys.argv):
         if a == "--cpu-threads" and i + 1 < len(sys.argv):
@@ -70,8 +72,8 @@ def parse():
     ap.add_argument("--scenario", default="turn", choices=["turn", "duplex"],
                     help="turn: config 3 (default, the headline line); duplex: config 5 sessions")
     ap.add_argument("--duplex-sec", type=float, default=60.0, help="duplex: seconds of audio per session")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="BLAS threads of the cpu_baseline leg (set before numpy is imported)")
+    ap.add_argument("--cpu-threads", type=int, default=64,
+                    help="BLAS threads of the cpu_baseline leg (set before numpy is imported; default one socket)")
     ap.add_argument("--no-single-user", action="store_true", help="skip the config-2 (1 user) leg")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
