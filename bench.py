@@ -428,42 +428,46 @@ def cpu_baseline(cfg_name, threads, text_tokens, sentence_tokens, codec_tokens):
         feats = np.load(os.path.join(ROOT, "tests", "golden", "fbank.npz"))["A_feats"]
         n_sent = (text_tokens + sentence_tokens - 1) // sentence_tokens
         per = [codec_tokens // n_sent] * n_sent
-        t0 = time.perf_counter()
-        kv = nets.KV(n_layers)
-        V = cfg["llm"]["vocab_size"]
+        def config1_run():
+            t0 = time.perf_counter()
+            kv = nets.KV(n_layers)
+            V = cfg["llm"]["vocab_size"]
 
-        def emb(ids):   # Qwen2-7B-Instruct chat-template ids (configs.QWEN2_IDS), folded into a smaller vocabulary
-            return llm.embed([i % V for i in ids])
+            def emb(ids):   # Qwen2-7B-Instruct chat-template ids (configs.QWEN2_IDS), folded into a smaller vocabulary
+                return llm.embed([i % V for i in ids])
 
-        llm.forward(emb(list(range(1, 16))), kv)                    # 'pre': the system role (15 tokens)
-        est, ac = nets.new_encoder_state(enc.nb), None
-        for c in range(len(feats)):                                 # listen: 13 chunks
-            e = enc.infer(feats[c], est)
-            a, ac = ada(e, ac)
-            if c == 0:
-                a = np.concatenate([emb([151645, 198, 151644, 872, 198]), a])   # user chat prefix
-            h = llm.forward(a, kv)
-            nets.state_probs(W, h)
-        t_listen = time.perf_counter() - t0
-        h = llm.forward(emb([151645, 198, 151644, 77091, 198]), kv)   # dialog_ss: assistant prefix
-        toks, hids = [], []
-        for j in range(text_tokens):
-            hids.append(h[-1])
-            tok = int(np.argmax(llm.logits(h[-1:])[0]))
-            toks.append(tok)
-            if j < text_tokens - 1:
-                h = llm.forward(llm.embed([tok]), kv)
-        for si in range(n_sent):                                    # speak, sentence by sentence
-            sl = slice(si * sentence_tokens, (si + 1) * sentence_tokens)
-            kvt, P = tts.prefill(llm.embed(toks[sl]).reshape(-1, idim), np.stack(hids[sl]).reshape(-1, idim))
-            cur, ids = tts.vocab + 1, []
-            for _ in range(per[si]):
-                lg = tts.step(cur, kvt, P)
-                cur = int(np.argmax(lg[:n_codes]))                  # EOS masked (benchmark policy)
-                ids.append(cur)
-            for T in vocoder_calls(per[si]):                     # the calls' token counts (which ids: immaterial)
-                codec(np.asarray(ids[:T]))
-        config1 = time.perf_counter() - t0
+            llm.forward(emb(list(range(1, 16))), kv)                    # 'pre': the system role (15 tokens)
+            est, ac = nets.new_encoder_state(enc.nb), None
+            for c in range(len(feats)):                                 # listen: 13 chunks
+                e = enc.infer(feats[c], est)
+                a, ac = ada(e, ac)
+                if c == 0:
+                    a = np.concatenate([emb([151645, 198, 151644, 872, 198]), a])   # user chat prefix
+                h = llm.forward(a, kv)
+                nets.state_probs(W, h)
+            t_listen = time.perf_counter() - t0
+            h = llm.forward(emb([151645, 198, 151644, 77091, 198]), kv)   # dialog_ss: assistant prefix
+            toks, hids = [], []
+            for j in range(text_tokens):
+                hids.append(h[-1])
+                tok = int(np.argmax(llm.logits(h[-1:])[0]))
+                toks.append(tok)
+                if j < text_tokens - 1:
+                    h = llm.forward(llm.embed([tok]), kv)
+            for si in range(n_sent):                                    # speak, sentence by sentence
+                sl = slice(si * sentence_tokens, (si + 1) * sentence_tokens)
+                kvt, P = tts.prefill(llm.embed(toks[sl]).reshape(-1, idim), np.stack(hids[sl]).reshape(-1, idim))
+                cur, ids = tts.vocab + 1, []
+                for _ in range(per[si]):
+                    lg = tts.step(cur, kvt, P)
+                    cur = int(np.argmax(lg[:n_codes]))                  # EOS masked (benchmark policy)
+                    ids.append(cur)
+                for T in vocoder_calls(per[si]):                     # the calls' token counts (which ids: immaterial)
+                    codec(np.asarray(ids[:T]))
+            config1 = time.perf_counter() - t0
+            return config1, t_listen, kv, est, ac, toks
+
+        config1, t_listen, kv, est, ac, toks = config1_run()
         # ---------------------------------------------------------------- units
         e = enc.infer(feats[0], est)
         t = time.perf_counter()
@@ -486,6 +490,13 @@ def cpu_baseline(cfg_name, threads, text_tokens, sentence_tokens, codec_tokens):
         t = time.perf_counter()
         codec(rng.integers(0, n_codes, 60))
         u4 = time.perf_counter() - t
+        # the same config-1 run at the cgroup quota's thread count, when the threads above exceed it (the box
+        # admits 16 CPUs of time: 64 BLAS threads there only time-slice, so this is the faster CPU number)
+        quota = cpu_quota()
+        config1_q = None
+        if limiter is not None and quota and quota < used:
+            with threadpool_limits(limits=quota, user_api="blas"):
+                config1_q = config1_run()[0]
     finally:
         if limiter is not None:
             limiter.restore_original_limits()
@@ -501,6 +512,8 @@ def cpu_baseline(cfg_name, threads, text_tokens, sentence_tokens, codec_tokens):
                        f" = {config1:.2f} s; {used} BLAS threads ({blas_lib}) within a cgroup quota of {cpu_quota()} "
                        f"CPUs of {os.cpu_count()} ({cpu_model()})"),
             "config1_s": round(config1, 3), "config1_listen_s": round(t_listen, 3),
+            "config1_s_at_quota_threads": None if config1_q is None else round(config1_q, 3),
+            "value_at_quota_threads": None if config1_q is None else round(audio1 / config1_q, 4),
             "config2_rtf_from_units": round(10.0 / turn2, 4),
             "host_cpus": os.cpu_count(), "cpu_quota": cpu_quota(), "cpu_model": cpu_model(),
             "units_ms": {"U1": round(u1 * 1e3, 2), "U2": round(u2 * 1e3, 2), "U3": round(u3 * 1e3, 3),

@@ -223,6 +223,242 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
   }
 }
 
+// One ResBlock1 step with both of its convolutions in one workgroup (models/decoder/ticodec/models.py:90-110):
+//   y = x + c2(leaky(c1(leaky(x))))      c1: K taps, dilation d;  c2: K taps, dilation 1;  C -> C channels
+// A workgroup owns a time tile [t0, t0 + TW) of one batch row and ALL C output channels (c2 reads every channel of
+// c1's output).  Phase A computes c1 on the extended rows [t0 - 8, t0 + TW + 8) (8 >= c2's half width) into LDS as
+// leaky'd bf16 hi + lo, zero outside the sequence (c2's zero padding); phase B computes c2 from that LDS tile and
+// adds the bias and the residual x.  The intermediate never goes to memory: per step one read of x and one write
+// of y instead of x -> t1 -> y through HBM, and one launch instead of two.  Members as in ConvMulti (blockIdx.z =
+// b + B * g: the stage's resblock chains side by side); sum != 0: a workgroup runs every member into one c2
+// accumulator and stores (sum_g y_g) * oscale + gadd (the chains' last step and their mean, models.py:236-238).
+struct PairArgs {
+  const float* x;      // [B][T][C] chain input, also the residual
+  const bf16_t* w1;    // c1 packed (fo_pack_conv, Cin = Cout = C)
+  const float* b1;
+  const bf16_t* w2;    // c2 packed
+  const float* b2;
+  float* out;          // [B][T][C]
+  int K, dil, nks_c;
+};
+struct PairMulti {
+  PairArgs a[CONV_MAXG];
+  int B, G, sum, T;
+  float slope, oscale;
+  const float* gadd;   // [B][C] or null
+};
+constexpr int PAIR_OFF = 8;  // phase A's extra rows on each side (>= (K - 1) / 2 for K <= 11... up to 17)
+
+template <int MTW, int NTW, int CK>
+__global__ __launch_bounds__(256) void k_conv_pair(PairMulti pm) {
+  constexpr int C = 16 * MTW;
+  constexpr int TW = 64 * NTW;
+  constexpr int R1 = TW + 2 * PAIR_OFF;       // phase A rows (a multiple of 16)
+  constexpr int NT1 = R1 / 16;                // phase A time tiles
+  constexpr int NA = (NT1 + 3) / 4;           // phase A tiles per wave (the last round on a few waves)
+  constexpr int ROWS = R1 + HALO;             // x window rows
+  constexpr int LP = CK + 8, LT = C + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 xh[ROWS][LP];
+  __shared__ __attribute__((aligned(16))) __bf16 xl[ROWS][LP];
+  __shared__ __attribute__((aligned(16))) __bf16 th[R1][LT];
+  __shared__ __attribute__((aligned(16))) __bf16 tlo[R1][LT];
+  __shared__ __attribute__((aligned(16))) bf16_t wl[MTW * conv_wmax(CK) * 512];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t0 = blockIdx.x * TW;
+  const int g0 = pm.sum ? 0 : (int)blockIdx.z / pm.B;
+  const int b = pm.sum ? (int)blockIdx.z : (int)blockIdx.z % pm.B;
+  const int g1 = pm.sum ? pm.G : g0 + 1;
+  const int T = pm.T;
+  const int kq = 8 * (lane >> 4);
+  constexpr int NCH = C / CK;
+
+  f32x4 acc2[MTW][NTW];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc2[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // weights of Cin chunk c of a packed conv into wl (LDS-DMA, one fragment per wave-instruction)
+  auto stage_w = [&](const bf16_t* wp, int nks_c, int c) {
+    const int nks = NCH * nks_c;
+    for (int f = wave; f < MTW * nks_c; f += 4) {
+      const int m = f / nks_c, st = f - m * nks_c;
+      const bf16_t* src = wp + ((size_t)m * nks + c * nks_c + st) * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)&wl[f * 512], 16, 0, 0);
+    }
+  };
+
+  for (int g = g0; g < g1; ++g) {
+    const PairArgs& a = pm.a[g];
+    const int p1 = a.dil * (a.K - 1) / 2, p2 = (a.K - 1) / 2;
+    const int span = R1 + a.dil * (a.K - 1);
+    const float* xb = a.x + (size_t)b * T * C;
+    // ---- phase A: c1 over rows r <-> time t0 - PAIR_OFF + r
+    f32x4 acc1[MTW][NA];
+#pragma unroll
+    for (int m = 0; m < MTW; ++m)
+#pragma unroll
+      for (int i = 0; i < NA; ++i) acc1[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int MAXL = (ROWS * (CK / 4) + 255) / 256;
+    for (int c = 0; c < NCH; ++c) {
+      __syncthreads();  // previous readers of xh / xl / wl are done
+      stage_w(a.w1, a.nks_c, c);
+      float4 v[MAXL];
+#pragma unroll
+      for (int i = 0; i < MAXL; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        const int row = e / (CK / 4), c4 = e % (CK / 4);
+        const int ti = t0 - PAIR_OFF - p1 + row;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < span * (CK / 4) && ti >= 0 && ti < T)
+          v[i] = *reinterpret_cast<const float4*>(xb + (size_t)ti * C + c * CK + c4 * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < MAXL; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        if (e >= span * (CK / 4)) break;
+        const int row = e / (CK / 4), c4 = e % (CK / 4);
+        float f[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        __attribute__((ext_vector_type(4))) __bf16 h4, l4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f[q] = f[q] < 0.f ? f[q] * pm.slope : f[q];
+          const __bf16 h = (__bf16)f[q];
+          h4[q] = h;
+          l4[q] = (__bf16)(f[q] - (float)h);
+        }
+        *reinterpret_cast<decltype(h4)*>(&xh[row][c4 * 4]) = h4;
+        *reinterpret_cast<decltype(l4)*>(&xl[row][c4 * 4]) = l4;
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      for (int s = 0; s < a.nks_c; ++s) {
+        const int kk = s * 32 + kq;
+        int j = kk / CK;
+        const int cil = kk - j * CK;
+        if (j > a.K - 1) j = a.K - 1;
+        bf16x8 av[MTW];
+#pragma unroll
+        for (int m = 0; m < MTW; ++m) av[m] = *reinterpret_cast<const bf16x8*>(&wl[(m * a.nks_c + s) * 512 + lane * 8]);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int n = wave + 4 * i;
+          if (n >= NT1) continue;
+          const int rb = n * 16 + (lane & 15) + j * a.dil;
+          const bf16x8 hi = *reinterpret_cast<const bf16x8*>(&xh[rb][cil]);
+          const bf16x8 lo = *reinterpret_cast<const bf16x8*>(&xl[rb][cil]);
+#pragma unroll
+          for (int m = 0; m < MTW; ++m) {
+            acc1[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], hi, acc1[m][i], 0, 0, 0);
+            acc1[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], lo, acc1[m][i], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // c1 output + bias -> leaky (c2's pre-activation) -> zero outside [0, T) -> bf16 hi + lo tile in LDS
+    __syncthreads();  // (the previous member's phase B readers of th / tlo are done)
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int n = wave + 4 * i;
+      if (n >= NT1) continue;
+      const int r = n * 16 + (lane & 15);
+      const int t = t0 - PAIR_OFF + r;
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const int co = m * 16 + kq / 2;
+        const float4 bb = a.b1 ? *reinterpret_cast<const float4*>(a.b1 + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float f[4] = {acc1[m][i][0] + bb.x, acc1[m][i][1] + bb.y, acc1[m][i][2] + bb.z, acc1[m][i][3] + bb.w};
+        __attribute__((ext_vector_type(4))) __bf16 h4, l4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = f[q] < 0.f ? f[q] * pm.slope : f[q];
+          if (t < 0 || t >= T) v = 0.f;
+          const __bf16 h = (__bf16)v;
+          h4[q] = h;
+          l4[q] = (__bf16)(v - (float)h);
+        }
+        *reinterpret_cast<decltype(h4)*>(&th[r][co]) = h4;
+        *reinterpret_cast<decltype(l4)*>(&tlo[r][co]) = l4;
+      }
+    }
+    // ---- phase B: c2 over the workgroup's TW rows, B operands from the c1 tile
+    const int tlb = wave * 16 * NTW + (lane & 15);
+    for (int c = 0; c < NCH; ++c) {
+      __syncthreads();  // th / tlo complete; the previous chunk's wl readers are done
+      stage_w(a.w2, a.nks_c, c);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      for (int s = 0; s < a.nks_c; ++s) {
+        const int kk = s * 32 + kq;
+        int j = kk / CK;
+        const int cil = kk - j * CK;
+        if (j > a.K - 1) j = a.K - 1;
+        bf16x8 av[MTW];
+#pragma unroll
+        for (int m = 0; m < MTW; ++m) av[m] = *reinterpret_cast<const bf16x8*>(&wl[(m * a.nks_c + s) * 512 + lane * 8]);
+        const int rb = PAIR_OFF - p2 + tlb + j;
+#pragma unroll
+        for (int n = 0; n < NTW; ++n) {
+          const bf16x8 hi = *reinterpret_cast<const bf16x8*>(&th[rb + 16 * n][c * CK + cil]);
+          const bf16x8 lo = *reinterpret_cast<const bf16x8*>(&tlo[rb + 16 * n][c * CK + cil]);
+#pragma unroll
+          for (int m = 0; m < MTW; ++m) {
+            acc2[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], hi, acc2[m][n], 0, 0, 0);
+            acc2[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], lo, acc2[m][n], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  // epilogue: out = (sum_g (c2_g + b2_g + x_g)) * oscale + gadd
+  const int tlb = wave * 16 * NTW + (lane & 15);
+  float4 add[NTW][MTW], bb[MTW];
+#pragma unroll
+  for (int n = 0; n < NTW; ++n)
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) add[n][m] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) bb[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g = g0; g < g1; ++g) {
+    const PairArgs& a = pm.a[g];
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) {
+      const int t = min(t0 + tlb + 16 * n, T - 1);
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const float4 v = *reinterpret_cast<const float4*>(a.x + ((size_t)b * T + t) * C + m * 16 + kq / 2);
+        add[n][m].x += v.x; add[n][m].y += v.y; add[n][m].z += v.z; add[n][m].w += v.w;
+      }
+    }
+    if (a.b2) {
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const float4 v = *reinterpret_cast<const float4*>(a.b2 + m * 16 + kq / 2);
+        bb[m].x += v.x; bb[m].y += v.y; bb[m].z += v.z; bb[m].w += v.w;
+      }
+    }
+  }
+  float* out = pm.a[g0].out;
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) {
+    const int t = t0 + tlb + 16 * n;
+    if (t >= T) continue;
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) {
+      const int co = m * 16 + kq / 2;
+      const float4 gg = pm.gadd ? *reinterpret_cast<const float4*>(pm.gadd + (size_t)b * C + co)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 v;
+      v.x = (acc2[m][n][0] + bb[m].x + add[n][m].x) * pm.oscale + gg.x;
+      v.y = (acc2[m][n][1] + bb[m].y + add[n][m].y) * pm.oscale + gg.y;
+      v.z = (acc2[m][n][2] + bb[m].z + add[n][m].z) * pm.oscale + gg.z;
+      v.w = (acc2[m][n][3] + bb[m].w + add[n][m].w) * pm.oscale + gg.w;
+      *reinterpret_cast<float4*>(out + ((size_t)b * T + t) * C + co) = v;
+    }
+  }
+}
+
 // Pack W (conv: [Cout][Cin][K]; transposed conv: [Cin][Cout][Ktot], taps j0 + u*m of one phase,
 // reversed) into A fragments with K ordered (chunk of CK channels, tap, channel), each chunk
 // padded to whole 32-wide k-steps.
@@ -385,10 +621,21 @@ static int conv_launch(ConvMulti& mc, int Tq_max, hipStream_t s) {
     MTW = 2;
     NTW = 2;
   }
+  // FO_CONV_HALFT=1 (A/B probe): half the time tile on the narrow late stages (Cout <= 32: 16 or 32 channels,
+  // 18k-36k steps per user) -- less LDS and fewer registers per workgroup, more workgroups per CU
+  static int halft = -1;
+  if (halft < 0) {
+    const char* e = getenv("FO_CONV_HALFT");
+    halft = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (halft && MTW <= 2 && NTW == 8 / MTW && CK <= 32) NTW /= 2;
   dim3 grid((Tq_max + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B * zg);
   if (MTW == 1 && CK == 64) grid.x = (Tq_max + 255) / 256;
   if (MTW == 2 && NTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 2, 64>), grid, dim3(256), 0, s, mc);
   else if (MTW == 2 && NTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 2, 32>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 2 && NTW == 2 && CK == 16) hipLaunchKernelGGL((k_conv_cl<2, 2, 16>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 1 && NTW == 4 && CK == 32) hipLaunchKernelGGL((k_conv_cl<1, 4, 32>), grid, dim3(256), 0, s, mc);
+  else if (MTW == 1 && NTW == 4 && CK == 16) hipLaunchKernelGGL((k_conv_cl<1, 4, 16>), grid, dim3(256), 0, s, mc);
   else if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, mc);
   else if (MTW == 2 && NTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, mc);
   else if (MTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 4, 32>), grid, dim3(256), 0, s, mc);
@@ -439,6 +686,45 @@ int fo_conv_cl_multi(const FoConvDesc* d, int G, int B, int Cin, int Cout, int s
       for (int h = g + 1; h < G; ++h)
         FO_REQUIRE(d[g].out != d[h].out || d[g].ostride > 1, "fo_conv_cl_multi: convs %d and %d write one output", g, h);
   return conv_launch(mc, tqmax, s);
+}
+
+int fo_conv_pair_multi(const FoPairDesc* d, int G, int B, int C, int T, int sum, float slope, float oscale,
+                       const float* gadd, hipStream_t s) {
+  FO_REQUIRE(d && G >= 1 && G <= CONV_MAXG && B >= 1 && T >= 1, "fo_conv_pair_multi: G=%d B=%d T=%d", G, B, T);
+  FO_REQUIRE(C == 16 || C == 32 || C == 64, "fo_conv_pair_multi: C=%d (16, 32 or 64)", C);
+  FO_REQUIRE(pick_ck(C) == (C >= 32 ? 32 : 16), "fo_conv_pair_multi: needs the default 32-channel chunks");
+  PairMulti pm{};
+  pm.B = B;
+  pm.G = G;
+  pm.sum = sum ? 1 : 0;
+  pm.T = T;
+  pm.slope = slope;
+  pm.oscale = oscale;
+  pm.gadd = gadd;
+  for (int g = 0; g < G; ++g) {
+    const FoPairDesc& e = d[g];
+    FO_REQUIRE(e.x && e.w1 && e.w2 && e.out, "fo_conv_pair_multi: member %d lacks a pointer", g);
+    FO_REQUIRE(e.K >= 1 && e.K <= CONV_KMAX && e.K % 2 == 1 && e.dil >= 1 && e.dil * (e.K - 1) <= HALO &&
+               (e.K - 1) / 2 <= PAIR_OFF, "fo_conv_pair_multi: K=%d dil=%d", e.K, e.dil);
+    FO_REQUIRE((const void*)e.out != (const void*)e.x, "fo_conv_pair_multi: out aliases the input");
+    for (int h = 0; h < G; ++h)
+      FO_REQUIRE(h == g || (const void*)d[h].out != (const void*)e.x, "fo_conv_pair_multi: member %d reads member %d's "
+                 "output", g, h);
+    if (!sum)
+      for (int h = g + 1; h < G; ++h)
+        FO_REQUIRE(d[h].out != e.out, "fo_conv_pair_multi: members %d and %d write one output", g, h);
+    pm.a[g] = PairArgs{e.x, (const bf16_t*)e.w1, e.b1, (const bf16_t*)e.w2, e.b2, e.out, e.K, e.dil,
+                       nks_per_chunk(e.K, pick_ck(C))};
+  }
+  const int zg = sum ? 1 : G;
+  if (C == 16) {
+    hipLaunchKernelGGL((k_conv_pair<1, 4, 16>), dim3((T + 255) / 256, 1, B * zg), dim3(256), 0, s, pm);
+  } else if (C == 32) {
+    hipLaunchKernelGGL((k_conv_pair<2, 2, 32>), dim3((T + 127) / 128, 1, B * zg), dim3(256), 0, s, pm);
+  } else {
+    hipLaunchKernelGGL((k_conv_pair<4, 2, 32>), dim3((T + 127) / 128, 1, B * zg), dim3(256), 0, s, pm);
+  }
+  return fo::check_launch("fo_conv_pair_multi");
 }
 
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s) {

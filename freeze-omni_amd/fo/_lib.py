@@ -28,6 +28,12 @@ class FoConvDesc(ctypes.Structure):
                 ("oscale", c_float), ("gadd", c_vp)]
 
 
+class FoPairDesc(ctypes.Structure):
+    """include/fo_hip.h FoPairDesc (fo_conv_pair_multi)."""
+    _fields_ = [("x", c_vp), ("w1", c_vp), ("b1", c_vp), ("w2", c_vp), ("b2", c_vp), ("out", c_vp), ("K", c_int),
+                ("dil", c_int)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "fo_version": (c_int, []),
@@ -106,6 +112,8 @@ _SIGS = {
     "fo_conv_pack_elems": (c_ll, [c_int, c_int, c_int]),
     "fo_pack_conv": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "fo_conv_cl_multi": (c_int, [ctypes.POINTER(FoConvDesc), c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "fo_conv_pair_multi": (c_int, [ctypes.POINTER(FoPairDesc), c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                                   c_vp, c_vp]),
     "fo_conv_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_int, c_int, c_float, c_vp, c_vp, c_vp, c_float, c_vp, c_vp]),
     "fo_codec_embed_cl": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp]),

@@ -67,6 +67,9 @@ class CodecEngine:
         # in one launch, the stage's resblock chains side by side (one launch per conv position), their last
         # convs summed into the stage output by one launch -- 7 launches a stage instead of u + 18.
         # FO_CODEC_GROUPED=0: one launch per conv (A/B)
+        # and the narrow stages' (16 / 32 / 64 channels) two convs of a ResBlock1 step in one workgroup
+        # (fo_conv_pair_multi), FO_CODEC_PAIR=0 to keep them apart (A/B)
+        self.pair = os.environ.get("FO_CODEC_PAIR", "1") != "0"
         self.grouped = (h["resblock"] == "1" and os.environ.get("FO_CODEC_GROUPED", "1") != "0"
                         and len({len(c) for _, c in self.res[0]}) == 1 and len(self.res[0]) <= 5
                         and max(h["upsample_rates"]) <= 5)
@@ -163,6 +166,16 @@ class CodecEngine:
         ever stored."""
         dev, nk, nd = self.device, len(res), len(res[0][1])
         src = [S.up] * nk
+        if self.pair and C in ops.PAIR_CHANNELS:
+            # narrow late stages: both convs of a step in one workgroup (fo_conv_pair_multi), c1's output in LDS
+            for m in range(nd):
+                last = m == nd - 1
+                dst = [S.xs] * nk if last else [S.ya[j] if src[j] is not S.ya[j] else S.yb[j] for j in range(nk)]
+                ops.conv_pair_multi([(src[j], res[j][1][m][0], res[j][1][m][2], res[j][0], res[j][1][m][1], dst[j])
+                                     for j in range(nk)], B, C, L, dev, summed=last,
+                                    oscale=1.0 / nk if last else 1.0, gadd=gadd if last else None)
+                src = dst
+            return
         for m in range(nd):
             ops.conv_cl_multi([ops.conv_desc(src[j], L, res[j][1][m][0], res[j][1][m][1],
                                              (res[j][0] * res[j][1][m][1] - res[j][1][m][1]) // 2, S.t1[j],

@@ -488,6 +488,20 @@ def conv_cl_multi(descs, B, Cin, Cout, device, summed=False):
     _lib.call("fo_conv_cl_multi", arr, len(descs), B, Cin, Cout, 1 if summed else 0, stream(device))
 
 
+PAIR_CHANNELS = (16, 32, 64)   # fo_conv_pair_multi's channel counts
+
+
+def conv_pair_multi(members, B, C, T, device, slope=0.1, summed=False, oscale=1.0, gadd=None):
+    """ResBlock1 steps y = x + c2(leaky(c1(leaky(x)))) side by side in one launch (fo_conv_pair_multi); members:
+    (x, pc1, pc2, K, dil, out) with PackedConv weights.  summed=True: members[0]'s out = (sum of the members' y) *
+    oscale + gadd."""
+    arr = (_lib.FoPairDesc * len(members))(*[
+        _lib.FoPairDesc(x.data_ptr(), p1.packed.data_ptr(), ptr(p1.bias), p2.packed.data_ptr(), ptr(p2.bias),
+                        out.data_ptr(), K, dil) for x, p1, p2, K, dil, out in members])
+    _lib.call("fo_conv_pair_multi", arr, len(members), B, C, T, 1 if summed else 0, float(slope), float(oscale),
+              ptr(gadd), stream(device))
+
+
 def codec_embed_cl(table, E, n_codes, ids, B, T, out):
     _lib.call("fo_codec_embed_cl", table.data_ptr(), E, n_codes, ids.data_ptr(), B, T, out.data_ptr(),
               stream(out.device))

@@ -227,6 +227,22 @@ typedef struct FoConvDesc {
   const float* gadd;    /* [B][Cout] or NULL */
 } FoConvDesc;
 int fo_conv_cl_multi(const FoConvDesc* descs, int G, int B, int Cin, int Cout, int sum, hipStream_t s);
+/* One ResBlock1 step y = x + c2(leaky(c1(leaky(x)))) per descriptor (models/decoder/ticodec/models.py:90-110;
+ * c1: K taps at dilation dil, c2: K taps at dilation 1, both C -> C, "same" padding), both convolutions in one
+ * workgroup (c1's output tile stays in LDS), G (<= 5) chains side by side in one launch.  C = 16, 32 or 64
+ * (the generator's narrow late stages).  sum != 0: one output = (sum_g y_g) * oscale + gadd into descs[0].out
+ * (the chains' last step and their mean, models.py:236-238); otherwise oscale 1 / gadd NULL. */
+typedef struct FoPairDesc {
+  const float* x;       /* [B][T][C], also the residual */
+  const void* w1;       /* c1 (fo_pack_conv) */
+  const float* b1;
+  const void* w2;       /* c2 */
+  const float* b2;
+  float* out;           /* [B][T][C] */
+  int K, dil;
+} FoPairDesc;
+int fo_conv_pair_multi(const FoPairDesc* descs, int G, int B, int C, int T, int sum, float slope, float oscale,
+                       const float* gadd, hipStream_t s);
 /* Quantizer.embed (models/decoder/ticodec/models.py:661-700), channel-last output */
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 /* xs / num_kernels (+ global feature, models.py:233-238), channel-last */
