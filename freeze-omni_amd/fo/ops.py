@@ -488,7 +488,10 @@ def conv_cl_multi(descs, B, Cin, Cout, device, summed=False):
     _lib.call("fo_conv_cl_multi", arr, len(descs), B, Cin, Cout, 1 if summed else 0, stream(device))
 
 
-PAIR_CHANNELS = (16, 32, 64)   # fo_conv_pair_multi's channel counts
+# channel counts that take fo_conv_pair_multi by default: 16 and 32 (r03l: the 16-channel stage 247 -> 173 us a
+# call, the 32-channel one 272 -> 233 us); at 64 channels the kernel needs 122 KB of LDS (one workgroup per CU)
+# and is slower than two launches (3 x 111 vs 6 x 43 us), so that stage keeps k_conv_cl
+PAIR_CHANNELS = (16, 32)
 
 
 def conv_pair_multi(members, B, C, T, device, slope=0.1, summed=False, oscale=1.0, gadd=None):
