@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include "fo_common.h"
+#include <hip/hip_ext.h>
 
 static thread_local char g_err[1024] = {0};
 
@@ -97,6 +98,16 @@ int fo_stream_create_prio(void** s_out, int level) {
   FO_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   hipStream_t s;
   FO_HIP(hipStreamCreateWithPriority(&s, hipStreamDefault, level > 0 ? hi : (level < 0 ? lo : 0)));
+  *s_out = (void*)s;
+  return 0;
+}
+// A blocking stream whose kernels run only on the CUs set in mask (nwords 32-bit words, bit i = CU i in the
+// runtime's CU numbering): the listen stages' CU partition (the encoder stage on a few CUs, the Qwen2 stage on
+// the rest, so no Qwen2 workgroup shares a CU with the encoder stage).
+int fo_stream_create_cumask(void** s_out, const unsigned* mask, int nwords) {
+  FO_REQUIRE(mask && nwords > 0, "fo_stream_create_cumask: empty mask");
+  hipStream_t s;
+  FO_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask));
   *s_out = (void*)s;
   return 0;
 }

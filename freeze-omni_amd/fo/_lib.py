@@ -46,6 +46,7 @@ _SIGS = {
     "fo_stream_create": (c_int, [ctypes.POINTER(c_vp)]),
     "fo_stream_create_prio": (c_int, [ctypes.POINTER(c_vp), c_int]),
     "fo_stream_priority_range": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "fo_stream_create_cumask": (c_int, [ctypes.POINTER(c_vp), ctypes.POINTER(ctypes.c_uint), c_int]),
     "fo_stream_destroy": (c_int, [c_vp]),
     "fo_stream_wait_event": (c_int, [c_vp, c_vp]),
     "fo_host_alloc": (c_int, [c_ll, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),

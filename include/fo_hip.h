@@ -29,6 +29,8 @@ int fo_stream_create(void** s_out);
 // level < 0: its least; 0: the default
 int fo_stream_create_prio(void** s_out, int level);
 int fo_stream_priority_range(int* least, int* greatest);
+/* a blocking stream restricted to the CUs set in mask (nwords 32-bit words; hipExtStreamCreateWithCUMask) */
+int fo_stream_create_cumask(void** s_out, const unsigned* mask, int nwords);
 int fo_stream_destroy(void* s);
 int fo_stream_wait_event(hipStream_t s, void* ev);
 int fo_host_alloc(long long bytes, void** host_ptr, void** dev_ptr);
