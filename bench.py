@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=64,
                     help="BLAS threads of the cpu_baseline leg (set before numpy is imported; default one socket)")
     ap.add_argument("--no-single-user", action="store_true", help="skip the config-2 (1 user) leg")
+    ap.add_argument("--switch-interval", type=float, default=None,
+                    help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
+                         "decode (default: the interpreter's 5 ms)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
 
@@ -713,6 +716,8 @@ def main_duplex(args, eng, dev, dist, world, rank, load_s):
 
 def main():
     args = parse()
+    if args.switch_interval:
+        sys.setswitchinterval(args.switch_interval)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

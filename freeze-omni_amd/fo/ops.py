@@ -33,6 +33,21 @@ SIDE_STREAM_PRIORITY = int(os.environ.get("FO_SIDE_PRIORITY", "0"))
 MAIN_STREAM_PRIORITY = int(os.environ.get("FO_MAIN_PRIORITY", "0"))
 
 
+# FO_ENC_CUS=k (probe): the side stream (the pipelined listen's encoder stage, fbank) runs on k CUs spread over the
+# device's 32-CU blocks and the engine stream on the others, so no Qwen2 workgroup shares a CU with the encoder's
+ENC_CUS = int(os.environ.get("FO_ENC_CUS", "0"))
+
+
+def _enc_partition(idx):
+    if ENC_CUS <= 0:
+        return None
+    n = torch.cuda.get_device_properties(idx).multi_processor_count
+    blk = n // 8
+    per = max(1, ENC_CUS // 8)
+    enc = sorted({x * blk + j for x in range(8) for j in range(per)})
+    return [c for c in range(n) if c not in set(enc)], enc, n
+
+
 def engine_stream(device, side=False, name=None):
     """A blocking HIP stream per device (fo_stream_create) wrapped for torch: it orders against the
     legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it.
@@ -47,7 +62,16 @@ def engine_stream(device, side=False, name=None):
     if key not in _ENGINE_STREAMS:
         h = ctypes.c_void_p()
         with torch.cuda.device(idx):
-            if name in HIGH_PRIORITY_STREAMS:
+            part = _enc_partition(idx) if name is None else None
+            if part is not None:   # listen-stage CU partition: side stream on the encoder's CUs, engine on the rest
+                cus = part[1] if side else part[0]
+                words = (part[2] + 31) // 32
+                m = (ctypes.c_uint * words)()
+                for c in cus:
+                    m[c // 32] |= 1 << (c % 32)
+                with torch.cuda.device(idx):
+                    _lib.call("fo_stream_create_cumask", ctypes.byref(h), m, words)
+            elif name in HIGH_PRIORITY_STREAMS:
                 _lib.call("fo_stream_create_prio", ctypes.byref(h), 1)
             elif name is None and side and SIDE_STREAM_PRIORITY:
                 _lib.call("fo_stream_create_prio", ctypes.byref(h), SIDE_STREAM_PRIORITY)
