@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=64,
                     help="BLAS threads of the cpu_baseline leg (set before numpy is imported; default one socket)")
     ap.add_argument("--no-single-user", action="store_true", help="skip the config-2 (1 user) leg")
+    ap.add_argument("--tts-workers", type=int, default=1,
+                    help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")
@@ -153,7 +155,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
     # 400 codec tokens per response (EOS masked until then), dealt over the sentences
     codec_per = [args.codec_tokens // n_sent + (1 if s < args.codec_tokens % n_sent else 0) for s in range(n_sent)]
     rec = SpeechRecorder(B)
-    tts = SentenceTTS(engine, args, rec) if args.concurrent_tts else None
+    tts = SentenceTTS(engine, args, rec, args.tts_workers) if args.concurrent_tts else None
     text_ids = [[] for _ in turns]
     hiddens = []
     nxt, hid = engine.text_step([(t.kv, pre) for t in turns])
@@ -165,7 +167,8 @@ def run_turn(engine, base_kv, pcms, args, sync):
         if (j + 1) % S == 0 or j == T - 1:
             # sentence boundary (benchmark policy: every S tokens; bin/inference.py:160-173 cuts at punctuation):
             # this sentence's speech starts now, while the text decode goes on (bin/inference.py:82-92)
-            job = (hiddens[s0:j + 1], [ids[s0:j + 1] for ids in text_ids], codec_per[len(rec.sentences)])
+            job = (hiddens[s0:j + 1], [ids[s0:j + 1] for ids in text_ids], codec_per[len(rec.sentences)],
+                   len(rec.sentences))
             rec.sentences.append(time.perf_counter())
             if tts is not None:
                 tts.submit(job)
@@ -183,6 +186,9 @@ def run_turn(engine, base_kv, pcms, args, sync):
         t.kv.free()
     stage = {"listen": (t_ss - t_begin) * 1e3, "text": (t_text - t_ss) * 1e3, "speak": (t_end - t_ss) * 1e3,
              "speak_after_text": (t_end - t_text) * 1e3, "listen_chunk0": (t_c0 - t_begin) * 1e3}
+    for k in sorted(rec.sent_end):   # per sentence: boundary -> speech start (queueing), start -> end
+        stage[f"sentence{k}_wait"] = (rec.sent_start[k] - rec.sentences[k]) * 1e3
+        stage[f"sentence{k}_speech"] = (rec.sent_end[k] - rec.sent_start[k]) * 1e3
     return dict(t_ss=t_ss, first=rec.first, last=rec.last, samples=rec.samples, first_pcm=rec.first_pcm,
                 stage=stage, n_sent=n_sent, codec_tokens=rec.codec_tokens)
 
@@ -197,6 +203,8 @@ class SpeechRecorder:
         self.samples = [0] * B
         self.codec_tokens = [0] * B
         self.sentences = []            # host time of each sentence boundary
+        self.sent_start = {}           # host time each sentence's speech started / ended (worker side)
+        self.sent_end = {}
 
     def segment(self, i, seg):
         now = time.perf_counter()      # the segment's length is known on the host: the cut index was read back
@@ -206,7 +214,7 @@ class SpeechRecorder:
         self.samples[i] += seg.numel()
 
 
-def run_sentence(engine, args, rec, hiddens, ids, n_codec, stream=None, voc=None):
+def run_sentence(engine, args, rec, hiddens, ids, n_codec, k=0, stream=None, voc=None):
     """llm2TTS.run for one sentence of every user (bin/inference.py:82-92): the sentence's text-token
     embeddings and LLM hidden rows, each reshaped to [-1, 896] sub-tokens, through the AR decoder (EOS masked
     until n_codec tokens) and the vocoder with silence-cut emission.  stream / voc: the AR
@@ -218,6 +226,7 @@ def run_sentence(engine, args, rec, hiddens, ids, n_codec, stream=None, voc=None
     from fo.speak import speak
     B, n = len(ids), len(ids[0])
     idim = engine.cfg["decoder_json"][0]
+    rec.sent_start[k] = time.perf_counter()
     with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
         ids_d = torch.tensor(ids, dtype=torch.int32).to(engine.device)
         emb = engine.llm.embed(ids_d.view(-1))
@@ -228,6 +237,7 @@ def run_sentence(engine, args, rec, hiddens, ids, n_codec, stream=None, voc=None
         for i, seg in speak(engine, items, top_k=args.top_k, min_tokens=n_codec, max_tokens=n_codec,
                             states_out=states, stream=stream, voc_stream=voc):
             rec.segment(i, seg)
+    rec.sent_end[k] = time.perf_counter()
     for i, st in enumerate(states):
         if rec.first_pcm[i] is None:
             rec.first_pcm[i] = st.t_first_pcm
@@ -241,37 +251,49 @@ class SentenceTTS:
     are those of the reference's sequential loop (bin/inference.py:152-183, which pauses the text decode for
     each sentence).  Sentences are spoken in order (one user's audio is a sequence)."""
 
-    def __init__(self, engine, args, rec):
+    def __init__(self, engine, args, rec, workers=1):
+        """workers > 1: sentence k goes to worker k % workers, each with its own streams, so a sentence's speech
+        does not queue behind the previous sentence's (the AR decode graphs and vocoder graphs are cached per
+        stream, fo/tts.py, fo/codec.py)."""
         import queue
         import threading
         from fo import ops
-        self.q = queue.Queue()
         self.err = None
-        self.stream = ops.engine_stream(engine.device, name="tts")
-        self.voc = ops.engine_stream(engine.device, name="voc")
+        self.k = 0
+        self.qs, self.ts = [], []
+        for w in range(workers):
+            q = queue.Queue()
+            sfx = "" if w == 0 else str(w)
+            stream = ops.engine_stream(engine.device, name="tts" + sfx)
+            voc = ops.engine_stream(engine.device, name="voc" + sfx)
 
-        def work():
-            import torch
-            torch.cuda.set_device(engine.device)
-            while True:
-                job = self.q.get()
-                if job is None:
-                    return
-                if self.err is None:
-                    try:
-                        run_sentence(engine, args, rec, *job, stream=self.stream, voc=self.voc)
-                    except BaseException as e:  # re-raised in the main thread by join()
-                        self.err = e
+            def work(q=q, stream=stream, voc=voc):
+                import torch
+                torch.cuda.set_device(engine.device)
+                while True:
+                    job = q.get()
+                    if job is None:
+                        return
+                    if self.err is None:
+                        try:
+                            run_sentence(engine, args, rec, *job, stream=stream, voc=voc)
+                        except BaseException as e:  # re-raised in the main thread by join()
+                            self.err = e
 
-        self.t = threading.Thread(target=work, daemon=True)
-        self.t.start()
+            t = threading.Thread(target=work, daemon=True)
+            t.start()
+            self.qs.append(q)
+            self.ts.append(t)
 
     def submit(self, job):
-        self.q.put(job)
+        self.qs[self.k % len(self.qs)].put(job)
+        self.k += 1
 
     def join(self):
-        self.q.put(None)
-        self.t.join()
+        for q in self.qs:
+            q.put(None)
+        for t in self.ts:
+            t.join()
         if self.err is not None:
             raise self.err
 
@@ -892,8 +914,9 @@ def main():
             # wall ms per stage of a timed turn (median over the timed turns): listen = 63 chunks through
             # fbank / encoder / adapter / Qwen2 / state head (pipelined), text = dialog_ss -> the last text
             # token's id on the host, speak = TTS prefill + AR decode + vocoder until the last PCM segment
+            # (+ per sentence: boundary -> its speech starting on the worker, and that speech's duration)
             "stage_ms": {k: round(float(np.median([s["stage"][k] for s in stats])), 2)
-                         for k in ("listen", "text", "speak", "speak_after_text", "listen_chunk0")},
+                         for k in stats[0]["stage"]},
             "single_user": single,
             "cpu_baseline": cpu,
         }

@@ -14,7 +14,7 @@ from .ops import F32, I32
 
 
 class CodecEngine:
-    MAX_GRAPHS = 16
+    MAX_GRAPHS = 32
 
     def __init__(self, src, codec_json, device):
         h = self.h = codec_json
@@ -73,7 +73,7 @@ class CodecEngine:
         self.grouped = (h["resblock"] == "1" and os.environ.get("FO_CODEC_GROUPED", "1") != "0"
                         and len({len(c) for _, c in self.res[0]}) == 1 and len(self.res[0]) <= 5
                         and max(h["upsample_rates"]) <= 5)
-        self._graphs = {}   # (B, T) -> static buffers (+ captured graph), least recently used first
+        self._graphs = {}   # (B, T, stream) -> static buffers (+ captured graph), least recently used first
         self.p_res = [[(k, [(ops.PackedConv(c1[0], c1[1]), c1[2], None if c2 is None else ops.PackedConv(c2[0], c2[1]))
                             for c1, c2 in convs]) for k, convs in stage] for stage in self.res]
 
@@ -196,7 +196,7 @@ class CodecEngine:
         non-default stream the call is one hipGraph replay per (B, T) (captured on first use; the
         ~100 launches of a call otherwise cost more host time than the GPU work)."""
         B, T = ids.shape
-        key = (B, T)
+        key = (B, T, ops.stream(self.device))   # static buffers per stream: calls on two streams may overlap
         bf = self._graphs.pop(key, None)
         if bf is None:
             if len(self._graphs) >= self.MAX_GRAPHS:   # least recently used (dict order) goes

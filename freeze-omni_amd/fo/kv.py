@@ -7,6 +7,8 @@ fixed-size pages ([layer][page][kv_head][slot][hd], fp32).  A sequence is a bloc
 shares full pages copy-on-write (refcounts), so N sessions forked from one system prompt store it
 once, and appending never moves existing keys.
 """
+import threading
+
 import numpy as np
 import torch
 
@@ -20,22 +22,25 @@ class KVPool:
         self.ref = np.zeros(n_pages, dtype=np.int32)
         self.free = list(range(n_pages - 1, -1, -1))
         self.device = torch.device(device)
+        self.lock = threading.Lock()   # sequences of one pool may grow from several host threads (speech workers)
 
     @property
     def bytes_per_token(self):
         return self.n_layers * self.n_kv * self.hd * 4 * 2
 
     def alloc(self):
-        if not self.free:
-            raise RuntimeError(f"KV pool exhausted ({self.n_pages} pages of {self.PS} tokens)")
-        p = self.free.pop()
-        self.ref[p] = 1
-        return p
+        with self.lock:
+            if not self.free:
+                raise RuntimeError(f"KV pool exhausted ({self.n_pages} pages of {self.PS} tokens)")
+            p = self.free.pop()
+            self.ref[p] = 1
+            return p
 
     def release(self, p):
-        self.ref[p] -= 1
-        if self.ref[p] == 0:
-            self.free.append(p)
+        with self.lock:
+            self.ref[p] -= 1
+            if self.ref[p] == 0:
+                self.free.append(p)
 
     def copy_page(self, src, dst):
         self.k[:, dst].copy_(self.k[:, src])

@@ -25,7 +25,7 @@ def stream(device=None):
 _ENGINE_STREAMS = {}
 
 
-HIGH_PRIORITY_STREAMS = ("tts", "voc")
+HIGH_PRIORITY_STREAMS = ("tts", "voc")   # name prefixes ("tts1", "voc1": a second speech worker's)
 # priority level of the side stream (the pipelined listen's encoder stage, the vocoder when no "voc" stream is
 # given): 0 default, -1 the device's least (FO_SIDE_PRIORITY, A/B probes)
 SIDE_STREAM_PRIORITY = int(os.environ.get("FO_SIDE_PRIORITY", "0"))
@@ -71,7 +71,7 @@ def engine_stream(device, side=False, name=None):
                     m[c // 32] |= 1 << (c % 32)
                 with torch.cuda.device(idx):
                     _lib.call("fo_stream_create_cumask", ctypes.byref(h), m, words)
-            elif name in HIGH_PRIORITY_STREAMS:
+            elif name is not None and name.startswith(HIGH_PRIORITY_STREAMS):
                 _lib.call("fo_stream_create_prio", ctypes.byref(h), 1)
             elif name is None and side and SIDE_STREAM_PRIORITY:
                 _lib.call("fo_stream_create_prio", ctypes.byref(h), SIDE_STREAM_PRIORITY)

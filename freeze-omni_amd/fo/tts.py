@@ -114,7 +114,9 @@ class TTSEngine:
         """Captured decode step for a batch of B sessions (cached; rebuilt when a bound grows).
         pen = (window, penalty) adds the repetition penalty before the draw (None: off).
         capture=False: the same step body launched directly each step (no graph)."""
-        key = (B, V_sample, top_k, seed, pen, capture)
+        # per stream: a graph's static buffers belong to the stream it was captured on and replays on (two
+        # sentences' speech may decode side by side on their own streams)
+        key = (B, V_sample, top_k, seed, pen, capture, ops.stream(self.device))
         g = self._graphs.get(key) if hasattr(self, "_graphs") else None
         if g is None or g.max_keys < max_keys or g.hist_rows < hist_rows:
             if not hasattr(self, "_graphs"):
