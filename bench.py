@@ -75,8 +75,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=64,
                     help="BLAS threads of the cpu_baseline leg (set before numpy is imported; default one socket)")
     ap.add_argument("--no-single-user", action="store_true", help="skip the config-2 (1 user) leg")
-    ap.add_argument("--tts-workers", type=int, default=1,
-                    help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N")
+    ap.add_argument("--tts-workers", type=int, default=2,
+                    help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N "
+                         "(2: a sentence's speech never queues behind the previous one's; r03p A/B 1 / 2 / 4 "
+                         "workers: 193.5x / 194.8-195.4x / 173.2x)")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")

@@ -684,13 +684,14 @@ class ListenPipe:
         pe_next, prev = pipe.push(items_c, decide)   # chunk c's next pe_index per session; results of c-1
         ...; last = pipe.flush()
 
-    push(items_c): queues chunk c's encoder stage (side stream), waits for chunk c-1's LLM stage and
-    reads its results (the state decision), then -- unless decide(results of c-1) returns False, the
-    reference's "stop listening on dialog_ss" -- queues chunk c's LLM stage and returns at once.  So the
-    LLM stage of chunk c is never queued before the decision on chunk c-1 (no speculation), the encoder
-    stage of chunk c overlaps the LLM stage of chunk c-1, and the caller prepares chunk c+1 (framing,
+    push(items_c): queues chunk c's encoder stage (side stream) and, behind chunk c-1's, chunk c's LLM stage
+    (engine stream), then waits for chunk c-1's LLM stage and reads its results (the state decision).  If
+    decide(results of c-1) returns False -- the reference's "stop listening on dialog_ss" -- chunk c's LLM
+    stage is rolled back (waited for, its KV rows truncated), so the context holds exactly the chunks before
+    it, as if it had never been queued.  The encoder stage of chunk c overlaps the LLM stage of chunk c-1,
+    the engine stream never idles on the host's read-back, and the caller prepares chunk c+1 (framing,
     fbank) while chunk c's LLM stage runs.  A refused chunk's encoder stage has run (its caches are reset
-    on dialog_ss anyway, bin/inference.py:133-135) but nothing was appended to the context.
+    on dialog_ss anyway, bin/inference.py:133-135).
     (encoder / adapter caches are advanced in place at submission, like listen().)
 
     Every push must be graphable (same identity and batch, no chat prefix, open caches); the results
@@ -713,17 +714,29 @@ class ListenPipe:
             self.g = g
             k = self.k
             pe = g.submit_encoder(items, k)
+            # chunk c's LLM stage is queued speculatively right behind chunk c-1's on the engine stream, so the
+            # stream never idles while the host reads c-1's state head back; if the decision on c-1 stops the
+            # listen (dialog_ss), chunk c is rolled back below and never reaches the context
+            g.submit_llm(items, pe, k, wait=False)
             out = None
             if self.pending is not None:
                 out = g.collect_llm(self.pending)
-                self.pending = None
-            if decide is not None and out is not None and not decide(out):
-                self.stopped = True
-                return pe, out
-            g.submit_llm(items, pe, k, wait=False)
             self.pending = k
             self.k = 1 - k
+            if decide is not None and out is not None and not decide(out):
+                self._roll_back(k)
+                self.stopped = True
             return pe, out
+
+    def _roll_back(self, k):
+        """Undo the speculative LLM stage in slot k: wait for it, drop the KV rows it appended."""
+        g = self.g
+        items, _ = g.inflight[k]
+        _lib.call("fo_event_sync", g.ev_llm[k])
+        g.inflight[k] = None
+        for it in items:
+            it["kv"].truncate(it["kv"].length - g.To)
+        self.pending = None
 
     def flush(self):
         if self.pending is None:

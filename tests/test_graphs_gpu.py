@@ -104,9 +104,9 @@ def test_listen_pipe_matches_sequential(eng, dev):
             np.testing.assert_array_equal(a, b)
 
 
-def test_listen_pipe_decide_stops_before_queuing(eng, dev):
-    """decide(results of chunk c-1) returning False (dialog_ss) queues nothing for chunk c: the context
-    holds exactly the chunks before it, and the states seen match the sequential run's."""
+def test_listen_pipe_decide_stops_and_rolls_back(eng, dev):
+    """decide(results of chunk c-1) returning False (dialog_ss) rolls back chunk c's speculatively queued LLM
+    stage: the context holds exactly the chunks before it, and the states seen match the sequential run's."""
     g = np.load(os.path.join(G, "fbank.npz"))
     n_users = 2
     feats = torch.from_numpy(g["A_feats"]).to(dev)
