@@ -359,3 +359,43 @@ def test_codec_graph_replay_matches_eager(dev, src):
             assert torch.equal(g, e), (B, T)
         assert len(eng._graphs) <= 2
     eng.destroy()
+
+
+def test_speak_two_workers_side_by_side_match_sequential(dev, speech_engine):
+    """Two sentences' speech decoded at the same time from two host threads on their own streams (the bench's
+    --tts-workers 2: per-stream decode / vocoder graph caches, a locked KV page pool) gives, sentence by
+    sentence, exactly the ids and PCM of speaking them one after the other on one stream."""
+    import threading
+    from fo import ops
+    from fo.speak import speak
+    jobs = [_items(dev, 3, 11), _items(dev, 3, 12)]
+    kw = dict(top_k=4, min_tokens=50, max_tokens=50, seed=5)
+
+    def run(items, stream=None, voc=None):
+        states = []
+        segs = [(i, s.cpu().numpy()) for i, s in speak(speech_engine, items, states_out=states, stream=stream,
+                                                        voc_stream=voc, **kw)]
+        return [s.all_ids for s in states], segs
+
+    ref = [run(j) for j in jobs]
+    got, errs = [None, None], []
+
+    def worker(w):
+        try:
+            torch.cuda.set_device(dev)
+            sfx = "" if w == 0 else str(w)
+            got[w] = run(jobs[w], ops.engine_stream(dev, name="tts" + sfx), ops.engine_stream(dev, name="voc" + sfx))
+        except BaseException as e:   # noqa: BLE001 (re-raised below)
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not errs, errs
+    for (ids_r, segs_r), (ids_g, segs_g) in zip(ref, got):
+        assert ids_g == ids_r
+        assert [i for i, _ in segs_g] == [i for i, _ in segs_r]
+        for (_, a), (_, b) in zip(segs_g, segs_r):
+            np.testing.assert_array_equal(a, b)
