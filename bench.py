@@ -566,7 +566,8 @@ def recorded_traffic(kernel_regex):
     command (profiles/rNN_fetch.json, written by scripts/summarize_profile.py: KiB x 1024 x 2)."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_fetch.json"))
+                   if re.fullmatch(r"r\d\d[a-z]*_fetch\.json", os.path.basename(f)))
     if not files:
         return None, None
     groups = [g for g in json.load(open(files[-1]))["groups"] if re.search(kernel_regex, g["kernel"])]
@@ -582,7 +583,9 @@ def recorded_kernel_avg_us(kernel_regex):
     import csv
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.csv")))
+    # only the bench's own summaries (rNN<letter>_kernel_stats.csv), not the AR-step / text-step ones
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.csv"))
+                   if re.fullmatch(r"r\d\d[a-z]*_kernel_stats\.csv", os.path.basename(f)))
     for f in reversed(files):
         rows = [r for r in csv.DictReader(open(f)) if re.search(kernel_regex, r["Name"])]
         if rows:
