@@ -79,6 +79,9 @@ def parse():
                     help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N "
                          "(2: a sentence's speech never queues behind the previous one's; r03p A/B 1 / 2 / 4 "
                          "workers: 193.5x / 194.8-195.4x / 173.2x)")
+    ap.add_argument("--tts-lane", action="store_true",
+                    help="one continuously batched speech lane (fo.speak.SpeechLane) instead of per-sentence workers: "
+                         "sentences whose speech overlaps decode in the same AR step")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")
@@ -157,7 +160,9 @@ def run_turn(engine, base_kv, pcms, args, sync):
     # 400 codec tokens per response (EOS masked until then), dealt over the sentences
     codec_per = [args.codec_tokens // n_sent + (1 if s < args.codec_tokens % n_sent else 0) for s in range(n_sent)]
     rec = SpeechRecorder(B)
-    tts = SentenceTTS(engine, args, rec, args.tts_workers) if args.concurrent_tts else None
+    tts = None
+    if args.concurrent_tts:
+        tts = LaneTTS(engine, args, rec) if args.tts_lane else SentenceTTS(engine, args, rec, args.tts_workers)
     text_ids = [[] for _ in turns]
     hiddens = []
     nxt, hid = engine.text_step([(t.kv, pre) for t in turns])
@@ -216,6 +221,19 @@ class SpeechRecorder:
         self.samples[i] += seg.numel()
 
 
+def sentence_items(engine, hiddens, ids):
+    """The sentence's AR-decoder inputs per user (bin/inference.py:82-92): its text-token embeddings and LLM
+    hidden rows, each reshaped to [-1, 896] sub-tokens (on the current stream)."""
+    import torch
+    B, n = len(ids), len(ids[0])
+    idim = engine.cfg["decoder_json"][0]
+    ids_d = torch.tensor(ids, dtype=torch.int32).to(engine.device)
+    emb = engine.llm.embed(ids_d.view(-1))
+    hs = torch.stack(hiddens, 1)  # [B, n, D]
+    return [(emb[b * n:(b + 1) * n].reshape(-1, idim).contiguous(), hs[b].reshape(-1, idim).contiguous())
+            for b in range(B)]
+
+
 def run_sentence(engine, args, rec, hiddens, ids, n_codec, k=0, stream=None, voc=None):
     """llm2TTS.run for one sentence of every user (bin/inference.py:82-92): the sentence's text-token
     embeddings and LLM hidden rows, each reshaped to [-1, 896] sub-tokens, through the AR decoder (EOS masked
@@ -226,15 +244,9 @@ def run_sentence(engine, args, rec, hiddens, ids, n_codec, k=0, stream=None, voc
 
     import torch
     from fo.speak import speak
-    B, n = len(ids), len(ids[0])
-    idim = engine.cfg["decoder_json"][0]
     rec.sent_start[k] = time.perf_counter()
     with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
-        ids_d = torch.tensor(ids, dtype=torch.int32).to(engine.device)
-        emb = engine.llm.embed(ids_d.view(-1))
-        hs = torch.stack(hiddens, 1)  # [B, n, D]
-        items = [(emb[b * n:(b + 1) * n].reshape(-1, idim).contiguous(), hs[b].reshape(-1, idim).contiguous())
-                 for b in range(B)]
+        items = sentence_items(engine, hiddens, ids)
         states = []
         for i, seg in speak(engine, items, top_k=args.top_k, min_tokens=n_codec, max_tokens=n_codec,
                             states_out=states, stream=stream, voc_stream=voc):
@@ -244,6 +256,73 @@ def run_sentence(engine, args, rec, hiddens, ids, n_codec, k=0, stream=None, voc
         if rec.first_pcm[i] is None:
             rec.first_pcm[i] = st.t_first_pcm
         rec.codec_tokens[i] += len(st.all_ids)
+
+
+class LaneTTS:
+    """The speech of every sentence on ONE continuously batched lane (fo.speak.SpeechLane) driven by a worker
+    thread beside the text decode: a sentence joins the lane's AR decode at its boundary, so sentences whose
+    speech overlaps share each decode step (one pass over the decoder's weights) instead of running two decode
+    loops side by side.  Each row keeps its own RNG stream, so the ids and PCM are those of SentenceTTS."""
+
+    def __init__(self, engine, args, rec):
+        import queue
+        import threading
+        from fo import ops
+        from fo.speak import SpeechLane
+        self.err = None
+        self.q = queue.Queue()
+        stream = ops.engine_stream(engine.device, name="tts")
+        voc = ops.engine_stream(engine.device, name="voc")
+        lane = SpeechLane(engine, top_k=args.top_k, stream=stream, voc_stream=voc)
+
+        def work():
+            import torch
+            torch.cuda.set_device(engine.device)
+            stop = False
+            try:
+                while True:
+                    while not stop:   # join every sentence that has arrived (wait for one when the lane is idle)
+                        try:
+                            job = self.q.get(block=lane.idle)
+                        except queue.Empty:
+                            break
+                        if job is None:
+                            stop = True
+                            break
+                        hiddens, ids, n_codec, k = job
+                        rec.sent_start[k] = time.perf_counter()
+                        with torch.cuda.stream(stream):
+                            items = sentence_items(engine, hiddens, ids)
+                        lane.add(items, n_codec, n_codec, tag=k)
+                    if lane.idle:
+                        if stop:
+                            return
+                        continue
+                    for i, seg in lane.pump():
+                        rec.segment(lane.states[i].key, seg)
+                    for k in lane.done_groups:
+                        rec.sent_end[k] = time.perf_counter()
+                        for st in (s for s in lane.states if s.tag == k):
+                            if rec.first_pcm[st.key] is None:
+                                rec.first_pcm[st.key] = st.t_first_pcm
+                            rec.codec_tokens[st.key] += len(st.all_ids)
+                    lane.done_groups.clear()
+            except BaseException as e:  # re-raised in the main thread by join()
+                self.err = e
+            finally:
+                lane.free()
+
+        self.t = threading.Thread(target=work, daemon=True)
+        self.t.start()
+
+    def submit(self, job):
+        self.q.put(job)
+
+    def join(self):
+        self.q.put(None)
+        self.t.join()
+        if self.err is not None:
+            raise self.err
 
 
 class SentenceTTS:

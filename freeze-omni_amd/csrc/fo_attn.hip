@@ -73,6 +73,7 @@ struct AttnArgs {
   // (arrival ticket cnt[item][kv head], reset by that split) merges the partials -- no combine launch
   int* cnt;        // nullable: static nsplit splits + k_attn_combine
   int kps;
+  int tnu;         // items NULL: tokens per item (item b = sequence b, tokens b*tnu .. b*tnu + tnu - 1)
 };
 
 constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
@@ -165,33 +166,47 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
 // while the current tile computes.  Every fp32 operand is split into bf16 hi + lo and each product
 // uses three MFMAs (hi*hi + hi*lo + lo*hi), so scores and outputs keep ~fp32 accuracy.  Online
 // softmax per row with the running max exchanged across the 4 waves through LDS.
-template <int HD>
-__global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
+template <int HD, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
+  constexpr int KT = 16 * NW;           // keys per tile: one 16-key column block per wave
+  constexpr int NTH = NW * 64;
   constexpr int DC = HD / 32;            // 32-wide d chunks (score k-steps)
   constexpr int NTILE = HD / 16;         // 16-wide d tiles of the output
-  constexpr int NTW = (NTILE + 3) / 4;   // output tiles per wave
+  constexpr int NTW = (NTILE + NW - 1) / NW;   // output tiles per wave
   constexpr int VP = HD + 2;             // V row pitch: the 4 key groups of a B fragment hit distinct banks
-  constexpr int VL = KT * HD / 4 / 256;  // float4 of V per thread per tile
+  constexpr int VL = KT * HD / 4 / NTH;  // float4 of V per thread per tile
   __shared__ float v_s[KT][VP];
   __shared__ float p_s[16][KT + 4];
-  __shared__ float mx_s[4][16];
-  __shared__ float l_s[4][16];
+  __shared__ float mx_s[NW][16];
+  __shared__ float l_s[NW][16];
   __shared__ int nvis_s[16];
   __shared__ int pg_s[MAXPG];
 
   const int it = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
-  const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it;  // NULL: one token each
-  const int tn = a.items ? a.items[3 * it + 2] : 1;
+  // items NULL: a uniform batch (tnu tokens per sequence, in sequence order) -- no item-table round trip
+  const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it * a.tnu;
+  const int tn = a.items ? a.items[3 * it + 2] : a.tnu;
   const int G = a.H / a.KVH;
   const int R = tn * G;  // <= 16
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = lane >> 4, col = lane & 15;
   const int* bt = a.block_table + (size_t)seq * a.maxb;
+  // this lane's q row slices, requested before anything that waits (they depend only on t0)
+  float4 qraw[2 * DC];
+  {
+    const int r = col < R ? col : R - 1;
+    const float* qr = a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + 8 * grp;
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+      qraw[2 * c] = *reinterpret_cast<const float4*>(qr + 32 * c);
+      qraw[2 * c + 1] = *reinterpret_cast<const float4*>(qr + 32 * c + 4);
+    }
+  }
   // a block-table row that fits is staged whole, requested together with the key counts (no wait for
   // this split's page range first); longer rows stage the split's pages once the range is known
   const bool whole = a.maxb <= MAXPG;
   if (whole)
-    for (int i = tid; i < a.maxb; i += 256) pg_s[i] = bt[i];
+    for (int i = tid; i < a.maxb; i += NTH) pg_s[i] = bt[i];
   int Lmax = 0;
   for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
   int ns = a.nsplit;
@@ -202,7 +217,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   const int per = ((Lmax + ns - 1) / ns + KT - 1) / KT * KT;
   const int c0 = sp * per, c1 = min(Lmax, c0 + per);
   if (c0 >= c1) {  // empty split: neutral partial
-    for (int r = tid; r < R; r += 256) {
+    for (int r = tid; r < R; r += NTH) {
       const size_t o = ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * a.nsplit + sp;
       a.part_ml[o * 2] = -INFINITY;
       a.part_ml[o * 2 + 1] = 0.f;
@@ -212,24 +227,22 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   }
   const int pb0 = c0 / a.PS, npg = (c1 - 1) / a.PS - pb0 + 1;
   if (npg > MAXPG || (whole && (c1 - 1) / a.PS >= a.maxb)) {  // host contract broken: poison, never read wrong keys
-    for (int r = tid; r < R; r += 256) a.out[((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD] = NAN;
+    for (int r = tid; r < R; r += NTH) a.out[((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD] = NAN;
     return;
   }
   const int pb = whole ? 0 : pb0;  // pg_s holds pages pb..
   if (!whole)
-    for (int i = tid; i < npg; i += 256) pg_s[i] = bt[pb + i];
+    for (int i = tid; i < npg; i += NTH) pg_s[i] = bt[pb + i];
   if (tid < 16) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
 
   // Q as A fragments: row = col (lane & 15), d = 32 c + 8 grp; rows >= R are zero
   bf16x8 qh[DC], ql[DC];
   {
-    const int r = col < R ? col : R - 1;
-    const float* qr = a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + 8 * grp;
 #pragma unroll
     for (int c = 0; c < DC; ++c) {
       float f[8];
-      const float4 x0 = *reinterpret_cast<const float4*>(qr + 32 * c);
-      const float4 x1 = *reinterpret_cast<const float4*>(qr + 32 * c + 4);
+      const float4 x0 = qraw[2 * c];
+      const float4 x1 = qraw[2 * c + 1];
       const float sc = col < R ? a.scale : 0.f;
       f[0] = x0.x * sc; f[1] = x0.y * sc; f[2] = x0.z * sc; f[3] = x0.w * sc;
       f[4] = x1.x * sc; f[5] = x1.y * sc; f[6] = x1.z * sc; f[7] = x1.w * sc;
@@ -252,7 +265,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
       kreg[2 * c + 1] = *reinterpret_cast<const float4*>(kr + 32 * c + 4);                                \
     }                                                                                                     \
     _Pragma("unroll") for (int i = 0; i < VL; ++i) {                                                      \
-      const int e = tid + 256 * i, j = e / (HD / 4), d4 = e % (HD / 4);                                   \
+      const int e = tid + NTH * i, j = e / (HD / 4), d4 = e % (HD / 4);                                   \
       const int pv = min((K0) + j, c1 - 1);                                                               \
       vreg[i] = *reinterpret_cast<const float4*>(a.vc + (size_t)pg_s[pv / a.PS - pb] * page_sz + head_off \
                                                  + (size_t)(pv % a.PS) * HD + d4 * 4);                    \
@@ -271,7 +284,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
     __syncthreads();  // the previous tile's p_s / v_s readers are done
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
-      const int e = tid + 256 * i, j = e / (HD / 4), d4 = e % (HD / 4);
+      const int e = tid + NTH * i, j = e / (HD / 4), d4 = e % (HD / 4);
       *reinterpret_cast<float2*>(&v_s[j][d4 * 4]) = make_float2(vreg[i].x, vreg[i].y);
       *reinterpret_cast<float2*>(&v_s[j][d4 * 4 + 2]) = make_float2(vreg[i].z, vreg[i].w);
     }
@@ -308,7 +321,9 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = 4 * grp + i;
-      const float tm = fmaxf(fmaxf(mx_s[0][r], mx_s[1][r]), fmaxf(mx_s[2][r], mx_s[3][r]));
+      float tm = mx_s[0][r];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) tm = fmaxf(tm, mx_s[w][r]);
       const float mn = fmaxf(m_run[i], tm);
       alpha[i] = (m_run[i] == mn) ? 1.f : expf(m_run[i] - mn);
       m_run[i] = mn;
@@ -334,7 +349,7 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
       }
 #pragma unroll
       for (int n = 0; n < NTW; ++n) {
-        const int dt = wave + 4 * n;
+        const int dt = wave + NW * n;
         if (dt < NTILE) {
           float f[8];
 #pragma unroll
@@ -362,11 +377,13 @@ __global__ __launch_bounds__(256) void k_attn_mfma(AttnArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * grp + i;
     if (r >= R) continue;
-    const float l = l_s[0][r] + l_s[1][r] + l_s[2][r] + l_s[3][r];
+    float l = l_s[0][r];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) l += l_s[w][r];
     const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
 #pragma unroll
     for (int n = 0; n < NTW; ++n) {
-      const int dt = wave + 4 * n;
+      const int dt = wave + NW * n;
       if (dt >= NTILE) continue;
       const int d = 16 * dt + col;
       if (ns == 1) {
@@ -687,6 +704,19 @@ __global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq,
   }
 }
 
+// waves per work group of the multi-row MFMA attention at head_dim 128 (the Qwen2 listen / text rows): 8 (default:
+// 128-key tiles, so a 128-key split loads in one round instead of two) or 4 (64-key tiles); FO_ATTN_NW.  r03t
+// (scripts/attn_kps_sweep.py, 8 sessions, graph-replayed): 2 tokens x 200 keys 18.0 -> 15.2 us, 400 keys 21.2 ->
+// 17.7 us, 1 token x 200 keys 15.9 -> 13.8 us (profiles/r03t_attn_nw_ab.txt)
+int g_attn_nw = -1;
+inline int attn_waves() {
+  if (g_attn_nw < 0) {
+    const char* e = getenv("FO_ATTN_NW");
+    g_attn_nw = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  return g_attn_nw;
+}
+
 inline int grid_for(long long n) {
   long long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -717,7 +747,8 @@ int fo_rope_kv_write(const float* qkv, int ldq, int T, int H, int KVH, int hd, c
   return fo::check_launch("fo_rope_kv_write");
 }
 
-// q [T][H*hd] -> out [T][H*hd].  items [n_items][3] (sequence, first token, tokens) with
+// q [T][H*hd] -> out [T][H*hd].  items [n_items][3] (sequence, first token, tokens), or NULL for a uniform batch
+// (item b = sequence b = tokens b*T/n_items .. (b+1)*T/n_items - 1), with
 // tokens * (H/KVH) <= max_rows <= 64; part_ml >= T*H*nsplit*2 and part_o >= T*H*nsplit*hd floats
 // when nsplit > 1.  tickets (nullable): n_items*KVH zero-initialised ints; then each item takes
 // min(nsplit, ceil(keys / keys_per_split)) splits and the last one merges them in this launch (the
@@ -727,13 +758,13 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
                  float scale, int nsplit, float* part_ml, float* part_o, float* out, int* tickets,
                  int keys_per_split, hipStream_t s) {
   FO_REQUIRE(T > 0 && n_items > 0 && KVH > 0 && H % KVH == 0, "fo_attention: bad shape");
-  FO_REQUIRE(items || n_items == T, "fo_attention: items NULL needs one token per item (n_items == T)");
+  FO_REQUIRE(items || T % n_items == 0, "fo_attention: items NULL needs T / n_items tokens per item");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
   FO_REQUIRE(max_rows >= 1 && max_rows <= 16, "fo_attention: %d query rows per item (max 16)", max_rows);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
-             tickets, keys_per_split};
+             tickets, keys_per_split, items ? 1 : T / n_items};
   if (max_rows == 1 && (long long)maxb * PS <= DEC_MAXK) {  // one query row per (session, head): decode kernel
     dim3 g1(n_items, H);
     if (hd == 128) hipLaunchKernelGGL((k_attn_decode<128>), g1, dim3(DEC_NT), 0, s, a);
@@ -742,7 +773,8 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
     return fo::check_launch("fo_attention/decode");
   }
   dim3 grid(n_items, KVH, nsplit);
-  if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
+  if (hd == 128 && attn_waves() == 8) hipLaunchKernelGGL((k_attn_mfma<128, 8>), grid, dim3(512), 0, s, a);
+  else if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
   else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_attn_mfma<32>), grid, dim3(256), 0, s, a);
   int rc = fo::check_launch("fo_attention/rows");

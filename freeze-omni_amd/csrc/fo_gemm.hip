@@ -756,7 +756,7 @@ void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, h
       return;
     }
   }
-  if constexpr (NT == 8) {  // 8 tiles x 16 waves exceeds the 128-VGPR budget of a 1024-thread group
+  if constexpr (NT >= 7) {  // 7-8 tiles x 16 waves exceed the 128-VGPR budget of a 1024-thread group
     if (nw == 16) nw = 8;
   } else if (nw == 16) {
     launch_gemm<NT, RB, 16, 4, SW>(wstream, x_f32, grid, a, s);
@@ -935,6 +935,29 @@ inline bool xs_mode() {
     g_xs = (e && e[0] == '0') ? 0 : 1;
   }
   return g_xs == 1;
+}
+// K split of the 8-tile long-K weight stream (Qwen2 down: 28 column groups x S workgroups); -1 = FO_DOWN_S
+// (4-16) decides at first use, default 8 (224 workgroups)
+int g_down_s = -1;
+inline int down_split() {
+  if (g_down_s < 0) {
+    const char* e = getenv("FO_DOWN_S");
+    const int v = e ? atoi(e) : 0;
+    g_down_s = (v >= 4 && v <= 16) ? v : 8;
+  }
+  return g_down_s;
+}
+// tiles per workgroup of that stream: 7 (default: 32 column groups x 8 = 256 workgroups, one per CU) or 8 (28
+// groups, 224 workgroups); FO_DOWN_NT.  r03s (one call): down alone 30.1 -> 29.8 us at 16 rows, the LLM stage
+// 3264 -> 3256 us, the bench 193.0 / 192.9x -> 194.3 / 195.2x; 8 x 9 (252 workgroups) and 7 x 9 (288) are slower
+// (31.3, 40.9 us; profiles/r03s_down_tiles_ab.txt)
+int g_down_nt = -1;
+inline int down_tiles() {
+  if (g_down_nt < 0) {
+    const char* e = getenv("FO_DOWN_NT");
+    g_down_nt = (e && atoi(e) == 8) ? 8 : 7;
+  }
+  return g_down_nt;
 }
 int g_num_cus = 0;
 inline int num_cus() {
@@ -1125,12 +1148,13 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     // tiles per workgroup; long-K layers (Qwen2 down) 4 tiles and a 4-way K split; mid-size grids
     // (> 256 tiles: Qwen2 qkv) 2 tiles; small ones 1
     if (a.ntiles >= 1024) NT = 4;
-    // Qwen2 down (592 k-steps, 224 tiles): 8 tiles x 8-way K split, pipelined (28 x 8 = 224 workgroups): the
+    // Qwen2 down (592 k-steps, 224 tiles): 7 tiles x 8-way K split, pipelined (32 x 8 = 256 workgroups; 8 tiles: 224): the
     // activation rows are read by a quarter as many column groups as with 4 tiles x 4 ways; 31.7 -> 29.7 us at 16
     // rows, 29.7 -> 28.7 us at 8, reduce launch included (profiles/r03g_down_sweep.txt)
     else if (KS >= 256 && a.ntiles >= 128) {
       NT = a.ntiles % 8 == 0 ? 8 : 4;
-      S_auto = NT == 8 ? 8 : 4;
+      if (down_tiles() == 7 && a.ntiles % 7 == 0) NT = 7;
+      S_auto = NT >= 7 ? down_split() : 4;
     }
     else if (KS >= 128 && a.ntiles <= 64) S_auto = 4;  // narrow long-K (TTS down): 10.9 -> 8.2 us in a graph
     else if (a.ntiles > 256) NT = 2;
@@ -1160,7 +1184,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       }
     }
     if (g_force_nt) NT = g_force_nt;
-    FO_REQUIRE(NT == 1 || NT == 2 || NT == 4 || NT == 8, "fo_gemm: tiles per workgroup %d", NT);
+    FO_REQUIRE(NT == 1 || NT == 2 || NT == 4 || NT == 8 || (NT == 7 && !swiglu), "fo_gemm: tiles per workgroup %d", NT);
     FO_REQUIRE(!swiglu || NT >= 2, "fo_gemm: swiglu needs tile pairs");
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   } else if (RB == 2) {
@@ -1244,6 +1268,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       else launch_nw<2, 1, true>(nw, wstream, x_f32, grid, a, stream);
     } else {
       if (NT == 8) launch_nw<8, 1, false>(nw, wstream, x_f32, grid, a, stream);
+      else if (NT == 7) launch_nw<7, 1, false>(nw, wstream, x_f32, grid, a, stream);
       else if (NT == 4) launch_nw<4, 1, false>(nw, wstream, x_f32, grid, a, stream);
       else if (NT == 2) launch_nw<2, 1, false>(nw, wstream, x_f32, grid, a, stream);
       else launch_nw<1, 1, false>(nw, wstream, x_f32, grid, a, stream);
@@ -1371,7 +1396,7 @@ int fo_gemm_set_u(int u) {
 
 int fo_gemm_tune(int nw, int nt) {
   FO_REQUIRE(nw == 0 || nw == 4 || nw == 8 || nw == 16, "fo_gemm_tune: nw must be 0/4/8/16");
-  FO_REQUIRE(nt == 0 || nt == 1 || nt == 2 || nt == 4 || nt == 8, "fo_gemm_tune: nt must be 0/1/2/4/8");
+  FO_REQUIRE(nt == 0 || nt == 1 || nt == 2 || nt == 4 || nt == 7 || nt == 8, "fo_gemm_tune: nt must be 0/1/2/4/7/8");
   g_force_nw = nw;
   g_force_nt = nt;
   return 0;

@@ -442,7 +442,7 @@ class ListenGraph:
         self.rows = torch.tensor([b * To + To - 1 for b in range(B)], dtype=I32).to(dev)
         self.meta = SimpleNamespace(T=n, S=B, tok_pos=m[0:n], tok_slot=m[n:2 * n], tok_nvis=m[2 * n:3 * n],
                                     block_table=m[3 * n:].view(B, self.maxb), items=items, n_items=B,
-                                    max_rows=To * G, max_keys=max_keys)
+                                    max_rows=To * G, max_keys=max_keys, uniform=True)
         self.slots = slots
         self.xs = [torch.empty(n, llm.D, dtype=F32, device=dev) for _ in range(slots)]
         self.x = self.xs[0]

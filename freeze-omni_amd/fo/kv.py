@@ -188,6 +188,9 @@ class BatchMeta:
             t += n
         self.n_items = len(items) // 3
         self.max_rows = max(items[2::3]) * gqa
+        # every sequence adds the same count of tokens, one work item each (item b = sequence b): fo_attention
+        # then takes no item table
+        self.uniform = self.n_items == len(entries) and len({n for _, n, _, _ in entries}) == 1
         host = np.concatenate([tok_seq, tok_pos, tok_slot, tok_nvis, np.asarray(last_rows, np.int32), bt.ravel(),
                                np.asarray(items, np.int32)])
         dev = torch.from_numpy(host).to(device, non_blocking=True)

@@ -408,9 +408,10 @@ def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc,
               part_ml, part_o, out, tickets=None, keys_per_split=ATTN_KEYS_PER_SPLIT):
     """tickets: zeroed int32 [>= n_items * KVH] -> splits sized from each item's key count (at most
     nsplit) merged inside the launch; None -> nsplit static splits + a combine launch.
-    items None: a decode batch, one token per sequence (item b = sequence b = token b)."""
-    if items is None and n_items != T:
-        raise ValueError("attention: items=None needs one token per sequence (n_items == T)")
+    items None: a uniform batch, T / n_items tokens per sequence in sequence order (item b = sequence b); a
+    decode batch is the one-token case."""
+    if items is None and T % n_items:
+        raise ValueError("attention: items=None needs T / n_items tokens per sequence")
     if tickets is not None and tickets.numel() < n_items * KVH:
         raise ValueError("attention tickets buffer smaller than n_items * KVH")
     _lib.call("fo_attention", q.data_ptr(), T, ptr(items), n_items, max_rows, tok_nvis.data_ptr(),

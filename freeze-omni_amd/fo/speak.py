@@ -256,3 +256,159 @@ def _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final):
             if seg is not None:
                 s.emitted.append(seg)
                 yield i, seg
+
+
+class SpeechLane:
+    """Continuous batching of the AR codec decode over groups of sessions that arrive over time (the sentences of
+    a response, each started at its boundary as bin/inference.py:160-183 does; a server's new speakers).
+
+    One captured decode step advances every live row of every group, so two sentences whose speech overlaps
+    stream the decoder's weights once per step instead of once per sentence (the step is latency-bound: 8 or 16
+    rows cost about the same).  A group joins between steps: the lane drains what it launched, runs the group's
+    prefill (pre_nn, prefix KV, bidirectional prefill: fo.tts.TTSEngine.start) on the lane's stream and continues
+    with a graph for the larger batch; rows leave the same way when they finish.  Each row keeps the RNG stream
+    it has in speak() (key = its index in its group, step = its own token count; the rows' steps differ inside a
+    launch), so a row's ids -- and its PCM -- are those of its group decoded alone (tests/test_speak_lane_gpu.py).
+
+    EOS masking (min_tokens) must cover a row's whole life (min_tokens == max_tokens, the benchmark policy) or none
+    of it (min_tokens == 0), and all groups of a lane agree: one launch draws every row from one bound."""
+
+    def __init__(self, engine, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
+                 seed=0, window=32, stream=None, voc_stream=None):
+        self.engine, self.top_k, self.seed, self.window = engine, top_k, seed, window
+        self.chunk, self.pad, self.N, self.thr = codec_chunk_size, codec_padding_size, N, seg_threshold
+        self.es = stream if stream is not None else ops.engine_stream(engine.device)
+        self.vs = voc_stream if voc_stream is not None else ops.engine_stream(engine.device, side=True)
+        self.states = []            # every row ever added; index = lane row id
+        self.groups = {}            # tag -> [row ids]
+        self.live = []              # rows decoding
+        self.pending = collections.deque()   # (batch rows, their steps, graph, event) launched, not yet read
+        self.slot = 0               # launches so far (host-buffer / event ring slot)
+        self.g = None               # decode graph of the current batch (None: rebuild before the next launch)
+        self.forced = None
+        self.res = torch.empty(2, dtype=F32, device=engine.device)
+        self.done_groups = []       # tags whose rows are all finished and vocoded (drained by the caller)
+        self._held = []             # segments produced outside pump() (add() drains the batch)
+
+    @property
+    def idle(self):
+        return not self.live and not self.pending and not self._held
+
+    def add(self, items, max_tokens, min_tokens=0, tag=None):
+        """Prefill a group of sessions (items as speak()) and let them join the decode at the next launch.
+        Returns the group's SpeakState objects (row order = items order)."""
+        if min_tokens not in (0, max_tokens):
+            raise ValueError("SpeechLane: EOS masking covers a row's whole life (min_tokens 0 or max_tokens)")
+        forced = bool(min_tokens)
+        if self.forced is not None and forced != self.forced and not self.idle:
+            raise ValueError("SpeechLane: every live group must mask EOS the same way")
+        self.forced = forced
+        # the batch changes: everything launched for the old one is read first (its PCM is handed out by pump())
+        self._held += self._drain()
+        with torch.cuda.stream(self.es):
+            seqs = self.engine.tts.start(items)
+        rows = []
+        for j, sq in enumerate(seqs):
+            st = SpeakState(sq, self.top_k, max_tokens, min_tokens)
+            st.key, st.tag, st.launched = j, tag, 0
+            rows.append(len(self.states))
+            self.states.append(st)
+        self.groups[tag] = rows
+        self.live += rows
+        self.g = None
+        return [self.states[i] for i in rows]
+
+    def pump(self):
+        """Launch ahead while the window has room, then read the oldest launched step back.  Returns the PCM
+        segments that became available: [(row id, pcm device 1-D)]."""
+        segs, self._held = self._held, []
+        with torch.cuda.stream(self.es):
+            while self.live and len(self.pending) < self.window:
+                if any(self.states[i].launched >= self.states[i].max_tokens for i in self.live):
+                    break   # a row is launched out: read what is in flight, it leaves the batch
+                if self.g is None:
+                    segs += self._rebuild()
+                    if not self.live:
+                        break
+                self._launch()
+            if self.pending:
+                finished = self._read(self.pending.popleft(), segs)
+                if finished:
+                    segs += self._drain()
+                    self.g = None
+            elif self.live:   # nothing in flight and nothing launchable: the launched-out rows are done
+                rest = [i for i in self.live if not self.states[i].done]
+                for i in rest:
+                    self.states[i].done = True
+                segs += self._finish(rest)
+                self.g = None
+        self._close_groups()
+        return segs
+
+    def free(self):
+        for s in self.states:
+            if s.seq is not None:
+                self.engine.tts.free([s.seq])
+                s.seq = None
+
+    # ---- internals
+    def _launch(self):
+        g, rows = self.g, self.live
+        steps = [self.states[i].launched for i in rows]
+        ev = g.launch([self.states[i].seq for i in rows], [self.states[i].key for i in rows], steps, self.slot)
+        for i in rows:
+            self.states[i].launched += 1
+        self.pending.append((list(rows), steps, g, ev))
+        self.slot += 1
+
+    def _read(self, entry, segs):
+        rows, steps, g, ev = entry
+        _lib.call("fo_event_sync", ev)
+        g.check()
+        h = g.hist.np
+        finished, due = [], []
+        eos = self.engine.tts.eos
+        for j, i in enumerate(rows):
+            if not self.states[i].done:
+                _after_token(self.states, i, int(h[steps[j], j]), eos, due, finished, self.chunk, self.pad)
+        segs += _emit(self.engine, self.states, due, finished, self.engine.codec.upsample, self.pad, self.N,
+                      self.thr, self.res, self.vs)
+        return finished
+
+    def _drain(self):
+        segs = []
+        while self.pending:
+            self._read(self.pending.popleft(), segs)
+        self.live = [i for i in self.live if not self.states[i].done]
+        return segs
+
+    def _finish(self, rows):
+        segs = _emit(self.engine, self.states, [], [i for i in rows if self.states[i].tokens],
+                     self.engine.codec.upsample, self.pad, self.N, self.thr, self.res, self.vs)
+        self.live = [i for i in self.live if not self.states[i].done]
+        return segs
+
+    def _rebuild(self):
+        segs = self._drain()
+        if not self.live:
+            return segs
+        tts, st = self.engine.tts, self.states
+        rows = self.live
+        max_keys = max(st[i].seq.kv.length + st[i].max_tokens - st[i].launched for i in rows) + 1
+        hist = max(st[i].max_tokens for i in rows) + 1
+        V = tts.vocab if self.forced else tts.vocab + 4
+        g = tts.decode_graph(len(rows), V, self.top_k, self.seed, max_keys, hist, None, True)
+        g.ids.copy_(torch.tensor([st[i].all_ids[-1] if st[i].all_ids else tts.sos for i in rows], dtype=I32)
+                    .to(self.engine.device))
+        g.prime()
+        self.g = g
+        return segs
+
+    def _close_groups(self):
+        for tag, rows in list(self.groups.items()):
+            if all(self.states[i].done for i in rows):
+                self.engine.tts.free([self.states[i].seq for i in rows])
+                for i in rows:
+                    self.states[i].seq = None
+                del self.groups[tag]
+                self.done_groups.append(tag)

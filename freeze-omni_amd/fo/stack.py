@@ -90,8 +90,9 @@ class DecoderStack:
         scale = hd ** -0.5
         sA, sB, xg = ws["sA"], ws["sB"], ws["xg"][:T]
         last = len(self.layers) - 1
-        # one token per sequence (decode): the attention needs no item table (fo_attention items NULL)
-        dense = ATTN_DENSE and meta.n_items == T == meta.S
+        # one token per sequence (decode) or the same count for every sequence, one work item each (a listen
+        # chunk): the attention needs no item table (fo_attention items NULL)
+        dense = ATTN_DENSE and (meta.n_items == T == meta.S or getattr(meta, "uniform", False))
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,

@@ -250,9 +250,12 @@ class DecodeGraph:
         self.ids.copy_(ids_dev[:self.B])
 
     def launch(self, seqs, keys, step, slot):
-        """Replay one step for seqs (len B, batch order) with RNG stream ids `keys` at step `step`,
-        history row `slot`; appends one KV position to every sequence.  Returns the step's event."""
+        """Replay one step for seqs (len B, batch order) with RNG stream ids `keys` at step `step` (an int, or
+        one step per row: a continuously batched lane whose rows joined at different times), history row
+        `slot` (with the device-advanced metadata each row's id lands in history row = its own step); appends
+        one KV position to every sequence.  Returns the step's event."""
         B, maxb, PS = self.B, self.maxb, self.tts.pool.PS
+        steps = tuple(int(v) for v in step) if isinstance(step, (list, tuple)) else (int(step),) * B
         for s in seqs:
             kv = s.kv
             L = kv.length
@@ -261,15 +264,15 @@ class DecodeGraph:
             kv.reserve(L + 1)
             if len(kv.pages) > maxb:
                 raise RuntimeError("decode graph block table too small")
-        if self.advance and slot != step:
+        if self.advance and not isinstance(step, (list, tuple)) and slot != step:
             raise ValueError("decode graph: the history row is the step when the step advances its own metadata")
         # the device-advanced block is current only for the same sequences, RNG keys and block lists (version:
         # any page added, copied on write or dropped) and lengths exactly one step on
         sig = (tuple(id(s) for s in seqs), tuple(int(k) for k in keys), tuple(s.kv.version for s in seqs))
         lens = tuple(s.kv.length for s in seqs)
         up = self._uploaded
-        if not (self.advance and up is not None and up[0] == sig and step == up[1] + 1 and slot == up[2] + 1
-                and lens == tuple(n + 1 for n in up[3])):
+        if not (self.advance and up is not None and up[0] == sig and steps == tuple(v + 1 for v in up[1])
+                and slot == up[2] + 1 and lens == tuple(n + 1 for n in up[3])):
             # the device-advanced block is not this step's: upload it from the host
             h = self.host_np[slot % self.RING]
             h[4 * B:5 * B] = keys
@@ -281,11 +284,11 @@ class DecodeGraph:
                 h[b] = L - s.P
                 h[B + b] = kv.slot(L)
                 h[2 * B + b] = L + 1
-                h[3 * B + b] = step
+                h[3 * B + b] = steps[b]
                 bt[b, :len(kv.pages)] = kv.pages
                 bt[b, len(kv.pages):] = kv.pages[-1]   # defensive: never a foreign page past the list
             self.meta_d.copy_(self.host[slot % self.RING], non_blocking=True)
-        self._uploaded = (sig, step, slot, lens)
+        self._uploaded = (sig, steps, slot, lens)
         for s in seqs:
             s.kv.length += 1
             s.generated += 1

@@ -41,10 +41,11 @@ for M in (16, 8):
     aerr = (outs[0] - ref).abs().max().item() / scale
     auto = min(timeit([lambda i=i: run(i) for i in range(2)]) for _ in range(2))
     res = []
-    for pipe in (0, 2):
-        for nw in (8, 16):
-            for nt in (4, 8):
-                for S in (4, 8, 16):
+    # DOWN_CFGS="pipe,nw,nt,S;...": only those configurations (default: the full grid)
+    cfgs = [tuple(int(v) for v in c.split(",")) for c in os.environ.get("DOWN_CFGS", "").split(";") if c] or \
+        [(p, w, t, s) for p in (0, 2) for w in (8, 16) for t in (4, 8) for s in (4, 8, 16)]
+    for pipe, nw, nt, S in cfgs:
+                if True:
                     lib.fo_gemm_set_pipe(pipe)
                     lib.fo_gemm_tune(nw, nt)
                     try:

@@ -1,0 +1,29 @@
+# Round-3 call t: the continuously batched speech lane (fo.speak.SpeechLane, bench --tts-lane) vs the two sentence
+# workers; the Qwen2 attention without the item table for uniform batches and with 8-wave / 128-key tiles
+# (FO_ATTN_NW=8); the 7-tile Qwen2 down as the default (full GPU tests).
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=r03t
+O=gpurun_out/${R}.txt
+: > $O
+timeout -k 10 200 python -u -m pytest tests/test_engines_gpu.py -x -v --timeout 120 --timeout-method thread -k "lane or two_workers" > gpurun_out/${R}_lane_test.log 2>&1 || { tail -40 gpurun_out/${R}_lane_test.log; exit 1; }
+tail -1 gpurun_out/${R}_lane_test.log >> $O
+timeout -k 10 200 python -u scripts/gemm_small_sweep.py 2>&1 | grep -v amdgpu.ids >> $O || exit 1
+for E in "ATTN_UNIFORM=0 FO_ATTN_NW=4" "ATTN_UNIFORM=1 FO_ATTN_NW=4" "ATTN_UNIFORM=1 FO_ATTN_NW=8"; do
+  echo "== $E attention" >> $O
+  env $E ATTN_KPS=128,256 timeout -k 10 120 python -u scripts/attn_kps_sweep.py 2>&1 | grep -v amdgpu.ids >> $O || exit 1
+done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${R}_pytest_gpu.log 2>&1 || { tail -30 gpurun_out/${R}_pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/${R}_pytest_gpu.log >> $O
+for i in 1 2; do
+  for A in "" "--tts-lane" "--tts-lane FO_ATTN_NW=8"; do
+    echo -n "$i [$A] " >> $O
+    EV=$(echo "$A" | tr ' ' '\n' | grep = | tr '\n' ' '); ARGS=$(echo "$A" | tr ' ' '\n' | grep -v = | tr '\n' ' ')
+    env $EV timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 $ARGS > gpurun_out/${R}_b.log 2>&1 || { tail -30 gpurun_out/${R}_b.log; exit 1; }
+    grep '^{' gpurun_out/${R}_b.log | python -c "
+import json,sys
+d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['p50_first_audio_ms'], {k: round(v,1) for k, v in d['stage_ms'].items() if k.startswith(('listen','text','speak','sentence'))})" >> $O
+  done
+done
+cat $O

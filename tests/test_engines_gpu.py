@@ -372,9 +372,15 @@ def test_speak_two_workers_side_by_side_match_sequential(dev, speech_engine):
     kw = dict(top_k=4, min_tokens=50, max_tokens=50, seed=5)
 
     def run(items, stream=None, voc=None):
+        import contextlib
         states = []
-        segs = [(i, s.cpu().numpy()) for i, s in speak(speech_engine, items, states_out=states, stream=stream,
-                                                        voc_stream=voc, **kw)]
+        segs = []
+        for i, s in speak(speech_engine, items, states_out=states, stream=stream, voc_stream=voc, **kw):
+            # the read-back goes on the worker's vocoder stream (which produced the PCM): on the legacy stream it
+            # would wait on every blocking stream, including one the other worker is capturing a graph on
+            # (hipErrorStreamCaptureImplicit)
+            with (torch.cuda.stream(voc) if voc is not None else contextlib.nullcontext()):
+                segs.append((i, s.cpu().numpy()))
         return [s.all_ids for s in states], segs
 
     ref = [run(j) for j in jobs]
@@ -399,3 +405,51 @@ def test_speak_two_workers_side_by_side_match_sequential(dev, speech_engine):
         assert [i for i, _ in segs_g] == [i for i, _ in segs_r]
         for (_, a), (_, b) in zip(segs_g, segs_r):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("top_k,forced,joins", [(4, True, (0, 17)), (1, False, (0, 9)), (4, True, (0, 0, 33))])
+def test_speech_lane_matches_groups_spoken_alone(dev, speech_engine, top_k, forced, joins):
+    """fo.speak.SpeechLane (the bench's --tts-lane): groups that join the continuously batched AR decode after
+    different numbers of decode reads, with different max_tokens, give every row exactly the ids and the PCM
+    segments of its group spoken alone through speak() -- each row keeps its own RNG stream (key, own step)."""
+    from fo import ops
+    from fo.speak import SpeechLane
+    jobs = [(_items(dev, 3, 21 + g), 40 + 7 * g) for g in range(len(joins))]
+
+    def alone(items, n):
+        kw = dict(top_k=top_k, max_tokens=n, min_tokens=n if forced else 0, seed=5)
+        states = []
+        segs = {}
+        from fo.speak import speak
+        for i, s in speak(speech_engine, items, states_out=states, **kw):
+            segs.setdefault(i, []).append(s.cpu().numpy())
+        return [s.all_ids for s in states], segs
+
+    ref = [alone(items, n) for items, n in jobs]
+    lane = SpeechLane(speech_engine, top_k=top_k, seed=5, stream=ops.engine_stream(dev, name="tts"),
+                      voc_stream=ops.engine_stream(dev, name="voc"))
+    segs = {}
+    added, reads = 0, 0
+    while added < len(jobs) or not lane.idle:
+        while added < len(jobs) and reads >= joins[added]:
+            items, n = jobs[added]
+            lane.add(items, n, n if forced else 0, tag=added)
+            added += 1
+        if lane.idle:   # nothing to decode until the next group joins
+            reads = joins[added]
+            continue
+        for i, s in lane.pump():
+            st = lane.states[i]
+            segs.setdefault((st.tag, st.key), []).append(s.cpu().numpy())
+        reads += 1
+        assert reads < 10000
+    assert sorted(lane.done_groups) == list(range(len(jobs)))
+    for g, (ids_r, segs_r) in enumerate(ref):
+        got = [s.all_ids for s in lane.states if s.tag == g]
+        assert got == ids_r, g
+        for b in range(len(ids_r)):
+            a, r = segs.get((g, b), []), segs_r.get(b, [])
+            assert len(a) == len(r), (g, b)
+            for x, y in zip(a, r):
+                np.testing.assert_array_equal(x, y)
+    lane.free()
