@@ -79,6 +79,9 @@ def parse():
                     help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N "
                          "(2: a sentence's speech never queues behind the previous one's; r03p A/B 1 / 2 / 4 "
                          "workers: 193.5x / 194.8-195.4x / 173.2x)")
+    ap.add_argument("--text-ahead", action="store_true",
+                    help="queue each text step before the previous one is read back (TextGraph.launch with the "
+                         "ids left on the device; a step queued on an EOS draw is rolled back and relaunched)")
     ap.add_argument("--tts-lane", action="store_true",
                     help="one continuously batched speech lane (fo.speak.SpeechLane) instead of per-sentence workers: "
                          "sentences whose speech overlaps decode in the same AR step")
@@ -166,6 +169,9 @@ def run_turn(engine, base_kv, pcms, args, sync):
     text_ids = [[] for _ in turns]
     hiddens = []
     nxt, hid = engine.text_step([(t.kv, pre) for t in turns])
+    kvs = [t.kv for t in turns]
+    tg = engine.text_graph(kvs, T) if args.text_ahead else None
+    pend = None
     s0 = 0
     for j in range(T):
         hiddens.append(hid)
@@ -184,7 +190,21 @@ def run_turn(engine, base_kv, pcms, args, sync):
             s0 = j + 1
         if j == T - 1:
             break
-        nxt, hid = engine.text_step([(t.kv, [text_ids[b][-1]]) for b, t in enumerate(turns)])
+        if tg is None:
+            nxt, hid = engine.text_step([(t.kv, [text_ids[b][-1]]) for b, t in enumerate(turns)])
+            continue
+        # token j + 1: its step was queued behind step j on step j's draws (still on the device); an EOS draw
+        # is fed back as id 0 by this benchmark policy, so such a step is rolled back and relaunched
+        if pend is None:
+            pend = tg.launch(kvs, [text_ids[b][-1] for b in range(B)])
+        elif eod in nxt:
+            tg.read(pend)
+            for kv in kvs:
+                kv.length -= 1
+            pend = tg.launch(kvs, [text_ids[b][-1] for b in range(B)])
+        cur = pend
+        pend = tg.launch(kvs) if j + 2 <= T - 1 else None
+        nxt, hid = tg.read(cur)
     t_text = time.perf_counter()   # the last text step's ids were read back: the text stage is done
     if tts is not None:
         tts.join()
@@ -273,7 +293,8 @@ class LaneTTS:
         self.q = queue.Queue()
         stream = ops.engine_stream(engine.device, name="tts")
         voc = ops.engine_stream(engine.device, name="voc")
-        lane = SpeechLane(engine, top_k=args.top_k, stream=stream, voc_stream=voc)
+        pre = ops.engine_stream(engine.device, name="tts1")   # the sentences' prefills, beside the lane's steps
+        lane = SpeechLane(engine, top_k=args.top_k, stream=stream, voc_stream=voc, prefill_stream=pre)
 
         def work():
             import torch
@@ -291,7 +312,7 @@ class LaneTTS:
                             break
                         hiddens, ids, n_codec, k = job
                         rec.sent_start[k] = time.perf_counter()
-                        with torch.cuda.stream(stream):
+                        with torch.cuda.stream(pre):   # read by the prefill, on the same stream
                             items = sentence_items(engine, hiddens, ids)
                         lane.add(items, n_codec, n_codec, tag=k)
                     if lane.idle:

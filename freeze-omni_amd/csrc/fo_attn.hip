@@ -253,9 +253,9 @@ __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
 
   const size_t head_off = (size_t)kvh * a.PS * HD;
   const size_t page_sz = (size_t)a.KVH * a.PS * HD;
-  float4 kreg[2 * DC], vreg[VL];
+  float4 kA[2 * DC], vA[VL], kB[2 * DC], vB[VL];   // two tiles' K / V in flight (ping-pong)
   // K: this lane's key (16 per wave) x its 8-wide d slices; V: cooperative 16-B rows for LDS
-#define FO_ATTN_LOAD(K0)                                                                                  \
+#define FO_ATTN_LOAD(kreg, vreg, K0)                                                                      \
   {                                                                                                       \
     const int pk = min((K0) + 16 * wave + col, c1 - 1);                                                   \
     const float* kr = a.kc + (size_t)pg_s[pk / a.PS - pb] * page_sz + head_off + (size_t)(pk % a.PS) * HD \
@@ -279,8 +279,11 @@ __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
 #pragma unroll
   for (int n = 0; n < NTW; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  FO_ATTN_LOAD(c0)
-  for (int k0 = c0; k0 < c1; k0 += KT) {
+  // tile t's loads are issued while tile t - 1 computes and two tiles are in flight from the start, so a
+  // 256-key split waits for one round of memory, not two
+  FO_ATTN_LOAD(kA, vA, c0)
+  if (c0 + KT < c1) FO_ATTN_LOAD(kB, vB, c0 + KT)
+  auto tile = [&](float4 (&kreg)[2 * DC], float4 (&vreg)[VL], const int k0) {
     __syncthreads();  // the previous tile's p_s / v_s readers are done
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
                           kreg[2 * c + 1].x, kreg[2 * c + 1].y, kreg[2 * c + 1].z, kreg[2 * c + 1].w};
       split8(f, kh[c], kl[c]);
     }
-    if (k0 + KT < c1) FO_ATTN_LOAD(k0 + KT)
+    if (k0 + 2 * KT < c1) FO_ATTN_LOAD(kreg, vreg, k0 + 2 * KT)
     // S[r = 4 grp + i][key = k0 + 16 wave + col]
     f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -362,6 +365,10 @@ __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
         }
       }
     }
+  };
+  for (int k0 = c0; k0 < c1; k0 += 2 * KT) {
+    tile(kA, vA, k0);
+    if (k0 + KT < c1) tile(kB, vB, k0 + KT);
   }
 #undef FO_ATTN_LOAD
   // row sums: 16 lanes of the row group, then the 4 waves
@@ -712,7 +719,7 @@ int g_attn_nw = -1;
 inline int attn_waves() {
   if (g_attn_nw < 0) {
     const char* e = getenv("FO_ATTN_NW");
-    g_attn_nw = (e && atoi(e) == 4) ? 4 : 8;
+    g_attn_nw = (e && atoi(e) == 4) ? 4 : 8;   // (16 waves: 128 VGPRs a lane, 109 spilled -- not built)
   }
   return g_attn_nw;
 }

@@ -138,10 +138,24 @@ __global__ void k_scale_add_channel(float* y, int B, int C, int T, float s, cons
 
 // find_min_sum_index: window sums of |x| over N samples starting at mid - N/2; argmin (first);
 // then argmin |x| inside [s0, min(L, m + N + s0)).  res[0] = min window sum, res[1] = cut index.
-__global__ __launch_bounds__(1024) void k_silence_cut(const float* x, int L, int N, float* res) {
+// One work group per row (blockIdx.x: row x + blockIdx.x * ld, result res + 2 * blockIdx.x): the rows of a
+// vocoder call in one launch.  A row that fits (STAGE: L <= dynamic LDS floats) is staged into LDS once, so
+// the window sums' partial-chunk loops read LDS instead of issuing dependent global loads; the arithmetic
+// (double prefix sums, P(b) - P(a)) is the same either way, so the result is too.
+template <bool STAGE>
+__global__ __launch_bounds__(1024) void k_silence_cut(const float* xg, long long ld, int L, int N, float* res) {
+  extern __shared__ float xs_dyn[];
   __shared__ double cs[1025];
   __shared__ float bv[1024];
   __shared__ int bi[1024];
+  xg += (size_t)blockIdx.x * ld;
+  res += 2 * blockIdx.x;
+  const float* x = xg;
+  if constexpr (STAGE) {
+    for (int i = threadIdx.x; i < L; i += 1024) xs_dyn[i] = xg[i];
+    __syncthreads();
+    x = xs_dyn;
+  }
   const int mid = L / 2, start = mid - N / 2;
   const int nw = L - N + 1 - start;  // window count from `start`
   // prefix sums of |x| in double, 1024 threads over chunks
@@ -221,6 +235,8 @@ __global__ __launch_bounds__(1024) void k_silence_cut(const float* x, int L, int
     res[1] = (float)bi[0];
   }
 }
+constexpr int SC_STATIC_LDS = 1025 * 8 + 1024 * 4 * 2;
+constexpr int SC_MAX_STAGE = (160 * 1024 - SC_STATIC_LDS) / 4;  // floats of a row staged in LDS
 
 inline int grid_for(long long n) {
   long long g = (n + 255) / 256;
@@ -270,10 +286,18 @@ int fo_scale_add_channel(float* y, int B, int C, int T, float sc, const float* g
   return fo::check_launch("fo_scale_add_channel");
 }
 
-int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s) {
-  FO_REQUIRE(L >= N && L / 2 - N / 2 >= 0, "fo_silence_cut: L=%d < N=%d", L, N);
-  hipLaunchKernelGGL(k_silence_cut, dim3(1), dim3(1024), 0, s, x, L, N, res);
+int fo_silence_cut_rows(const float* x, long long ld, int rows, int L, int N, float* res, hipStream_t s) {
+  FO_REQUIRE(rows >= 1 && L >= N && L / 2 - N / 2 >= 0 && (rows == 1 || ld >= L),
+             "fo_silence_cut_rows: rows=%d L=%d N=%d ld=%lld", rows, L, N, ld);
+  if (L <= SC_MAX_STAGE)
+    hipLaunchKernelGGL((k_silence_cut<true>), dim3(rows), dim3(1024), (size_t)L * sizeof(float), s, x, ld, L, N, res);
+  else
+    hipLaunchKernelGGL((k_silence_cut<false>), dim3(rows), dim3(1024), 0, s, x, ld, L, N, res);
   return fo::check_launch("fo_silence_cut");
+}
+
+int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s) {
+  return fo_silence_cut_rows(x, 0, 1, L, N, res, s);
 }
 
 }  // extern "C"

@@ -121,6 +121,7 @@ _SIGS = {
     "fo_scale_add_cl": (c_int, [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_conv_post_cl": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_float, c_vp, c_vp]),
     "fo_silence_cut": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "fo_silence_cut_rows": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp]),
     "fo_sample_ws_floats": (c_ll, [c_int, c_int]),
     "fo_sample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, ctypes.c_ulonglong, c_vp, c_vp, c_int, c_vp,
                           c_vp, c_vp, c_vp, c_ll, c_vp]),

@@ -358,6 +358,13 @@ class FreezeOmniEngine:
         return ids, hid
 
 
+    def text_graph(self, kvs, n_tokens, top_k=1, top_p=0.0, temperature=1.0, seed=0):
+        """The captured one-token text step for the sessions kvs, sized for n_tokens more tokens: launch() /
+        read() queue a step before the previous one is read back (its ids stay on the device)."""
+        with torch.cuda.stream(ops.engine_stream(self.device)):
+            return self._text_graph_for([(kv, [0]) for kv in kvs], top_k, top_p, temperature, seed,
+                                        extra=n_tokens + 64)
+
     def _text_graph_for(self, items, top_k, top_p, temperature, seed, extra=64):
         B = len(items)
         need = max(kv.length for kv, _ in items) + extra
@@ -619,16 +626,22 @@ class TextGraph:
         self.par = torch.tensor([top_k] * B, dtype=I32).to(dev)
         self.tp = torch.tensor([temperature] * B + [top_p] * B, dtype=F32).to(dev)
         self.out = torch.empty(B, dtype=I32, device=dev)
-        self.out_host = torch.empty(B, dtype=I32).pin_memory()
+        # steps in flight (launch() / read()): each has its own pinned id read-back and event
+        self.out_host = [torch.empty(B, dtype=I32).pin_memory() for _ in range(self.DEPTH)]
+        self.evs = [ListenGraph._event() for _ in range(self.DEPTH)]
+        self.n_launched = 0
         self.top_k = top_k
         self.err = ops.SampleCheck()
         self.main = ops.engine_stream(dev)
         self.exec = ListenGraph._capture(self.main, self._body)
-        self.ev = ListenGraph._event()
+
+    DEPTH = 4
 
     def _body(self):
+        # the step's input ids are read from `out`: the previous step's draw (a step queued behind it, launch()
+        # without ids), or the host's ids copied there first; the draw then overwrites them
         llm, B = self.eng.llm, self.B
-        ops.gather_rows(llm.embed_tokens, self.ids, out=self.x, round_fp16=True)
+        ops.gather_rows(llm.embed_tokens, self.out, out=self.x, round_fp16=True)
         llm.stack.forward(self.x, self.meta, self.ws)
         ops.rmsnorm(self.x, llm.norm, llm.eps, out=self.x)
         llm.lm_head(self.x, out=self.logits)
@@ -637,15 +650,26 @@ class TextGraph:
 
     def run(self, items):
         """items: list of (kv, [token id]) in batch order; appends one KV position per session."""
+        return self.read(self.launch([kv for kv, _ in items], [toks[0] for _, toks in items]))
+
+    def launch(self, kvs, ids=None):
+        """Queue one step for the sessions kvs (batch order) and return its handle for read().  ids: the input
+        token per session from the host; None: the ids the previous launched step draws (still on the device),
+        so the step can be queued before that one is read back.  Appends one KV position per session."""
         B, maxb = self.B, self.maxb
+        if self.n_launched - getattr(self, "n_read", 0) >= self.DEPTH:
+            raise RuntimeError("text graph: more than DEPTH steps in flight")
+        if ids is None and self.n_launched == 0:
+            raise ValueError("text graph: the first step needs its input ids")
         j, h = self.ring.next()
         bt = h[5 * B:].reshape(B, maxb)
-        for b, (kv, toks) in enumerate(items):
+        for b, kv in enumerate(kvs):
             L = kv.length
             kv.reserve(L + 1)
             if len(kv.pages) > maxb:
                 raise RuntimeError("text graph block table too small")
-            h[b] = toks[0]
+            if ids is not None:
+                h[b] = ids[b]
             h[B + b] = L
             h[2 * B + b] = kv.slot(L)
             h[3 * B + b] = L + 1
@@ -654,19 +678,30 @@ class TextGraph:
             kv.length = L + 1
         st = self.main
         self.ring.upload(j, self.meta_d, st)
-        _lib.call("fo_graph_launch", self.exec, st.cuda_stream)
+        k = self.n_launched % self.DEPTH
         with torch.cuda.stream(st):
-            self.out_host.copy_(self.out, non_blocking=True)
+            if ids is not None:
+                self.out.copy_(self.ids)
+            _lib.call("fo_graph_launch", self.exec, st.cuda_stream)
+            self.out_host[k].copy_(self.out, non_blocking=True)
             hid = self.x.clone()
-        _lib.call("fo_event_record", self.ev, st.cuda_stream)
-        _lib.call("fo_event_sync", self.ev)
+        _lib.call("fo_event_record", self.evs[k], st.cuda_stream)
+        self.n_launched += 1
+        return (k, hid)
+
+    def read(self, handle):
+        """Wait for a launched step; returns (drawn ids list, last hidden rows [B, D] device)."""
+        k, hid = handle
+        _lib.call("fo_event_sync", self.evs[k])
+        self.n_read = getattr(self, "n_read", 0) + 1
         self.err.check("text decode step")
-        return self.out_host.tolist(), hid
+        return self.out_host[k].tolist(), hid
 
     def destroy(self):
         if self.exec is not None:
             _lib.call("fo_graph_destroy", self.exec)
-            _lib.call("fo_event_destroy", self.ev)
+            for e in self.evs:
+                _lib.call("fo_event_destroy", e)
             self.ring.destroy()
             self.err.free()
             self.exec = None

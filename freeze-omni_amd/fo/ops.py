@@ -401,7 +401,7 @@ def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS
 
 # keys per split of the decode attention: r03c's sweep (scripts/attn_kps_sweep.py, Qwen2 28/4 heads, 8 sessions
 # x 1-2 new tokens) puts 128 first or tied at every context from 100 to 800 keys (800 keys: 21.7 us vs 24.2 at 256)
-ATTN_KEYS_PER_SPLIT = 128
+ATTN_KEYS_PER_SPLIT = int(os.environ.get("FO_ATTN_KPS", "128"))
 
 
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,
@@ -571,6 +571,14 @@ def scale_add_channel_(y, B, C, T, s, g=None):
 
 def silence_cut(x, N, res):
     _lib.call("fo_silence_cut", x.data_ptr(), x.numel(), N, res.data_ptr(), stream(x.device))
+    return res
+
+
+def silence_cut_rows(x, N, res):
+    """find_min_sum_index's window search for every row of x [rows, L] (row stride x.stride(0)) in one launch;
+    res [rows, 2] fp32 (min window sum, cut index)."""
+    _lib.call("fo_silence_cut_rows", x.data_ptr(), x.stride(0), x.shape[0], x.shape[1], N, res.data_ptr(),
+              stream(x.device))
     return res
 
 

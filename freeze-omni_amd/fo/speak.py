@@ -228,11 +228,16 @@ def _vocode_on_stream(engine, states, idx, up, pad, N, thr, res, final):
         ids = torch.tensor([states[i].tokens for i in members], dtype=I32).to(engine.device)
         pcm = engine.codec(ids)
         cuts = None
-        if not final:   # every member's window search in one go, one read-back for the call
+        if not final:   # every member's window search in one launch, one read-back for the call
             resb = torch.empty(len(members), 2, dtype=F32, device=engine.device)
-            for j, i in enumerate(members):
-                s = states[i]
-                ops.silence_cut(pcm[j][s.left * up: pcm.shape[1] - pad * up], N, resb[j])
+            lefts = {states[i].left for i in members}
+            if len(lefts) == 1:   # (equal token counts: always one left context)
+                left = lefts.pop()
+                ops.silence_cut_rows(pcm[:len(members), left * up: pcm.shape[1] - pad * up], N, resb)
+            else:
+                for j, i in enumerate(members):
+                    s = states[i]
+                    ops.silence_cut(pcm[j][s.left * up: pcm.shape[1] - pad * up], N, resb[j])
             cuts = resb.cpu()
         for j, i in enumerate(members):
             s = states[i]
@@ -264,49 +269,57 @@ class SpeechLane:
 
     One captured decode step advances every live row of every group, so two sentences whose speech overlaps
     stream the decoder's weights once per step instead of once per sentence (the step is latency-bound: 8 or 16
-    rows cost about the same).  A group joins between steps: the lane drains what it launched, runs the group's
-    prefill (pre_nn, prefix KV, bidirectional prefill: fo.tts.TTSEngine.start) on the lane's stream and continues
-    with a graph for the larger batch; rows leave the same way when they finish.  Each row keeps the RNG stream
-    it has in speak() (key = its index in its group, step = its own token count; the rows' steps differ inside a
-    launch), so a row's ids -- and its PCM -- are those of its group decoded alone (tests/test_speak_lane_gpu.py).
+    rows cost about the same).  A group's prefill (pre_nn, prefix KV, bidirectional prefill: TTSEngine.start)
+    runs on its own stream beside the lane's decode steps; once it is done the group joins between two steps
+    without a host round trip: the rows already decoding carry their next-step ids and input rows over from
+    the old graph's buffers to the larger one's on the device, in stream order, and the new rows start from
+    SOS.  While a group is joining the lane launches only a few steps ahead, so the join is not queued behind a
+    long launch window.  Rows leave when they finish (the lane drains what it launched for them, then
+    continues with a graph for the survivors).  Each row keeps the RNG stream it has in speak() (key = its
+    index in its group, step = its own token count; the rows' steps differ inside a launch), so a row's ids --
+    and its PCM -- are those of its group decoded alone (tests/test_engines_gpu.py::test_speech_lane_*).
 
     EOS masking (min_tokens) must cover a row's whole life (min_tokens == max_tokens, the benchmark policy) or none
     of it (min_tokens == 0), and all groups of a lane agree: one launch draws every row from one bound."""
 
+    JOIN_WINDOW = 4
+
     def __init__(self, engine, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
-                 seed=0, window=32, stream=None, voc_stream=None):
+                 seed=0, window=32, stream=None, voc_stream=None, prefill_stream=None):
         self.engine, self.top_k, self.seed, self.window = engine, top_k, seed, window
         self.chunk, self.pad, self.N, self.thr = codec_chunk_size, codec_padding_size, N, seg_threshold
         self.es = stream if stream is not None else ops.engine_stream(engine.device)
         self.vs = voc_stream if voc_stream is not None else ops.engine_stream(engine.device, side=True)
+        self.ps = prefill_stream if prefill_stream is not None else self.es
         self.states = []            # every row ever added; index = lane row id
         self.groups = {}            # tag -> [row ids]
-        self.live = []              # rows decoding
+        self.live = []              # rows decoding, in the current graph's batch order
+        self.joining = []           # (row ids, prefill-done event) of groups not decoding yet
         self.pending = collections.deque()   # (batch rows, their steps, graph, event) launched, not yet read
         self.slot = 0               # launches so far (host-buffer / event ring slot)
         self.g = None               # decode graph of the current batch (None: rebuild before the next launch)
         self.forced = None
         self.res = torch.empty(2, dtype=F32, device=engine.device)
         self.done_groups = []       # tags whose rows are all finished and vocoded (drained by the caller)
-        self._held = []             # segments produced outside pump() (add() drains the batch)
+        self._held = []             # segments produced outside pump()
 
     @property
     def idle(self):
-        return not self.live and not self.pending and not self._held
+        return not self.live and not self.pending and not self.joining and not self._held
 
     def add(self, items, max_tokens, min_tokens=0, tag=None):
-        """Prefill a group of sessions (items as speak()) and let them join the decode at the next launch.
-        Returns the group's SpeakState objects (row order = items order)."""
+        """Prefill a group of sessions (items as speak()) on the prefill stream; the group joins the decode once
+        that is done.  Returns the group's SpeakState objects (row order = items order)."""
         if min_tokens not in (0, max_tokens):
             raise ValueError("SpeechLane: EOS masking covers a row's whole life (min_tokens 0 or max_tokens)")
         forced = bool(min_tokens)
         if self.forced is not None and forced != self.forced and not self.idle:
             raise ValueError("SpeechLane: every live group must mask EOS the same way")
         self.forced = forced
-        # the batch changes: everything launched for the old one is read first (its PCM is handed out by pump())
-        self._held += self._drain()
-        with torch.cuda.stream(self.es):
+        with torch.cuda.stream(self.ps):
             seqs = self.engine.tts.start(items)
+            ev = torch.cuda.Event()
+            ev.record()
         rows = []
         for j, sq in enumerate(seqs):
             st = SpeakState(sq, self.top_k, max_tokens, min_tokens)
@@ -314,18 +327,26 @@ class SpeechLane:
             rows.append(len(self.states))
             self.states.append(st)
         self.groups[tag] = rows
-        self.live += rows
-        self.g = None
+        self.joining.append((rows, ev))
         return [self.states[i] for i in rows]
 
     def pump(self):
-        """Launch ahead while the window has room, then read the oldest launched step back.  Returns the PCM
-        segments that became available: [(row id, pcm device 1-D)]."""
+        """Join the groups whose prefill is done, launch ahead while the window has room, then read the oldest
+        launched step back.  Returns the PCM segments that became available: [(row id, pcm device 1-D)]."""
         segs, self._held = self._held, []
         with torch.cuda.stream(self.es):
-            while self.live and len(self.pending) < self.window:
+            if self.joining:
+                ready = [j for j in self.joining if j[1].query()]
+                if not ready and not self.live and not self.pending:
+                    ready = self.joining[:1]   # nothing else to do: wait for the first group's prefill on the device
+                if ready:
+                    self._join(ready)
+            window = self.JOIN_WINDOW if self.joining else self.window
+            while self.live and len(self.pending) < window:
                 if any(self.states[i].launched >= self.states[i].max_tokens for i in self.live):
-                    break   # a row is launched out: read what is in flight, it leaves the batch
+                    segs += self._shrink()   # launched-out rows leave; the rest go on without a host round trip
+                    if not self.live:
+                        break
                 if self.g is None:
                     segs += self._rebuild()
                     if not self.live:
@@ -333,10 +354,10 @@ class SpeechLane:
                 self._launch()
             if self.pending:
                 finished = self._read(self.pending.popleft(), segs)
-                if finished:
+                if any(i in self.live for i in finished):   # an EOS inside the batch: drain, rebuild from the host
                     segs += self._drain()
                     self.g = None
-            elif self.live:   # nothing in flight and nothing launchable: the launched-out rows are done
+            elif self.live and self.g is not None:   # nothing launchable: the launched-out rows are done
                 rest = [i for i in self.live if not self.states[i].done]
                 for i in rest:
                     self.states[i].done = True
@@ -352,6 +373,43 @@ class SpeechLane:
                 s.seq = None
 
     # ---- internals
+    def _graph(self, rows):
+        """The decode graph for batch `rows`.  Graphs are cached by batch size; one that launched steps still
+        unread is drained first (its id history would be overwritten; a regrown cache entry is destroyed)."""
+        if any(e[2].B == len(rows) for e in self.pending):
+            self._held += self._drain_keep()
+        tts, st = self.engine.tts, self.states
+        max_keys = max(st[i].seq.kv.length + st[i].max_tokens - st[i].launched for i in rows) + 1
+        hist = max(st[i].max_tokens for i in rows) + 1
+        V = tts.vocab if self.forced else tts.vocab + 4
+        return tts.decode_graph(len(rows), V, self.top_k, self.seed, max_keys, hist, None, True)
+
+    def _join(self, ready):
+        """The ready groups join the batch between two steps (on the lane stream, after their prefill)."""
+        tts = self.engine.tts
+        new = []
+        for rows, ev in ready:
+            torch.cuda.current_stream().wait_event(ev)
+            new += rows
+        self.joining = [j for j in self.joining if all(j is not r for r in ready)]
+        if self.g is None or not self.live:
+            self.live += new   # no device state to carry over: the next launch rebuilds from the host ids
+            self.g = None
+            return
+        old, B0 = self.g, len(self.live)
+        rows = self.live + new
+        g = self._graph(rows)
+        # the old rows' next-step ids and input rows, written by the last launched step's sampler
+        g.ids[:B0].copy_(old.ids[:B0])
+        g.x[:B0].copy_(old.x[:B0])
+        g.ws["h"][:B0].copy_(old.ws["h"][:B0])
+        # the new rows start from SOS (DecodeGraph.prime's gather + norm on their rows only)
+        g.ids[B0:].fill_(tts.sos)
+        ops.gather_rows(tts.embedding, g.ids[B0:], out=g.x[B0:], M=len(new))
+        ops.rmsnorm(g.x[B0:], tts.main.layers[0].ln1, tts.eps, out=g.ws["h"][B0:], M=len(new))
+        g._uploaded = None
+        self.g, self.live = g, rows
+
     def _launch(self):
         g, rows = self.g, self.live
         steps = [self.states[i].launched for i in rows]
@@ -376,10 +434,39 @@ class SpeechLane:
         return finished
 
     def _drain(self):
+        segs = self._drain_keep()
+        self.live = [i for i in self.live if not self.states[i].done]
+        return segs
+
+    def _drain_keep(self):
+        """Read everything launched (the batch itself is left as it is)."""
         segs = []
         while self.pending:
             self._read(self.pending.popleft(), segs)
-        self.live = [i for i in self.live if not self.states[i].done]
+        return segs
+
+    def _shrink(self):
+        """Rows that have launched their max_tokens leave the batch (their last steps are still being read); the
+        others continue in a graph for the smaller batch with their next-step ids and input rows carried over on
+        the device, as a join does."""
+        st, old = self.states, self.g
+        keep = [j for j, i in enumerate(self.live) if st[i].launched < st[i].max_tokens]
+        rows = [self.live[j] for j in keep]
+        self.live = rows
+        if not rows or old is None:
+            self.g = None
+            return []
+        g = self._graph(rows)
+        if g is old:   # (unreachable: a smaller batch is another cache entry)
+            raise RuntimeError("SpeechLane: shrink reused the running graph")
+        idx = torch.tensor(keep, dtype=torch.long, device=self.engine.device)
+        n = len(rows)
+        g.ids[:n].copy_(old.ids.index_select(0, idx))
+        g.x[:n].copy_(old.x.index_select(0, idx))
+        g.ws["h"][:n].copy_(old.ws["h"][:old.B].index_select(0, idx))
+        g._uploaded = None
+        self.g = g
+        segs, self._held = self._held, []
         return segs
 
     def _finish(self, rows):
@@ -389,15 +476,13 @@ class SpeechLane:
         return segs
 
     def _rebuild(self):
+        """A graph for the live rows from the host-side ids (after a drain: the batch shrank, or rows joined an
+        empty lane)."""
         segs = self._drain()
         if not self.live:
             return segs
-        tts, st = self.engine.tts, self.states
-        rows = self.live
-        max_keys = max(st[i].seq.kv.length + st[i].max_tokens - st[i].launched for i in rows) + 1
-        hist = max(st[i].max_tokens for i in rows) + 1
-        V = tts.vocab if self.forced else tts.vocab + 4
-        g = tts.decode_graph(len(rows), V, self.top_k, self.seed, max_keys, hist, None, True)
+        tts, st, rows = self.engine.tts, self.states, self.live
+        g = self._graph(rows)
         g.ids.copy_(torch.tensor([st[i].all_ids[-1] if st[i].all_ids else tts.sos for i in rows], dtype=I32)
                     .to(self.engine.device))
         g.prime()

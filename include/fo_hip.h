@@ -255,6 +255,9 @@ int fo_conv_post_cl(const float* x, int B, int T, int C, const void* w, const fl
 
 /* llm2TTS.find_min_sum_index window search (models/decoder/llm2tts.py:70-112): res = {min_sum, cut} */
 int fo_silence_cut(const float* x, int L, int N, float* res, hipStream_t s);
+/* the same search for `rows` rows of one vocoder call in one launch: row r at x + r * ld (ld >= L), its
+   (min window sum, cut index) at res + 2 r; each row is staged in LDS when it fits (<= ~37k samples) */
+int fo_silence_cut_rows(const float* x, long long ld, int rows, int L, int N, float* res, hipStream_t s);
 
 /* ---------------------------------------------------------------- codec encoder (fo_codec_enc.hip)
  * VQVAE.encode (models/decoder/ticodec/vqvae.py:44-57).  Channel-first fp32 [B][C][T], fp32 weights. */

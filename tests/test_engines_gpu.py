@@ -180,6 +180,32 @@ def test_silence_cut_kernel_matches_golden(dev):
             assert int(res[1]) == len(s2) - len(g[f"c{ci}_buf"])
 
 
+def test_silence_cut_rows_match_single_rows_and_oracle(dev):
+    """fo_silence_cut_rows (one launch for a vocoder call's rows, each staged in LDS when it fits) gives each row
+    the single-row search's (min sum, cut) exactly; a row too long to stage (48,000 samples) takes the global-
+    memory path and still matches the oracle's find_min_sum_index."""
+    from fo import ops
+    g = np.load(os.path.join(G, "silence_cut.npz"))
+    syns = [g[f"c{ci}_syn"] for ci in range(4)]
+    L = min(len(x) for x in syns)
+    rng = np.random.default_rng(3)
+    rows = np.stack([x[:L] for x in syns] + [rng.standard_normal(L).astype(np.float32) * 0.1 for _ in range(3)])
+    buf = torch.zeros(rows.shape[0], L + 37, device=dev)   # row stride != L
+    buf[:, :L] = torch.from_numpy(rows).to(dev)
+    res = torch.empty(rows.shape[0], 2, device=dev)
+    ops.silence_cut_rows(buf[:, :L], 2401, res)
+    for r in range(rows.shape[0]):
+        one = ops.silence_cut(buf[r, :L].contiguous(), 2401, torch.empty(2, device=dev))
+        assert torch.equal(res[r], one), r
+    long = (rng.standard_normal(48000) * 0.05).astype(np.float32)
+    long[30000:33000] *= 1e-3   # a quiet stretch for the window search to find
+    res = ops.silence_cut(torch.from_numpy(long).to(dev), 2401, torch.empty(2, device=dev)).cpu().numpy()
+    b2, s2 = host.find_min_sum_index(np.zeros(0, np.float32), long, 2401, 0.01)
+    assert (res[0] / 2401 < 0.01) == (s2 is not None)
+    if s2 is not None:
+        assert int(res[1]) == len(s2)
+
+
 def test_sampler_topk_topp(dev):
     from fo import ops
     V = 1000
@@ -407,11 +433,14 @@ def test_speak_two_workers_side_by_side_match_sequential(dev, speech_engine):
             np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("top_k,forced,joins", [(4, True, (0, 17)), (1, False, (0, 9)), (4, True, (0, 0, 33))])
-def test_speech_lane_matches_groups_spoken_alone(dev, speech_engine, top_k, forced, joins):
+@pytest.mark.parametrize("top_k,forced,joins,window", [(4, True, (0, 17), 8), (1, False, (0, 9), 32),
+                                                        (4, True, (0, 0, 33), 8), (4, True, (0, 3, 5), 32)])
+def test_speech_lane_matches_groups_spoken_alone(dev, speech_engine, top_k, forced, joins, window):
     """fo.speak.SpeechLane (the bench's --tts-lane): groups that join the continuously batched AR decode after
-    different numbers of decode reads, with different max_tokens, give every row exactly the ids and the PCM
-    segments of its group spoken alone through speak() -- each row keeps its own RNG stream (key, own step)."""
+    different numbers of decode reads (while the rows before them still decode: the device-side carry-over of
+    their ids and input rows; or into an empty lane), with different max_tokens and their prefill on a stream
+    of its own, give every row exactly the ids and the PCM segments of its group spoken alone through speak()
+    -- each row keeps its own RNG stream (key, own step)."""
     from fo import ops
     from fo.speak import SpeechLane
     jobs = [(_items(dev, 3, 21 + g), 40 + 7 * g) for g in range(len(joins))]
@@ -426,8 +455,8 @@ def test_speech_lane_matches_groups_spoken_alone(dev, speech_engine, top_k, forc
         return [s.all_ids for s in states], segs
 
     ref = [alone(items, n) for items, n in jobs]
-    lane = SpeechLane(speech_engine, top_k=top_k, seed=5, stream=ops.engine_stream(dev, name="tts"),
-                      voc_stream=ops.engine_stream(dev, name="voc"))
+    lane = SpeechLane(speech_engine, top_k=top_k, seed=5, window=window, stream=ops.engine_stream(dev, name="tts"),
+                      voc_stream=ops.engine_stream(dev, name="voc"), prefill_stream=ops.engine_stream(dev, name="tts1"))
     segs = {}
     added, reads = 0, 0
     while added < len(jobs) or not lane.idle:

@@ -173,6 +173,38 @@ def test_text_graph_matches_eager(eng, top_k):
         np.testing.assert_allclose(hg, he, atol=2e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("top_k", [1, 5])
+def test_text_graph_launch_ahead_matches_step_by_step(eng, top_k):
+    """TextGraph.launch without ids (the step queued behind the previous one, fed by its draws on the device)
+    gives the step-by-step graph path's ids, hidden rows and KV lengths exactly -- including a step rolled back
+    and relaunched with host ids (what bench.py's --text-ahead does when a draw must be replaced)."""
+    ref, lr = _text_run(eng, True, 3, 12, top_k)
+    base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    kvs = [base.fork() for _ in range(3)]
+    pre = eng.prefix_ids["system"]
+    ids, hid = eng.text_step([(kv, pre) for kv in kvs], top_k=top_k, seed=7)
+    out = [(list(ids), hid.cpu().numpy().copy())]
+    tg = eng.text_graph(kvs, 12, top_k=top_k, seed=7)
+    pend = tg.launch(kvs, ids)
+    for j in range(12):
+        if j == 5:   # roll the queued step back and relaunch it from the host's ids (the same ones here)
+            tg.read(pend)
+            for kv in kvs:
+                kv.length -= 1
+            pend = tg.launch(kvs, out[-1][0])
+        cur = pend
+        pend = tg.launch(kvs) if j < 11 else None
+        ids, hid = tg.read(cur)
+        out.append((list(ids), hid.cpu().numpy().copy()))
+    assert [kv.length for kv in kvs] == lr
+    for (ir, hr), (ig, hg) in zip(ref, out):
+        assert ir == ig
+        np.testing.assert_array_equal(hg, hr)
+    for kv in kvs:
+        kv.free()
+    base.free()
+
+
 def test_shared_context_prefix_cache_matches_uncached(eng, dev):
     """First chunk (ipu_sl, chat prefix) of sessions forked from one system role: the cached prefix KV
     (computed once, each session a copy-on-write fork of it, the chunk then a captured steady-state step)
