@@ -79,12 +79,15 @@ def parse():
                     help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N "
                          "(2: a sentence's speech never queues behind the previous one's; r03p A/B 1 / 2 / 4 "
                          "workers: 193.5x / 194.8-195.4x / 173.2x)")
-    ap.add_argument("--text-ahead", action="store_true",
-                    help="queue each text step before the previous one is read back (TextGraph.launch with the "
-                         "ids left on the device; a step queued on an EOS draw is rolled back and relaunched)")
+    ap.add_argument("--no-text-ahead", dest="text_ahead", action="store_false",
+                    help="read every text step back before queuing the next (default: each step is queued behind the "
+                         "previous one with its ids left on the device, TextGraph.launch; a step queued on an EOS draw "
+                         "is rolled back and relaunched.  r03u/r03v A/B: text stage 143-147 -> 131-138 ms)")
     ap.add_argument("--tts-lane", action="store_true",
                     help="one continuously batched speech lane (fo.speak.SpeechLane) instead of per-sentence workers: "
-                         "sentences whose speech overlaps decode in the same AR step")
+                         "sentences whose speech overlaps decode in the same AR step (r03u/r03v: the text stage gains "
+                         "3-6 ms, the last sentence's speech loses 4-6 ms -- two latency-bound steps on two streams "
+                         "overlap about as well as one step of twice the rows -- so not the default)")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")
