@@ -56,355 +56,11 @@ __global__ __launch_bounds__(256) void k_rope_kv_write(const float* qkv, int ldq
   }
 }
 
-struct AttnArgs {
-  const float* q;          // [T][H*hd], rotated
-  const int* items;        // [n_items][3]: sequence, first token, token count (a sequence's tokens are contiguous)
-  const int* tok_nvis;     // keys visible to each query token (causal: own cache index + 1; full: all)
-  const int* block_table;  // [S][maxb]
-  const float* kc;
-  const float* vc;
-  float* part_ml;  // [T*H][nsplit][2]   (nsplit > 1)
-  float* part_o;   // [T*H][nsplit][hd]  (nsplit > 1)
-  float* out;      // [T][H*hd]
-  int H, KVH, PS, maxb, nsplit;
-  float scale;
-  // in-launch merge: a work item uses min(nsplit, ceil(keys / kps)) splits, chosen from its own key
-  // count at run time (one captured graph serves a context as it grows); the last split to finish
-  // (arrival ticket cnt[item][kv head], reset by that split) merges the partials -- no combine launch
-  int* cnt;        // nullable: static nsplit splits + k_attn_combine
-  int kps;
-  int tnu;         // items NULL: tokens per item (item b = sequence b, tokens b*tnu .. b*tnu + tnu - 1)
-};
+#include "fo_attn_rows.h"
 
-constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
-constexpr int MAXPG = 256;  // pages of one split staged in LDS (fo_attn_nsplit keeps splits <= 4096 keys)
-
-// fp32 -> bf16 hi + lo: two bf16 operands whose sum carries ~16 mantissa bits
-__device__ __forceinline__ void split8(const float* f, bf16x8& hi, bf16x8& lo) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const __bf16 h = (__bf16)f[i];
-    hi[i] = h;
-    lo[i] = (__bf16)(f[i] - (float)h);
-  }
-}
-
-// sum / max over the 16 lanes of a row group (lanes l, l^1, l^2, l^4, l^8)
-__device__ __forceinline__ float row16_max(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float row16_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Split `sp` of work item `it` has written its partial (part_o / part_ml): publish it and take an
-// arrival ticket; the split that draws ns - 1 merges all ns partials of the item's R rows with
-// k_attn_combine's arithmetic and resets the ticket for the next launch.  Protocol: every wave drains
-// its stores, lane 0 releases at agent scope before the relaxed ticket add, the merging split acquires
-// at agent scope before reading (correct for any placement of the splits over XCDs).
-// last_s / w_s: the kernel's existing LDS (no second __shared__ object for the flag).
-template <int HD>
-__device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns, int t0, int R, int G,
-                                      int& last_s, float* w_s) {
-  const int tid = threadIdx.x;
-  int* ticket = a.cnt + (size_t)it * a.KVH + kvh;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = old == ns - 1;
-  }
-  __syncthreads();
-  if (!last_s) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  // per row: split weights exp(m_q - M) (0 for empty splits) and 1 / l into LDS (w_s: [16][KT + 4],
-  // the kernel's P tile, ns <= KT), then every (row, d) sums its ns partials with independent loads
-  for (int r = tid; r < R; r += blockDim.x) {
-    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-    const float* ml = a.part_ml + th * a.nsplit * 2;
-    float M = -INFINITY;
-    for (int q = 0; q < ns; ++q)
-      if (ml[2 * q + 1] > 0.f) M = fmaxf(M, ml[2 * q]);
-    float l = 0.f;
-    for (int q = 0; q < ns; ++q) {
-      const float ls = ml[2 * q + 1];
-      const float w = ls > 0.f ? expf(ml[2 * q] - M) : 0.f;
-      if (ls > 0.f) l += ls * w;
-      w_s[r * (KT + 4) + q] = w;
-    }
-    w_s[r * (KT + 4) + KT] = 1.f / l;
-  }
-  __syncthreads();
-  for (int e = tid; e < R * HD; e += blockDim.x) {
-    const int r = e / HD, d = e - (e / HD) * HD;
-    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-    const float* po = a.part_o + th * a.nsplit * HD + d;
-    const float* w = w_s + r * (KT + 4);
-    float o = 0.f;
-    for (int q = 0; q < ns; ++q)
-      if (w[q] != 0.f) o += po[(size_t)q * HD] * w[q];
-    a.out[th * HD + d] = o * w[KT];
-  }
-}
-
-// One work item = up to 16 query rows (a sequence's batch tokens x the GQA group sharing one kv head)
-// against that kv head, over split `sp` of the sequence's keys, on the matrix cores:
-//   S = Q K^T   (A = Q rows, B = K rows read straight from the paged cache in B-fragment order)
-//   O = P V     (A = P through LDS, B = V staged in LDS as [key][d])
-// 64-key tiles, one 16-key column block per wave; K and V of the next tile are loaded into registers
-// while the current tile computes.  Every fp32 operand is split into bf16 hi + lo and each product
-// uses three MFMAs (hi*hi + hi*lo + lo*hi), so scores and outputs keep ~fp32 accuracy.  Online
-// softmax per row with the running max exchanged across the 4 waves through LDS.
 template <int HD, int NW = 4>
 __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
-  constexpr int KT = 16 * NW;           // keys per tile: one 16-key column block per wave
-  constexpr int NTH = NW * 64;
-  constexpr int DC = HD / 32;            // 32-wide d chunks (score k-steps)
-  constexpr int NTILE = HD / 16;         // 16-wide d tiles of the output
-  constexpr int NTW = (NTILE + NW - 1) / NW;   // output tiles per wave
-  constexpr int VP = HD + 2;             // V row pitch: the 4 key groups of a B fragment hit distinct banks
-  constexpr int VL = KT * HD / 4 / NTH;  // float4 of V per thread per tile
-  __shared__ float v_s[KT][VP];
-  __shared__ float p_s[16][KT + 4];
-  __shared__ float mx_s[NW][16];
-  __shared__ float l_s[NW][16];
-  __shared__ int nvis_s[16];
-  __shared__ int pg_s[MAXPG];
-
-  const int it = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
-  // items NULL: a uniform batch (tnu tokens per sequence, in sequence order) -- no item-table round trip
-  const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it * a.tnu;
-  const int tn = a.items ? a.items[3 * it + 2] : a.tnu;
-  const int G = a.H / a.KVH;
-  const int R = tn * G;  // <= 16
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int grp = lane >> 4, col = lane & 15;
-  const int* bt = a.block_table + (size_t)seq * a.maxb;
-  // this lane's q row slices, requested before anything that waits (they depend only on t0)
-  float4 qraw[2 * DC];
-  {
-    const int r = col < R ? col : R - 1;
-    const float* qr = a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + 8 * grp;
-#pragma unroll
-    for (int c = 0; c < DC; ++c) {
-      qraw[2 * c] = *reinterpret_cast<const float4*>(qr + 32 * c);
-      qraw[2 * c + 1] = *reinterpret_cast<const float4*>(qr + 32 * c + 4);
-    }
-  }
-  // a block-table row that fits is staged whole, requested together with the key counts (no wait for
-  // this split's page range first); longer rows stage the split's pages once the range is known
-  const bool whole = a.maxb <= MAXPG;
-  if (whole)
-    for (int i = tid; i < a.maxb; i += NTH) pg_s[i] = bt[i];
-  int Lmax = 0;
-  for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
-  int ns = a.nsplit;
-  if (a.cnt) {
-    ns = min(ns, max(1, (Lmax + a.kps - 1) / a.kps));
-    if (sp >= ns) return;  // beyond this item's splits: never counted, never read
-  }
-  const int per = ((Lmax + ns - 1) / ns + KT - 1) / KT * KT;
-  const int c0 = sp * per, c1 = min(Lmax, c0 + per);
-  if (c0 >= c1) {  // empty split: neutral partial
-    for (int r = tid; r < R; r += NTH) {
-      const size_t o = ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * a.nsplit + sp;
-      a.part_ml[o * 2] = -INFINITY;
-      a.part_ml[o * 2 + 1] = 0.f;
-    }
-    if (a.cnt) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
-    return;
-  }
-  const int pb0 = c0 / a.PS, npg = (c1 - 1) / a.PS - pb0 + 1;
-  if (npg > MAXPG || (whole && (c1 - 1) / a.PS >= a.maxb)) {  // host contract broken: poison, never read wrong keys
-    for (int r = tid; r < R; r += NTH) a.out[((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD] = NAN;
-    return;
-  }
-  const int pb = whole ? 0 : pb0;  // pg_s holds pages pb..
-  if (!whole)
-    for (int i = tid; i < npg; i += NTH) pg_s[i] = bt[pb + i];
-  if (tid < 16) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
-
-  // Q as A fragments: row = col (lane & 15), d = 32 c + 8 grp; rows >= R are zero
-  bf16x8 qh[DC], ql[DC];
-  {
-#pragma unroll
-    for (int c = 0; c < DC; ++c) {
-      float f[8];
-      const float4 x0 = qraw[2 * c];
-      const float4 x1 = qraw[2 * c + 1];
-      const float sc = col < R ? a.scale : 0.f;
-      f[0] = x0.x * sc; f[1] = x0.y * sc; f[2] = x0.z * sc; f[3] = x0.w * sc;
-      f[4] = x1.x * sc; f[5] = x1.y * sc; f[6] = x1.z * sc; f[7] = x1.w * sc;
-      split8(f, qh[c], ql[c]);
-    }
-  }
-  __syncthreads();  // pg_s, nvis_s
-
-  const size_t head_off = (size_t)kvh * a.PS * HD;
-  const size_t page_sz = (size_t)a.KVH * a.PS * HD;
-  float4 kA[2 * DC], vA[VL], kB[2 * DC], vB[VL];   // two tiles' K / V in flight (ping-pong)
-  // K: this lane's key (16 per wave) x its 8-wide d slices; V: cooperative 16-B rows for LDS
-#define FO_ATTN_LOAD(kreg, vreg, K0)                                                                      \
-  {                                                                                                       \
-    const int pk = min((K0) + 16 * wave + col, c1 - 1);                                                   \
-    const float* kr = a.kc + (size_t)pg_s[pk / a.PS - pb] * page_sz + head_off + (size_t)(pk % a.PS) * HD \
-                      + 8 * grp;                                                                          \
-    _Pragma("unroll") for (int c = 0; c < DC; ++c) {                                                      \
-      kreg[2 * c] = *reinterpret_cast<const float4*>(kr + 32 * c);                                        \
-      kreg[2 * c + 1] = *reinterpret_cast<const float4*>(kr + 32 * c + 4);                                \
-    }                                                                                                     \
-    _Pragma("unroll") for (int i = 0; i < VL; ++i) {                                                      \
-      const int e = tid + NTH * i, j = e / (HD / 4), d4 = e % (HD / 4);                                   \
-      const int pv = min((K0) + j, c1 - 1);                                                               \
-      vreg[i] = *reinterpret_cast<const float4*>(a.vc + (size_t)pg_s[pv / a.PS - pb] * page_sz + head_off \
-                                                 + (size_t)(pv % a.PS) * HD + d4 * 4);                    \
-    }                                                                                                     \
-  }
-
-  float m_run[4], l_lane[4];
-  f32x4 acc[NTW];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { m_run[i] = -INFINITY; l_lane[i] = 0.f; }
-#pragma unroll
-  for (int n = 0; n < NTW; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // tile t's loads are issued while tile t - 1 computes and two tiles are in flight from the start, so a
-  // 256-key split waits for one round of memory, not two
-  FO_ATTN_LOAD(kA, vA, c0)
-  if (c0 + KT < c1) FO_ATTN_LOAD(kB, vB, c0 + KT)
-  auto tile = [&](float4 (&kreg)[2 * DC], float4 (&vreg)[VL], const int k0) {
-    __syncthreads();  // the previous tile's p_s / v_s readers are done
-#pragma unroll
-    for (int i = 0; i < VL; ++i) {
-      const int e = tid + NTH * i, j = e / (HD / 4), d4 = e % (HD / 4);
-      *reinterpret_cast<float2*>(&v_s[j][d4 * 4]) = make_float2(vreg[i].x, vreg[i].y);
-      *reinterpret_cast<float2*>(&v_s[j][d4 * 4 + 2]) = make_float2(vreg[i].z, vreg[i].w);
-    }
-    bf16x8 kh[DC], kl[DC];
-#pragma unroll
-    for (int c = 0; c < DC; ++c) {
-      const float f[8] = {kreg[2 * c].x, kreg[2 * c].y, kreg[2 * c].z, kreg[2 * c].w,
-                          kreg[2 * c + 1].x, kreg[2 * c + 1].y, kreg[2 * c + 1].z, kreg[2 * c + 1].w};
-      split8(f, kh[c], kl[c]);
-    }
-    if (k0 + 2 * KT < c1) FO_ATTN_LOAD(kreg, vreg, k0 + 2 * KT)
-    // S[r = 4 grp + i][key = k0 + 16 wave + col]
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < DC; ++c) {
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[c], kh[c], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[c], kl[c], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ql[c], kh[c], s, 0, 0, 0);
-    }
-    const int key = k0 + 16 * wave + col;
-    bool valid[4];
-    float mw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      valid[i] = key < c1 && key < nvis_s[4 * grp + i];
-      mw[i] = row16_max(valid[i] ? s[i] : -INFINITY);
-    }
-    if (col == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) mx_s[wave][4 * grp + i] = mw[i];
-    }
-    __syncthreads();
-    float alpha[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * grp + i;
-      float tm = mx_s[0][r];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) tm = fmaxf(tm, mx_s[w][r]);
-      const float mn = fmaxf(m_run[i], tm);
-      alpha[i] = (m_run[i] == mn) ? 1.f : expf(m_run[i] - mn);
-      m_run[i] = mn;
-      const float p = valid[i] ? expf(s[i] - mn) : 0.f;
-      l_lane[i] = l_lane[i] * alpha[i] + p;
-      p_s[r][16 * wave + col] = p;
-    }
-    __syncthreads();  // p_s and v_s complete
-    // O[r][d] += P[r][:] V[:][d] for this wave's d tiles
-#pragma unroll
-    for (int n = 0; n < NTW; ++n) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[n][i] *= alpha[i];
-    }
-#pragma unroll
-    for (int kc = 0; kc < KT / 32; ++kc) {
-      bf16x8 ph, pl;
-      {
-        const float4 x0 = *reinterpret_cast<const float4*>(&p_s[col][32 * kc + 8 * grp]);
-        const float4 x1 = *reinterpret_cast<const float4*>(&p_s[col][32 * kc + 8 * grp + 4]);
-        const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        split8(f, ph, pl);
-      }
-#pragma unroll
-      for (int n = 0; n < NTW; ++n) {
-        const int dt = wave + NW * n;
-        if (dt < NTILE) {
-          float f[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = v_s[32 * kc + 8 * grp + e][16 * dt + col];
-          bf16x8 vh, vl;
-          split8(f, vh, vl);
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vh, acc[n], 0, 0, 0);
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vl, acc[n], 0, 0, 0);
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vh, acc[n], 0, 0, 0);
-        }
-      }
-    }
-  };
-  for (int k0 = c0; k0 < c1; k0 += 2 * KT) {
-    tile(kA, vA, k0);
-    if (k0 + KT < c1) tile(kB, vB, k0 + KT);
-  }
-#undef FO_ATTN_LOAD
-  // row sums: 16 lanes of the row group, then the 4 waves
-  float lw[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) lw[i] = row16_sum(l_lane[i]);
-  if (col == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) l_s[wave][4 * grp + i] = lw[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 4 * grp + i;
-    if (r >= R) continue;
-    float l = l_s[0][r];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) l += l_s[w][r];
-    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-#pragma unroll
-    for (int n = 0; n < NTW; ++n) {
-      const int dt = wave + NW * n;
-      if (dt >= NTILE) continue;
-      const int d = 16 * dt + col;
-      if (ns == 1) {
-        a.out[th * HD + d] = acc[n][i] / l;
-      } else {
-        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[n][i];
-      }
-    }
-    if (ns > 1 && wave == 0 && col == 0) {
-      a.part_ml[(th * a.nsplit + sp) * 2] = m_run[i];
-      a.part_ml[(th * a.nsplit + sp) * 2 + 1] = l;
-    }
-  }
-  if (a.cnt && ns > 1) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
+  attn_rows_body<HD, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Single-row decode attention (the AR speech decoder's step, models/decoder/decoder.py:341-349: one

@@ -67,7 +67,7 @@ class DecoderStack:
               "nsplit": nsplit, "part_ml": None, "part_o": None,
               "sA": ops.RowStats(T, device), "sB": ops.RowStats(T, device),
               "xg": torch.empty(T, self.D, dtype=F32, device=device),
-              "tickets": torch.zeros(T * KVH, dtype=torch.int32, device=device)}
+              "tickets": torch.zeros(max(T, 2) * KVH, dtype=torch.int32, device=device)}
         if nsplit > 1:
             ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
@@ -97,15 +97,15 @@ class DecoderStack:
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
                     self.pool.PS)
-            if i == 0:  # the stream's first rows come from a gather: no producer statistics yet
-                if not pre_normed:
-                    ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
-                L.qkv.qkv_rope(h, T, *rope)
-            else:       # input RMSNorm fused: x*gamma and row sums came from the previous down proj
-                L.qkv.qkv_rope(xg, T, *rope, norm=(sA, self.eps))
-            ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table,
-                          self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale, nsplit, part_ml, part_o,
-                          att, tickets=ws["tickets"], keys_per_split=self.attn_kps)
+            # (the first layer's rows come from a gather: no producer statistics yet; later layers apply the input
+            # RMSNorm from the previous down projection's x*gamma and row sums)
+            xin, norm = (h, None) if i == 0 else (xg, (sA, self.eps))
+            if i == 0 and not pre_normed:
+                ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
+            L.qkv.qkv_rope(xin, T, *rope, norm=norm)
+            ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis,
+                          meta.block_table, self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale,
+                          nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps)
             L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))
             L.gu(xg, out=m, M=T, norm=(sB, self.eps))
             if i == last and final_norm is None:
