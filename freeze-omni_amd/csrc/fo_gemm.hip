@@ -768,20 +768,20 @@ void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, h
 
 // X-stationary weight stream for M <= 16 fp32 rows and K = NW * KPW * 32 (Qwen2: K = 3584 = 16 x 7 x 32).
 // One workgroup per CU (the LDS footprint admits one), persistent over a contiguous, balanced range of
-// column units (2 packed tiles: a gate/up pair, a RoPE (i, i + hd/2) pair, or two plain tiles).
+// column units (2 packed tiles: a gate/up pair; the plain and RoPE unit forms measured slower than the grid
+// kernels on the 26-33 MB projections and are not built).
 //  * prologue: wave w loads ITS K slice of X once, split into bf16 hi (kept in VGPRs) and lo (kept in
 //    the wave's private LDS region) -- X never goes through the vector-memory path again, so the weight
 //    stream is the only VMEM traffic (the fo_gemm grid re-reads X from L2 once per column group);
 //  * steady state: per unit, two tiles' weight fragments (KPW x 1 KiB per wave each) are double
 //    buffered -- the next unit's loads are issued right after the MFMAs that free a buffer;
 //  * per unit the NW partial tiles are reduced through LDS (two barriers), then the epilogue of the
-//    row-major output (bias, SwiGLU, RoPE + KV append, residual, RMSNorm statistics) as in gemm_body.
+//    row-major output (the post-scaled RMSNorm and SwiGLU) as in gemm_body.
 constexpr int XS_NW = 8, XS_KPW = 14;
-template <int NW, int KPW, int MODE>  // MODE 0: plain (+stats), 1: SwiGLU pair, 2: RoPE pair
+template <int NW, int KPW>  // the SwiGLU pair (gate, up) of one 16-column output tile per unit
 __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
   __shared__ bf16x8 xlo[NW][KPW][64];
   __shared__ float part[NW][2][16][17];
-  __shared__ float ybuf[2][16][17];
   __shared__ float rstd_s[16];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int KS = NW * KPW;
@@ -859,57 +859,20 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
     }
     __syncthreads();
     const int e = threadIdx.x;
-    if constexpr (MODE != 0) {
-      if (e < 256) {
-        const int rr = e >> 4, c = e & 15;
-        float x1 = 0.f, x2 = 0.f;
+    if (e < 256) {
+      const int rr = e >> 4, c = e & 15;
+      float x1 = 0.f, x2 = 0.f;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          x1 += part[w][0][rr][c];
-          x2 += part[w][1][rr][c];
-        }
-        if (a.rstats) {
-          x1 *= rstd_s[rr];
-          x2 *= rstd_s[rr];
-        }
-        if (rr < a.M) {
-          if constexpr (MODE == 1) {
-            const int n = u * 16 + c;
-            if (n < a.N) epilogue_store(a, true, rr, n, x1, x2);
-          } else {
-            rope_store(a, rr, rope_col(a, u, c), x1, x2);
-          }
-        }
+      for (int w = 0; w < NW; ++w) {
+        x1 += part[w][0][rr][c];
+        x2 += part[w][1][rr][c];
       }
-    } else {
-      float y = 0.f;
-      const int t = e >> 8, rr = (e >> 4) & 15, c = e & 15;
-      const int n = (2 * u + t) * 16 + c;
-      if (e < 512) {
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) v += part[w][t][rr][c];
-        if (a.rstats) v *= rstd_s[rr];
-        if (rr < a.M && n < a.N) {
-          y = epilogue_store(a, false, rr, n, v, 0.f);
-          if (a.yg) a.yg[(size_t)rr * a.ldy + n] = y * a.gnext[n];
-        }
+      if (a.rstats) {
+        x1 *= rstd_s[rr];
+        x2 *= rstd_s[rr];
       }
-      if (a.sout) {  // row partial sums of squares (and sums) of this unit's 32 columns
-        if (e < 512) ybuf[t][rr][c] = (rr < a.M && n < a.N) ? y : 0.f;
-        __syncthreads();
-        if (e < 16 && e < a.M) {
-          float ss = 0.f, s1 = 0.f;
-#pragma unroll
-          for (int q = 0; q < 32; ++q) {
-            const float v = ybuf[q >> 4][e][q & 15];
-            ss += v * v;
-            s1 += v;
-          }
-          a.sout[(size_t)e * units + u] = ss;
-          if (a.sout1) a.sout1[(size_t)e * units + u] = s1;
-        }
-      }
+      const int n = u * 16 + c;
+      if (rr < a.M && n < a.N) epilogue_store(a, true, rr, n, x1, x2);
     }
   }
 }
@@ -1120,9 +1083,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.S = 1;
     if (sgroups) *sgroups = units;
     if (sout) FO_REQUIRE(!swiglu && !rope, "fo_gemm: statistics with a paired epilogue");
-    if (swiglu) hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 1>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
-    else if (rope) hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 2>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
-    else hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 0>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
     return fo::check_launch("fo_gemm/xs");
   }
   // mid-size row counts on large weights (the Qwen2 prefills of a turn: assistant prefix, the first

@@ -25,7 +25,11 @@ def stream(device=None):
 _ENGINE_STREAMS = {}
 
 
-HIGH_PRIORITY_STREAMS = ("tts", "voc")   # name prefixes ("tts1", "voc1": a second speech worker's)
+# name prefixes of the streams created at the device's greatest priority: the AR decode's ("tts", "tts1": a second
+# speech worker's).  The vocoder streams ("voc*") stay at the default priority: r03y A/B (bench, text steps queued
+# ahead) tts + voc high 189.9 / 196.9x, tts only 197.4 / 197.8x (text stage 137-139 -> 134.5 ms, first PCM unchanged
+# 58.7 ms), none 188.8 / 192.2x (first PCM 71 ms).  FO_HIGH_PRIO (comma-separated prefixes, "" none) overrides it.
+HIGH_PRIORITY_STREAMS = tuple(p for p in os.environ.get("FO_HIGH_PRIO", "tts").split(",") if p) or ("\0",)
 # priority level of the side stream (the pipelined listen's encoder stage, the vocoder when no "voc" stream is
 # given): 0 default, -1 the device's least (FO_SIDE_PRIORITY, A/B probes)
 SIDE_STREAM_PRIORITY = int(os.environ.get("FO_SIDE_PRIORITY", "0"))
@@ -52,9 +56,9 @@ def engine_stream(device, side=False, name=None):
     """A blocking HIP stream per device (fo_stream_create) wrapped for torch: it orders against the
     legacy default stream implicitly, and graph capture (which needs a non-null stream) runs on it.
     side=True: a second such stream, for work that overlaps the main one (pipelined listen stages).
-    name: further named streams ("tts", "voc": speech generation running beside the text decode; those two
-    are created at the device's greatest priority, HIGH_PRIORITY_STREAMS, so a sentence's audio is not
-    queued behind the text decode's weight streams)."""
+    name: further named streams ("tts", "voc": speech generation running beside the text decode; the AR decode's
+    "tts*" streams are created at the device's greatest priority, HIGH_PRIORITY_STREAMS, so a sentence's codec
+    tokens are not queued behind the text decode's weight streams)."""
     import ctypes
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()

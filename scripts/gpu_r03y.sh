@@ -1,0 +1,21 @@
+# Round-3 call y: the SwiGLU-only k_gemm_xs (GPU suite), then the bench with the text steps queued ahead under
+# speech-stream priority variants (default tts+voc high / tts only / none) and one sentence worker, twice each.
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=r03y
+O=gpurun_out/${R}.txt
+: > $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${R}_pytest_gpu.log 2>&1 || { tail -30 gpurun_out/${R}_pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/${R}_pytest_gpu.log >> $O
+for i in 1 2; do
+  for A in "" "FO_HIGH_PRIO=tts" "FO_HIGH_PRIO=" "--tts-workers 1"; do
+    echo -n "$i [$A] " >> $O
+    EV=$(echo "$A" | tr ' ' '\n' | grep = | tr '\n' ' '); ARGS=$(echo "$A" | tr ' ' '\n' | grep -v = | tr '\n' ' ')
+    env $EV timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 $ARGS > gpurun_out/${R}_b.log 2>&1 || { tail -30 gpurun_out/${R}_b.log; exit 1; }
+    grep '^{' gpurun_out/${R}_b.log | python -c "
+import json,sys
+d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['p50_first_audio_ms'], {k: round(v,1) for k, v in d['stage_ms'].items() if k in ('listen','text','speak_after_text')})" >> $O
+  done
+done
+cat $O
