@@ -85,9 +85,11 @@ def parse():
                          "is rolled back and relaunched.  r03u/r03v A/B: text stage 143-147 -> 131-138 ms)")
     ap.add_argument("--tts-lane", action="store_true",
                     help="one continuously batched speech lane (fo.speak.SpeechLane) instead of per-sentence workers: "
-                         "sentences whose speech overlaps decode in the same AR step (r03u/r03v: the text stage gains "
-                         "3-6 ms, the last sentence's speech loses 4-6 ms -- two latency-bound steps on two streams "
-                         "overlap about as well as one step of twice the rows -- so not the default)")
+                         "sentences whose speech overlaps decode in the same AR step; the last sentence (started when "
+                         "the text decode is over) speaks on its own streams.  r03u/r03v: joining the last sentence "
+                         "to the lane cost 4-6 ms after the text (two latency-bound steps on two streams overlap about "
+                         "as well as one step of twice the rows); r03z with the tail worker: text -3 ms, tail +1.5 ms, "
+                         "197.2x vs 196.9x over three runs each -- within noise, so not the default")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")
@@ -187,7 +189,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
                    len(rec.sentences))
             rec.sentences.append(time.perf_counter())
             if tts is not None:
-                tts.submit(job)
+                tts.submit(job, last=j == T - 1)
             else:
                 run_sentence(engine, args, rec, *job)
             s0 = j + 1
@@ -338,13 +340,20 @@ class LaneTTS:
 
         self.t = threading.Thread(target=work, daemon=True)
         self.t.start()
+        # the response's last sentence (submitted once the text decode is over) speaks on its own streams beside
+        # the lane's remaining rows instead of joining them (two latency-bound steps on two streams overlap; r03v)
+        self.tail = SentenceTTS(engine, args, rec, 1, names=("tts2", "voc2"))
 
-    def submit(self, job):
-        self.q.put(job)
+    def submit(self, job, last=False):
+        if last:
+            self.tail.submit(job)
+        else:
+            self.q.put(job)
 
     def join(self):
         self.q.put(None)
         self.t.join()
+        self.tail.join()
         if self.err is not None:
             raise self.err
 
@@ -356,7 +365,7 @@ class SentenceTTS:
     are those of the reference's sequential loop (bin/inference.py:152-183, which pauses the text decode for
     each sentence).  Sentences are spoken in order (one user's audio is a sequence)."""
 
-    def __init__(self, engine, args, rec, workers=1):
+    def __init__(self, engine, args, rec, workers=1, names=None):
         """workers > 1: sentence k goes to worker k % workers, each with its own streams, so a sentence's speech
         does not queue behind the previous sentence's (the AR decode graphs and vocoder graphs are cached per
         stream, fo/tts.py, fo/codec.py)."""
@@ -369,8 +378,8 @@ class SentenceTTS:
         for w in range(workers):
             q = queue.Queue()
             sfx = "" if w == 0 else str(w)
-            stream = ops.engine_stream(engine.device, name="tts" + sfx)
-            voc = ops.engine_stream(engine.device, name="voc" + sfx)
+            stream = ops.engine_stream(engine.device, name=names[0] if names else "tts" + sfx)
+            voc = ops.engine_stream(engine.device, name=names[1] if names else "voc" + sfx)
 
             def work(q=q, stream=stream, voc=voc):
                 import torch
@@ -390,7 +399,7 @@ class SentenceTTS:
             self.qs.append(q)
             self.ts.append(t)
 
-    def submit(self, job):
+    def submit(self, job, last=False):
         self.qs[self.k % len(self.qs)].put(job)
         self.k += 1
 
