@@ -125,6 +125,31 @@ def test_paged_kv_cow_fork_and_free():
     assert pool.pages_in_use() == 0
 
 
+def test_batch_meta_rows_match_per_token_rule():
+    """BatchMeta's per-token rows (sequence, RoPE position, cache slot, visible keys) follow the per-token rule for
+    ragged batches of short (filled token by token) and long (filled vectorised, > 8 tokens) entries, causal and
+    full, from arbitrary starting lengths across page boundaries."""
+    import numpy as np
+    from fo.kv import BatchMeta, KVPool, KVSeq
+    pool = KVPool(1, 1, 4, 512, 16, "cpu")
+    for trial in range(12):
+        rng = np.random.default_rng(trial)
+        seqs = [KVSeq(pool) for _ in range(5)]
+        for s in seqs:
+            s.reserve(int(rng.integers(0, 40)))
+            s.length = len(s.pages) * 16 - int(rng.integers(0, 16)) if s.pages else 0
+        ents = [(s, int(rng.integers(1, 40)), int(rng.integers(0, 9)), bool(rng.integers(0, 2))) for s in seqs]
+        olds = [s.length for s in seqs]
+        m = BatchMeta(ents, "cpu", gqa=2)
+        rows = []
+        for k, (s, n, p0, causal) in enumerate(ents):
+            rows += [(k, p0 + i, s.slot(olds[k] + i), olds[k] + i + 1 if causal else olds[k] + n) for i in range(n)]
+        got = list(zip(m.tok_seq.tolist(), m.tok_pos.tolist(), m.tok_slot.tolist(), m.tok_nvis.tolist()))
+        assert got == rows
+        for s in seqs:
+            s.free()
+
+
 def test_pastkv_deepcopy_forks():
     from fo.kv import KVPool, KVSeq, BatchMeta
     from models.audioLLM import PastKeyValues
