@@ -629,7 +629,7 @@ class TextGraph:
         # steps in flight (launch() / read()): each has its own pinned id read-back and event
         self.out_host = [torch.empty(B, dtype=I32).pin_memory() for _ in range(self.DEPTH)]
         self.evs = [ListenGraph._event() for _ in range(self.DEPTH)]
-        self.n_launched = 0
+        self.n_launched = self.n_read = 0
         self.top_k = top_k
         self.err = ops.SampleCheck()
         self.main = ops.engine_stream(dev)
@@ -657,7 +657,7 @@ class TextGraph:
         token per session from the host; None: the ids the previous launched step draws (still on the device),
         so the step can be queued before that one is read back.  Appends one KV position per session."""
         B, maxb = self.B, self.maxb
-        if self.n_launched - getattr(self, "n_read", 0) >= self.DEPTH:
+        if self.n_launched - self.n_read >= self.DEPTH:
             raise RuntimeError("text graph: more than DEPTH steps in flight")
         if ids is None and self.n_launched == 0:
             raise ValueError("text graph: the first step needs its input ids")
@@ -693,7 +693,7 @@ class TextGraph:
         """Wait for a launched step; returns (drawn ids list, last hidden rows [B, D] device)."""
         k, hid = handle
         _lib.call("fo_event_sync", self.evs[k])
-        self.n_read = getattr(self, "n_read", 0) + 1
+        self.n_read += 1
         self.err.check("text decode step")
         return self.out_host[k].tolist(), hid
 

@@ -29,7 +29,7 @@ _ENGINE_STREAMS = {}
 # speech worker's).  The vocoder streams ("voc*") stay at the default priority: r03y A/B (bench, text steps queued
 # ahead) tts + voc high 189.9 / 196.9x, tts only 197.4 / 197.8x (text stage 137-139 -> 134.5 ms, first PCM unchanged
 # 58.7 ms), none 188.8 / 192.2x (first PCM 71 ms).  FO_HIGH_PRIO (comma-separated prefixes, "" none) overrides it.
-HIGH_PRIORITY_STREAMS = tuple(p for p in os.environ.get("FO_HIGH_PRIO", "tts").split(",") if p) or ("\0",)
+HIGH_PRIORITY_STREAMS = tuple(p for p in os.environ.get("FO_HIGH_PRIO", "tts").split(",") if p)   # () matches none
 # priority level of the side stream (the pipelined listen's encoder stage, the vocoder when no "voc" stream is
 # given): 0 default, -1 the device's least (FO_SIDE_PRIORITY, A/B probes)
 SIDE_STREAM_PRIORITY = int(os.environ.get("FO_SIDE_PRIORITY", "0"))
