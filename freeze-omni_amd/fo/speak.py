@@ -373,11 +373,15 @@ class SpeechLane:
                 s.seq = None
 
     # ---- internals
+    def _busy(self, B):
+        """A cached graph of batch size B still has launched steps unread (reusing it would overwrite their id
+        history, regrowing it would destroy it)."""
+        return any(e[2].B == B for e in self.pending)
+
     def _graph(self, rows):
-        """The decode graph for batch `rows`.  Graphs are cached by batch size; one that launched steps still
-        unread is drained first (its id history would be overwritten; a regrown cache entry is destroyed)."""
-        if any(e[2].B == len(rows) for e in self.pending):
-            self._held += self._drain_keep()
+        """The decode graph for batch `rows` (graphs are cached by batch size; callers make sure it is not busy)."""
+        if self._busy(len(rows)):
+            raise RuntimeError("SpeechLane: decode graph reused with steps still in flight")
         tts, st = self.engine.tts, self.states
         max_keys = max(st[i].seq.kv.length + st[i].max_tokens - st[i].launched for i in rows) + 1
         hist = max(st[i].max_tokens for i in rows) + 1
@@ -392,8 +396,11 @@ class SpeechLane:
             torch.cuda.current_stream().wait_event(ev)
             new += rows
         self.joining = [j for j in self.joining if all(j is not r for r in ready)]
-        if self.g is None or not self.live:
-            self.live += new   # no device state to carry over: the next launch rebuilds from the host ids
+        if self.g is None or not self.live or self._busy(len(self.live) + len(new)):
+            # no device state to carry over (or the larger graph still has steps in flight): read everything
+            # launched, then the next launch rebuilds from the host ids
+            self._held += self._drain()
+            self.live += new
             self.g = None
             return
         old, B0 = self.g, len(self.live)
@@ -434,15 +441,11 @@ class SpeechLane:
         return finished
 
     def _drain(self):
-        segs = self._drain_keep()
-        self.live = [i for i in self.live if not self.states[i].done]
-        return segs
-
-    def _drain_keep(self):
-        """Read everything launched (the batch itself is left as it is)."""
+        """Read everything launched; rows that finished leave the batch."""
         segs = []
         while self.pending:
             self._read(self.pending.popleft(), segs)
+        self.live = [i for i in self.live if not self.states[i].done]
         return segs
 
     def _shrink(self):
@@ -452,10 +455,14 @@ class SpeechLane:
         st, old = self.states, self.g
         keep = [j for j, i in enumerate(self.live) if st[i].launched < st[i].max_tokens]
         rows = [self.live[j] for j in keep]
-        self.live = rows
-        if not rows or old is None:
+        if not rows or old is None or self._busy(len(rows)):
+            # nothing to carry over, or the smaller graph still has steps in flight: drain (the launched-out rows
+            # finish there) and rebuild from the host ids at the next launch
+            self.live = rows
+            segs = self._drain()
             self.g = None
-            return []
+            return segs
+        self.live = rows
         g = self._graph(rows)
         if g is old:   # (unreachable: a smaller batch is another cache entry)
             raise RuntimeError("SpeechLane: shrink reused the running graph")
@@ -466,8 +473,7 @@ class SpeechLane:
         g.ws["h"][:n].copy_(old.ws["h"][:old.B].index_select(0, idx))
         g._uploaded = None
         self.g = g
-        segs, self._held = self._held, []
-        return segs
+        return []
 
     def _finish(self, rows):
         segs = _emit(self.engine, self.states, [], [i for i in rows if self.states[i].tokens],
