@@ -83,13 +83,12 @@ def parse():
                     help="read every text step back before queuing the next (default: each step is queued behind the "
                          "previous one with its ids left on the device, TextGraph.launch; a step queued on an EOS draw "
                          "is rolled back and relaunched.  r03u/r03v A/B: text stage 143-147 -> 131-138 ms)")
-    ap.add_argument("--tts-lane", action="store_true",
-                    help="one continuously batched speech lane (fo.speak.SpeechLane) instead of per-sentence workers: "
-                         "sentences whose speech overlaps decode in the same AR step; the last sentence (started when "
-                         "the text decode is over) speaks on its own streams.  r03u/r03v: joining the last sentence "
-                         "to the lane cost 4-6 ms after the text (two latency-bound steps on two streams overlap about "
-                         "as well as one step of twice the rows); r03z with the tail worker: text -3 ms, tail +1.5 ms, "
-                         "197.2x vs 196.9x over three runs each -- within noise, so not the default")
+    ap.add_argument("--no-tts-lane", dest="tts_lane", action="store_false",
+                    help="per-sentence workers (--tts-workers) instead of the default continuously batched speech lane "
+                         "(fo.speak.SpeechLane): sentences whose speech overlaps decode in the same AR step; the last "
+                         "sentence (started when the text decode is over) speaks on its own streams.  r03zf, four runs "
+                         "each on one box: lane 198.3 / 198.5 / 197.9 / 198.6x vs workers 197.5 / 197.2 / 197.6 / "
+                         "197.0x (text stage -3.7 ms, speech after the text +1.5 ms)")
     ap.add_argument("--switch-interval", type=float, default=None,
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")
