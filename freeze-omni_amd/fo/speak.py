@@ -455,7 +455,14 @@ class SpeechLane:
         st, old = self.states, self.g
         keep = [j for j, i in enumerate(self.live) if st[i].launched < st[i].max_tokens]
         rows = [self.live[j] for j in keep]
-        if not rows or old is None or self._busy(len(rows)):
+        if not rows:
+            # every row launched out: the next pumps read their last steps one at a time, so a group that arrives
+            # meanwhile is taken in (its prefill starts) at once -- its join drains what is left (r03zi: draining
+            # here held the lane thread ~12.5 ms, a window of steps, while the next sentence waited in the queue;
+            # r03zj)
+            self.live, self.g = [], None
+            return []
+        if old is None or self._busy(len(rows)):
             # nothing to carry over, or the smaller graph still has steps in flight: drain (the launched-out rows
             # finish there) and rebuild from the host ids at the next launch
             self.live = rows
