@@ -6,6 +6,7 @@ same step share one vocoder launch.  Emission follows find_min_sum_index
 (models/decoder/llm2tts.py:70-112) using the fo_silence_cut kernel for the window search.
 """
 import collections
+import os
 import time
 
 import torch
@@ -282,7 +283,7 @@ class SpeechLane:
     EOS masking (min_tokens) must cover a row's whole life (min_tokens == max_tokens, the benchmark policy) or none
     of it (min_tokens == 0), and all groups of a lane agree: one launch draws every row from one bound."""
 
-    JOIN_WINDOW = 4
+    JOIN_WINDOW = int(os.environ.get("FO_LANE_JOIN_WINDOW", "4"))   # steps launched ahead while a group joins
 
     def __init__(self, engine, top_k=1, codec_chunk_size=40, codec_padding_size=10, N=2401, seg_threshold=0.01,
                  seed=0, window=32, stream=None, voc_stream=None, prefill_stream=None):
