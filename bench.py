@@ -13,12 +13,13 @@ One "step" = one full dialogue turn for every user on every rank (SURVEY.md §8(
            24 kHz audio per response) -> TiCodec vocoder per 40(+10+10) tokens -> silence-cut emission.
 value = seconds of 24 kHz speech emitted by all users on all ranks / max-over-ranks wall seconds
 (aggregate real-time factor, higher is better).  Also reported: per-user RTF (audio / (dialog_ss ->
-last PCM)), p50/p90 first-audio latency (dialog_ss -> PCM of the first vocoder chunk known on the host,
-the reference's "first PCM chunk" of assets/latency.png) and p50_first_emit_gated_ms (dialog_ss -> first
-segment released by the find_min_sum_index silence gate; random-weight codec output has no 100 ms
-quiet window, so the gate holds the audio until the final flush).
+last PCM)), p50/p90 first-audio latency = dialog_ss -> the first segment llm2TTS.run would YIELD, i.e. released by
+the find_min_sum_index silence gate (models/decoder/llm2tts.py:141-153, what the reference's caller sees;
+random-weight codec output has no 100 ms quiet window, so the gate holds the audio until a sentence's final
+flush), and p50_first_pcm_ms = dialog_ss -> PCM of the first vocoder chunk known on the host, before the gate.
 Weights: counter-hash synthetic weights at Qwen2-7B / paper geometry (configs/real), generated on
-device; no checkpoint is on the box.  Launch for N>1 with torch.distributed.run (one rank per GPU).
+device; no checkpoint is on the box.  `--gpus N` (N > 1) starts N ranks itself (torch.distributed.run, one rank
+per GPU, RCCL); under an outer torch.distributed.run each process is one rank and --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -75,16 +76,13 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=64,
                     help="BLAS threads of the cpu_baseline leg (set before numpy is imported; default one socket)")
     ap.add_argument("--no-single-user", action="store_true", help="skip the config-2 (1 user) leg")
-    ap.add_argument("--tts-workers", type=int, default=2,
-                    help="sentence-speech workers (streams) beside the text decode: sentence k on worker k %% N "
-                         "(2: a sentence's speech never queues behind the previous one's; r03p A/B 1 / 2 / 4 "
-                         "workers: 193.5x / 194.8-195.4x / 173.2x)")
     ap.add_argument("--no-text-ahead", dest="text_ahead", action="store_false",
                     help="read every text step back before queuing the next (default: each step is queued behind the "
                          "previous one with its ids left on the device, TextGraph.launch; a step queued on an EOS draw "
                          "is rolled back and relaunched.  r03u/r03v A/B: text stage 143-147 -> 131-138 ms)")
     ap.add_argument("--no-tts-lane", dest="tts_lane", action="store_false",
-                    help="per-sentence workers (--tts-workers) instead of the default continuously batched speech lane "
+                    help="one sentence-speech worker (each sentence in turn on its own streams) instead of the default "
+                         "continuously batched speech lane "
                          "(fo.speak.SpeechLane): sentences whose speech overlaps decode in the same AR step; the last "
                          "sentence (started when the text decode is over) speaks on its own streams.  r03zf, four runs "
                          "each on one box: lane 198.3 / 198.5 / 197.9 / 198.6x vs workers 197.5 / 197.2 / 197.6 / "
@@ -93,7 +91,82 @@ def parse():
                     help="Python thread switch interval (s) while the sentence-speech worker runs beside the text "
                          "decode (default: the interpreter's 5 ms)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def launch_plan(gpus, env, n_visible, argv, script, port):
+    """How `bench.py --gpus N` runs (bin/pool.py:61-91: one replica per GPU):
+      * ("rank", None): this process is one rank -- N = 1 without a launcher, or a rank started by
+        torch.distributed.run (WORLD_SIZE in the environment, which must equal N);
+      * ("spawn", cmd): N > 1 and no launcher: start N ranks with torch.distributed.run (one per GPU, RCCL), this
+        process only waits for them and exits with their code.  Decided before any GPU call (n_visible comes from
+        torch.cuda.device_count(), which does not initialise HIP on this image);
+      * ("error", msg): --gpus disagrees with WORLD_SIZE, or N exceeds the visible devices -- one GPU is never
+        oversubscribed silently.  FO_DIST_REHEARSAL=1 (every rank on cuda:0 over gloo, labelled as a one-GPU
+        rehearsal) is the only way to run N ranks on fewer GPUs."""
+    rehearsal = env.get("FO_DIST_REHEARSAL") == "1"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "error", f"--gpus {gpus} disagrees with WORLD_SIZE={world} set by the launcher"
+        local = int(env.get("LOCAL_RANK", "0"))
+        if not rehearsal and local >= n_visible:
+            return "error", (f"rank with LOCAL_RANK={local} but only {n_visible} GPU(s) visible "
+                             f"(FO_DIST_REHEARSAL=1 runs every rank on cuda:0)")
+        return "rank", None
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    if gpus > 1 and not rehearsal and gpus > n_visible:
+        return "error", (f"--gpus {gpus} exceeds the {n_visible} visible GPU(s); refusing to put several ranks on one "
+                         f"GPU (FO_DIST_REHEARSAL=1 rehearses the N-rank path on cuda:0 over gloo)")
+    if gpus == 1:
+        return "rank", None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", script] + list(argv)
+    return "spawn", cmd
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args):
+    """Apply launch_plan for this invocation; returns only in a process that is a rank."""
+    import subprocess
+
+    import torch
+    # no HIP initialisation on this image: safe before spawning ranks (the selftest never touches a GPU)
+    n_visible = args.gpus if args.launch_selftest else torch.cuda.device_count()
+    kind, what = launch_plan(args.gpus, os.environ, n_visible, sys.argv[1:], os.path.abspath(__file__),
+                             _free_port())
+    if kind == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if kind == "spawn":
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+        sys.exit(subprocess.call(what, env=env))
+
+
+def launch_selftest():
+    """--launch-selftest: what each rank of a spawned launch sees, without touching a GPU (CPU test of the plumbing):
+    ranks join a gloo group, gather (rank, local rank, world, device the rank would pin), rank 0 prints one line."""
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ["LOCAL_RANK"])
+    dist.init_process_group("gloo")
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "local_rank": local, "world": world, "device": f"cuda:{local}",
+                                 "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"})
+    if rank == 0:
+        print(json.dumps({"launch_selftest": got}), flush=True)
+    dist.destroy_process_group()
 
 
 def synth_pcm(n, seed):
@@ -169,7 +242,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
     rec = SpeechRecorder(B)
     tts = None
     if args.concurrent_tts:
-        tts = LaneTTS(engine, args, rec) if args.tts_lane else SentenceTTS(engine, args, rec, args.tts_workers)
+        tts = LaneTTS(engine, args, rec) if args.tts_lane else SentenceTTS(engine, args, rec)
     text_ids = [[] for _ in turns]
     hiddens = []
     nxt, hid = engine.text_step([(t.kv, pre) for t in turns])
@@ -341,7 +414,7 @@ class LaneTTS:
         self.t.start()
         # the response's last sentence (submitted once the text decode is over) speaks on its own streams beside
         # the lane's remaining rows instead of joining them (two latency-bound steps on two streams overlap; r03v)
-        self.tail = SentenceTTS(engine, args, rec, 1, names=("tts2", "voc2"))
+        self.tail = SentenceTTS(engine, args, rec, names=("tts2", "voc2"))
 
     def submit(self, job, last=False):
         if last:
@@ -362,51 +435,40 @@ class SentenceTTS:
     thread, while the main thread keeps decoding text on the engine stream: a sentence's speech depends only
     on its own text tokens and hidden rows, and the text decode never reads the speech, so the ids and PCM
     are those of the reference's sequential loop (bin/inference.py:152-183, which pauses the text decode for
-    each sentence).  Sentences are spoken in order (one user's audio is a sequence)."""
+    each sentence).  Sentences are spoken in order (one user's audio is a sequence).  (Round 3's multi-worker
+    mode is gone: the continuously batched lane, LaneTTS, is the default and measured faster, r03zf/zh.)"""
 
-    def __init__(self, engine, args, rec, workers=1, names=None):
-        """workers > 1: sentence k goes to worker k % workers, each with its own streams, so a sentence's speech
-        does not queue behind the previous sentence's (the AR decode graphs and vocoder graphs are cached per
-        stream, fo/tts.py, fo/codec.py)."""
+    def __init__(self, engine, args, rec, names=("tts", "voc")):
         import queue
         import threading
         from fo import ops
         self.err = None
-        self.k = 0
-        self.qs, self.ts = [], []
-        for w in range(workers):
-            q = queue.Queue()
-            sfx = "" if w == 0 else str(w)
-            stream = ops.engine_stream(engine.device, name=names[0] if names else "tts" + sfx)
-            voc = ops.engine_stream(engine.device, name=names[1] if names else "voc" + sfx)
+        self.q = queue.Queue()
+        stream = ops.engine_stream(engine.device, name=names[0])
+        voc = ops.engine_stream(engine.device, name=names[1])
 
-            def work(q=q, stream=stream, voc=voc):
-                import torch
-                torch.cuda.set_device(engine.device)
-                while True:
-                    job = q.get()
-                    if job is None:
-                        return
-                    if self.err is None:
-                        try:
-                            run_sentence(engine, args, rec, *job, stream=stream, voc=voc)
-                        except BaseException as e:  # re-raised in the main thread by join()
-                            self.err = e
+        def work():
+            import torch
+            torch.cuda.set_device(engine.device)
+            while True:
+                job = self.q.get()
+                if job is None:
+                    return
+                if self.err is None:
+                    try:
+                        run_sentence(engine, args, rec, *job, stream=stream, voc=voc)
+                    except BaseException as e:  # re-raised in the main thread by join()
+                        self.err = e
 
-            t = threading.Thread(target=work, daemon=True)
-            t.start()
-            self.qs.append(q)
-            self.ts.append(t)
+        self.t = threading.Thread(target=work, daemon=True)
+        self.t.start()
 
     def submit(self, job, last=False):
-        self.qs[self.k % len(self.qs)].put(job)
-        self.k += 1
+        self.q.put(job)
 
     def join(self):
-        for q in self.qs:
-            q.put(None)
-        for t in self.ts:
-            t.join()
+        self.q.put(None)
+        self.t.join()
         if self.err is not None:
             raise self.err
 
@@ -641,17 +703,24 @@ def cpu_baseline(cfg_name, threads, text_tokens, sentence_tokens, codec_tokens):
     audio1 = codec_tokens * 600 / 24000.0
     n_voc = n_sent * len(vocoder_calls(codec_tokens // n_sent))
     turn2 = 63 * u1 + text_tokens * u2 + codec_tokens * u3 + n_voc * u4
-    return {"value": round(audio1 / config1, 4),
+    # the CPU path's best configuration on what the box grants: the faster of the measured thread counts
+    best_s, best_threads = config1, used
+    if config1_q is not None and config1_q < config1:
+        best_s, best_threads = config1_q, quota
+    return {"value": round(audio1 / best_s, 4),
             "unit": f"x real-time (config 1: 1 user, question.wav 2.0 s in, {audio1:.0f} s of speech out)",
-            "cores": used, "kind": "port",
+            "cores": best_threads, "kind": "port",
             "sample": (f"config 1 end to end on the numpy fp32 oracle (oracle/nets.py) at REAL geometry with distinct "
-                       f"weights per layer: {len(feats)} question.wav chunks (listen {t_listen:.2f} s), assistant prefix "
-                       f"+ {text_tokens} text tokens, {n_sent} sentences x {per[0]} codec tokens, {n_voc} vocoder calls"
-                       f" = {config1:.2f} s; {used} BLAS threads ({blas_lib}) within a cgroup quota of {cpu_quota()} "
-                       f"CPUs of {os.cpu_count()} ({cpu_model()})"),
-            "config1_s": round(config1, 3), "config1_listen_s": round(t_listen, 3),
-            "config1_s_at_quota_threads": None if config1_q is None else round(config1_q, 3),
-            "value_at_quota_threads": None if config1_q is None else round(audio1 / config1_q, 4),
+                       f"weights per layer: {len(feats)} question.wav chunks (listen {t_listen:.2f} s at {used} "
+                       f"threads), assistant prefix + {text_tokens} text tokens, {n_sent} sentences x {per[0]} codec "
+                       f"tokens, {n_voc} vocoder calls = {best_s:.2f} s at {best_threads} BLAS threads ({blas_lib}), "
+                       f"the faster of {used} threads ({config1:.2f} s)"
+                       + ("" if config1_q is None else f" and the cgroup quota's {quota} ({config1_q:.2f} s)")
+                       + f"; host {os.cpu_count()} CPUs ({cpu_model()}), cgroup quota {cpu_quota()} CPUs"),
+            "config1_s": round(best_s, 3), "config1_listen_s": round(t_listen, 3),
+            "threads_measured": {str(used): round(config1, 3),
+                                 **({} if config1_q is None else {str(quota): round(config1_q, 3)})},
+            "value_at_socket_threads": round(audio1 / config1, 4),
             "config2_rtf_from_units": round(10.0 / turn2, 4),
             "host_cpus": os.cpu_count(), "cpu_quota": cpu_quota(), "cpu_model": cpu_model(),
             "units_ms": {"U1": round(u1 * 1e3, 2), "U2": round(u2 * 1e3, 2), "U3": round(u3 * 1e3, 3),
@@ -803,6 +872,14 @@ def run_duplex(eng, args, seconds, sync):
     return {"wall": wall, "ticks": ticks, "counts": counts, "audio_s": args.users * n * ch / 16000.0}
 
 
+def topology(world):
+    """n_gpus = GPUs the job ran on: a FO_DIST_REHEARSAL run puts every rank on cuda:0, so it is one GPU (its ranks
+    are replicas sharing that GPU, not a scaling point)."""
+    rehearsal = os.environ.get("FO_DIST_REHEARSAL") == "1"
+    return {"n_gpus": 1 if rehearsal else world, "ranks": world, "physical_gpus": 1 if rehearsal else world,
+            "rehearsal": "one-GPU rehearsal: every rank on cuda:0 over gloo" if rehearsal else None}
+
+
 def main_duplex(args, eng, dev, dist, world, rank, load_s):
     import torch
 
@@ -830,7 +907,7 @@ def main_duplex(args, eng, dev, dist, world, rank, load_s):
             "metric": "duplex: real-time factor of two-party dialogue audio processed + p50 state-decision latency",
             "value": round(audio / wall, 3),
             "unit": "x real-time (seconds of per-session dialogue per wall second, all sessions)",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            **topology(world), "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16w-fp32a",
             "data": "synthetic (counter-hash weights; synthetic 16 kHz PCM for both parties; scripted VAD)",
@@ -854,6 +931,10 @@ def main_duplex(args, eng, dev, dist, world, rank, load_s):
 
 def main():
     args = parse()
+    launch(args)   # --gpus N > 1 without a launcher: spawns N ranks and exits with their code
+    if args.launch_selftest:
+        launch_selftest()
+        return
     if args.switch_interval:
         sys.setswitchinterval(args.switch_interval)
     import torch
@@ -862,7 +943,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     # FO_DIST_REHEARSAL=1: the N > 1 path (receive-only replicas, weight broadcast, result gathering) with
-    # every rank on cuda:0 over gloo -- a one-GPU rehearsal of what the 8-GPU run does over RCCL
+    # every rank on cuda:0 over gloo -- a one-GPU rehearsal of what the 8-GPU run does over RCCL; its line says
+    # physical_gpus 1 and n_gpus 1 (the ranks are replicas sharing one GPU, not a scaling point)
     rehearsal = os.environ.get("FO_DIST_REHEARSAL") == "1"
     if rehearsal:
         local = 0
@@ -945,8 +1027,8 @@ def main():
         a1 = s1["samples"][0] / 24000.0
         single = {"workload": "config 2: 1 user on 1 GPU, 10 s input, same turn",
                   "ms_per_turn": round(w1 * 1e3, 2), "value": round(a1 / w1, 3),
-                  "first_audio_ms": round((s1["first_pcm"][0] - s1["t_ss"]) * 1e3, 2),
-                  "first_emit_gated_ms": round((s1["first"][0] - s1["t_ss"]) * 1e3, 2),
+                  "first_audio_ms": round((s1["first"][0] - s1["t_ss"]) * 1e3, 2),
+                  "first_pcm_ms": round((s1["first_pcm"][0] - s1["t_ss"]) * 1e3, 2),
                   "rtf_per_user": round(a1 / (s1["last"][0] - s1["t_ss"]), 3)}
     probe = gemm_probe(eng, 2 * args.users)
     codec_ok, codec_n = codec_ids_check(eng)
@@ -980,7 +1062,7 @@ def main():
             "metric": "real-time factor + p50 first-audio-chunk latency, Qwen2-7B, N users/GPU",
             "value": round(audio / wall, 3),
             "unit": "x real-time (aggregate seconds of 24 kHz speech out per wall second)",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            **topology(world), "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16w-fp32a",
             "data": "synthetic (counter-hash weights at Qwen2-7B + paper geometry; synthetic 16 kHz PCM)",
@@ -995,9 +1077,12 @@ def main():
                        "model": f"Freeze-Omni ({args.config}): speech encoder + adapter + Qwen2-7B + AR decoder + "
                                 "TiCodec", "users_per_gpu": args.users, "global_users": args.users * world,
                        "parallelism": f"dp{world} (session-pinned replicas)"},
-            "p50_first_audio_ms": round(float(np.percentile(lat, 50)), 2) if lat else None,
-            "p90_first_audio_ms": round(float(np.percentile(lat, 90)), 2) if lat else None,
-            "p50_first_emit_gated_ms": round(float(np.percentile(lat_gated, 50)), 2) if lat_gated else None,
+            # first audio = the first segment llm2TTS.run yields, after find_min_sum_index's gate
+            # (models/decoder/llm2tts.py:141-153); first PCM = the first vocoder chunk on the host, before the gate
+            "p50_first_audio_ms": round(float(np.percentile(lat_gated, 50)), 2) if lat_gated else None,
+            "p90_first_audio_ms": round(float(np.percentile(lat_gated, 90)), 2) if lat_gated else None,
+            "p50_first_pcm_ms": round(float(np.percentile(lat, 50)), 2) if lat else None,
+            "p90_first_pcm_ms": round(float(np.percentile(lat, 90)), 2) if lat else None,
             "rtf_per_user_p50": round(float(np.percentile(rtf_user, 50)), 3) if rtf_user else None,
             "load_s": round(load_s, 2), "weight_broadcast_s": None if bcast_s is None else round(bcast_s, 3),
             "weight_broadcast_bytes": bcast_bytes, "weights_verified": weights_verified,

@@ -161,6 +161,10 @@ class DialogServer:
 
     def disconnect(self, sid):
         self.stop(sid)
+        with self.lock:   # a dropped task-manager connection frees the streams it registered for re-registration
+            for s in self.sessions.values():
+                if getattr(s, "tm_sid", None) == sid:
+                    s.tm_sid = None
         self.hub.unregister(sid)
 
     # ---------------------------------------------------------------- events
@@ -313,6 +317,10 @@ class DialogClient:
         raise TimeoutError(event)
 
     def close(self):
+        try:   # shutdown first: a makefile() reader keeps the descriptor open past close(), the peer would see no EOF
+            self.sock.shutdown(socket.SHUT_RDWR)
+        except OSError:
+            pass
         try:
             self.sock.close()
         except OSError:

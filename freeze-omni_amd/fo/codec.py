@@ -22,9 +22,11 @@ class CodecEngine:
         assert h["residul_layer"] == 1 and h["n_code_groups"] == 1, "single-codebook TiCodec only (the speech decoder emits one id per frame)"
         self.codebook = src.get("codec.quantizer.quantizer_modules.0.embedding.weight", torch.bfloat16)
         gt = h["global_tokens"]
-        parts = [src.get(f"codec.quantizer.quantizer_modules_globaltokens.{j}.embedding.weight")[t]
-                 for j, t in enumerate(gt)]
-        self.gfeat = torch.cat(parts).contiguous()  # [128] (embed_gst, models.py:703-715)
+        # embed_gst's tables (models.py:703-715), one per global token: row t of table j is that token's slice
+        self.gst_tables = [src.get(f"codec.quantizer.quantizer_modules_globaltokens.{j}.embedding.weight").contiguous()
+                           for j in range(len(gt))]
+        parts = [tab[t] for tab, t in zip(self.gst_tables, gt)]
+        self.gfeat = torch.cat(parts).contiguous()  # [128]: the configured voice (h.global_tokens), the default
         p = "codec.generator."
         g = lambda n, dt=F32: src.get(p + n, dt)  # noqa: E731
         self.U = h["upsample_initial_channel"]
@@ -190,8 +192,28 @@ class CodecEngine:
                                                  pre_leaky=0.1, res=src[j], oscale=1.0 / nk, gadd=gadd)
                                    for j in range(nk)], B, C, C, dev, summed=True)
 
-    def __call__(self, ids):
+    def global_feature(self, gst, B):
+        """embed_gst (models/decoder/ticodec/models.py:703-715) of per-call global style tokens: gst int [Bg, 1, n] or
+        [Bg, n] (VQVAE.encode's layout; Bg = B, or 1 broadcast over the batch) -> device fp32 [B, n * d], each row the
+        concatenation of table j's row gst[b, j] (fo_gather_rows per table into its column slice)."""
+        n, d = len(self.gst_tables), self.gst_tables[0].shape[1]
+        g = torch.as_tensor(gst).reshape(-1, n)
+        if g.shape[0] not in (1, B):
+            raise ValueError(f"global_style_token batch {g.shape[0]} does not match the codes' batch {B}")
+        hi = min(int(t.shape[0]) for t in self.gst_tables)
+        gh = g.cpu()
+        if int(gh.min()) < 0 or int(gh.max()) >= hi:   # nn.Embedding raises IndexError on such ids
+            raise IndexError(f"global style token out of range [0, {hi})")
+        idx = g.expand(B, n).to(self.device, I32).t().contiguous()   # [n][B]
+        out = torch.empty(B, n * d, dtype=F32, device=self.device)
+        for j, tab in enumerate(self.gst_tables):
+            ops.gather_rows(tab, idx[j], out=out[:, j * d:(j + 1) * d], D=d, M=B)
+        return out
+
+    def __call__(self, ids, gfeat=None):
         """ids: device int32 [B, T] codec token ids -> pcm [B, T*upsample] fp32 (tanh output).
+        gfeat: optional device fp32 [B, 128] global-style feature per row (global_feature(); None: the configured
+        h.global_tokens, as llm2TTS.run passes them).
         Channel-last activations [B][T][C]; every conv on the matrix cores (fo_conv_cl).  On a
         non-default stream the call is one hipGraph replay per (B, T) (captured on first use; the
         ~100 launches of a call otherwise cost more host time than the GPU work)."""
@@ -207,6 +229,13 @@ class CodecEngine:
             bf = self._buffers(B, T)
         self._graphs[key] = bf
         bf.ids.copy_(ids)
+        # the graph reads bf.g: per-call global features are copied in, the default restored after them
+        if gfeat is not None:
+            bf.g.copy_(gfeat)
+            bf.g_default = False
+        elif not getattr(bf, "g_default", True):
+            bf.g.copy_(self.gfeat.view(1, -1).expand(B, -1))
+            bf.g_default = True
         st = ops.stream(self.device)
         if not self.use_graphs or st in (0, None):
             self._run(bf)

@@ -22,7 +22,9 @@ class KVPool:
         self.ref = np.zeros(n_pages, dtype=np.int32)
         self.free = list(range(n_pages - 1, -1, -1))
         self.device = torch.device(device)
-        self.lock = threading.Lock()   # sequences of one pool may grow from several host threads (speech workers)
+        # sequences of one pool may grow, fork and free from several host threads (speech workers, server sessions):
+        # every refcount change goes through a method below, under this lock (numpy element updates are not atomic)
+        self.lock = threading.RLock()
 
     @property
     def bytes_per_token(self):
@@ -41,6 +43,32 @@ class KVPool:
             self.ref[p] -= 1
             if self.ref[p] == 0:
                 self.free.append(p)
+
+    def share(self, pages):
+        """One more holder of each page (fork / adopt)."""
+        with self.lock:
+            for p in pages:
+                if self.ref[p] <= 0:
+                    raise RuntimeError(f"KV page {p} shared after it was freed")
+                self.ref[p] += 1
+
+    def release_all(self, pages):
+        with self.lock:
+            for p in pages:
+                self.release(p)
+
+    def make_private(self, pg, keep):
+        """Copy-on-write of one page a sequence is about to write: if another sequence holds it too, returns a fresh
+        page (with the keys copied when keep) and drops this holder's reference; else returns pg.  The refcount check
+        and the alloc / release it decides happen under one lock hold, so a concurrent release cannot slip between."""
+        with self.lock:
+            if self.ref[pg] <= 1:
+                return pg
+            fresh = self.alloc()
+            if keep:
+                self.copy_page(pg, fresh)
+            self.release(pg)
+            return fresh
 
     def copy_page(self, src, dst):
         self.k[:, dst].copy_(self.k[:, src])
@@ -71,11 +99,8 @@ class KVSeq:
             last_pg = min(len(self.pages), (new_len + PS - 1) // PS)
             for li in range(first, last_pg):
                 pg = self.pages[li]
-                if self.pool.ref[pg] > 1:
-                    fresh = self.pool.alloc()
-                    if li * PS < self.length:   # holds live keys: keep them
-                        self.pool.copy_page(pg, fresh)
-                    self.pool.release(pg)
+                fresh = self.pool.make_private(pg, keep=li * PS < self.length)   # live keys on it: kept
+                if fresh != pg:
                     self.pages[li] = fresh
                     self.version += 1
         while len(self.pages) * PS < new_len:
@@ -93,8 +118,7 @@ class KVSeq:
         used = (self.length + self.pool.PS - 1) // self.pool.PS
         n.pages = list(self.pages[:used])
         n.length = self.length
-        for p in n.pages:
-            self.pool.ref[p] += 1
+        self.pool.share(n.pages)
         n.origin = (tuple(n.pages), n.length)
         return n
 
@@ -113,9 +137,9 @@ class KVSeq:
         """Become a copy-on-write fork of `other` (this sequence's own pages are released)."""
         self.free()
         used = (other.length + self.pool.PS - 1) // self.pool.PS
-        self.pages = list(other.pages[:used])
-        for p in self.pages:
-            self.pool.ref[p] += 1
+        pages = list(other.pages[:used])
+        self.pool.share(pages)
+        self.pages = pages
         self.length = other.length
         self.version += 1
         self.origin = None
@@ -123,16 +147,14 @@ class KVSeq:
     def truncate(self, new_len):
         PS = self.pool.PS
         keep = (new_len + PS - 1) // PS
-        for p in self.pages[keep:]:
-            self.pool.release(p)
+        self.pool.release_all(self.pages[keep:])
         if keep < len(self.pages):
             self.version += 1
         self.pages = self.pages[:keep]
         self.length = new_len
 
     def free(self):
-        for p in self.pages:
-            self.pool.release(p)
+        self.pool.release_all(self.pages)
         self.pages = []
         self.length = 0
         self.version += 1

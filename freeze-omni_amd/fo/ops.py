@@ -4,6 +4,8 @@ torch is used only for device memory and the current stream (plumbing); every co
 below is a hand-written gfx950 kernel in libfo_hip.so.
 """
 import os
+import threading
+
 import torch
 
 from . import _lib
@@ -612,15 +614,21 @@ class SampleCheck:
 
 
 _CHECKS = {}
+_CHECKS_LOCK = threading.Lock()
 
 
 def sample_check(device):
-    """The default SampleCheck of a device (used when a sampler call passes none)."""
+    """The default SampleCheck of a device FOR THE CALLING THREAD (used when a sampler call passes none).  Keyed by
+    (device, thread): the eager text step, AudioLLM._post_decode, LLM2TTSCodecAR.infer and speak's eager loop may run
+    on several host threads (speech workers, server sessions), and a NaN row drawn by one thread must raise in that
+    thread's check, not in another's (check() clears the word on read)."""
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
-    if idx not in _CHECKS:
-        _CHECKS[idx] = SampleCheck()
-    return _CHECKS[idx]
+    key = (idx, threading.get_ident())
+    with _CHECKS_LOCK:
+        if key not in _CHECKS:
+            _CHECKS[key] = SampleCheck()
+        return _CHECKS[key]
 
 
 def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None,

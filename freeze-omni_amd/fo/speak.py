@@ -302,11 +302,10 @@ class SpeechLane:
         self.forced = None
         self.res = torch.empty(2, dtype=F32, device=engine.device)
         self.done_groups = []       # tags whose rows are all finished and vocoded (drained by the caller)
-        self._held = []             # segments produced outside pump()
 
     @property
     def idle(self):
-        return not self.live and not self.pending and not self.joining and not self._held
+        return not self.live and not self.pending and not self.joining
 
     def add(self, items, max_tokens, min_tokens=0, tag=None):
         """Prefill a group of sessions (items as speak()) on the prefill stream; the group joins the decode once
@@ -334,14 +333,16 @@ class SpeechLane:
     def pump(self):
         """Join the groups whose prefill is done, launch ahead while the window has room, then read the oldest
         launched step back.  Returns the PCM segments that became available: [(row id, pcm device 1-D)]."""
-        segs, self._held = self._held, []
+        segs = []
         with torch.cuda.stream(self.es):
             if self.joining:
                 ready = [j for j in self.joining if j[1].query()]
                 if not ready and not self.live and not self.pending:
                     ready = self.joining[:1]   # nothing else to do: wait for the first group's prefill on the device
                 if ready:
-                    self._join(ready)
+                    # segments a join drains are returned by this pump, before _close_groups() below can report
+                    # their group done (ADVICE r03: they were held for the next pump)
+                    segs += self._join(ready)
             window = self.JOIN_WINDOW if self.joining else self.window
             while self.live and len(self.pending) < window:
                 if any(self.states[i].launched >= self.states[i].max_tokens for i in self.live):
@@ -390,7 +391,8 @@ class SpeechLane:
         return tts.decode_graph(len(rows), V, self.top_k, self.seed, max_keys, hist, None, True)
 
     def _join(self, ready):
-        """The ready groups join the batch between two steps (on the lane stream, after their prefill)."""
+        """The ready groups join the batch between two steps (on the lane stream, after their prefill).  Returns the
+        segments of the steps it had to drain."""
         tts = self.engine.tts
         new = []
         for rows, ev in ready:
@@ -400,10 +402,10 @@ class SpeechLane:
         if self.g is None or not self.live or self._busy(len(self.live) + len(new)):
             # no device state to carry over (or the larger graph still has steps in flight): read everything
             # launched, then the next launch rebuilds from the host ids
-            self._held += self._drain()
+            segs = self._drain()
             self.live += new
             self.g = None
-            return
+            return segs
         old, B0 = self.g, len(self.live)
         rows = self.live + new
         g = self._graph(rows)
@@ -417,6 +419,7 @@ class SpeechLane:
         ops.rmsnorm(g.x[B0:], tts.main.layers[0].ln1, tts.eps, out=g.ws["h"][B0:], M=len(new))
         g._uploaded = None
         self.g, self.live = g, rows
+        return []
 
     def _launch(self):
         g, rows = self.g, self.live

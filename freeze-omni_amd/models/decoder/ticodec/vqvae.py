@@ -1,5 +1,6 @@
 """VQVAE facade (reference: models/decoder/ticodec/vqvae.py:37-57): forward(codes [B, T, 1], global
-tokens) -> [B, 1, T*600] PCM through fo.codec.CodecEngine (the engine's configured global tokens);
+tokens [B or 1, 1, n]) -> [B, 1, T*600] PCM through fo.codec.CodecEngine, the global tokens embedded per call and
+per row (embed_gst, models.py:703-715) -- the configured h.global_tokens when the caller passes None;
 encode(wav [B, T]) -> (local tokens [B, T', L*G], global tokens [B, 1, n]) through
 fo.codec.CodecEncoderEngine when the facade was built with one (the reference's with_encoder=True)."""
 import torch
@@ -13,7 +14,12 @@ class VQVAE:
 
     def __call__(self, x, global_style_token=None):
         ids = torch.as_tensor(x).reshape(x.shape[0], -1).to(self.engine.device, torch.int32)
-        return self.engine(ids).unsqueeze(1)
+        g = None
+        if global_style_token is not None:
+            gt = torch.as_tensor(global_style_token)
+            if gt.reshape(-1).tolist() != list(self.h.global_tokens):   # the configured voice: the engine's default
+                g = self.engine.global_feature(gt, ids.shape[0])
+        return self.engine(ids, g).unsqueeze(1)
 
     def encode(self, x):
         if self.encoder is None:

@@ -1,0 +1,70 @@
+# One parameterised GPU call (replaces the per-call scripts of rounds 1-3).
+#   usage: bash scripts/gpu_call.sh <tag> <step> [<step> ...]
+# Steps run in order, each under its own time limit, and the call stops at the first failing step (no GPU step is
+# started after a fault, abort or time-out). Outputs go to gpurun_out/<tag>_*.
+#   tests      pytest -m gpu (PYTEST_K=expr narrows it)
+#   smoke      __graft_entry__.smoke()
+#   bench      the default bench line (cpu_baseline + config-2 leg)      -> <tag>_bench.json
+#   quick      bench without the CPU baseline / config-2 leg, 3 turns    -> <tag>_quick.json
+#   prof       rocprofv3 --kernel-trace --stats of the bench (2 turns)   -> <tag>_prof/
+#   fetch      FETCH_SIZE pass on the dominant kernel                    -> <tag>_pmc/
+#   tts        rocprofv3 kernel stats of the AR decode step alone        -> <tag>_prof_tts/
+#   text       rocprofv3 kernel stats of the text step alone             -> <tag>_prof_text/
+#   duplex     the config-5 duplex line                                  -> <tag>_duplex.json
+#   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
+#   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
+#   ab         ENV_A / ENV_B (e.g. 'FO_X=0') alternated twice on the quick bench -> <tag>_ab.txt
+#   py:<script args>   any scripts/ probe, e.g. 'py:llm_stage_time.py' (200 s limit)
+set -o pipefail
+R=$1; shift
+ROOTD=$GRAFT_REPO_ROOT
+cd $ROOTD; mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out/${R}
+line() {   # the JSON line's headline fields
+  grep '^{' "$1" | tail -1 | python -c "
+import json,sys
+d=json.loads(sys.stdin.read()); print(d.get('value'), d.get('ms_per_step'), d.get('p50_first_audio_ms'), d.get('p50_decision_ms'),
+ {k: round(v,1) for k, v in (d.get('stage_ms') or {}).items() if k in ('listen','text','speak_after_text')})"
+}
+for S in "$@"; do
+  echo "== step $S" >&2
+  case $S in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+             ${PYTEST_K:+-k "$PYTEST_K"} > ${O}_pytest_gpu.log 2>&1; rc=$?; tail -3 ${O}_pytest_gpu.log ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > ${O}_smoke.log 2>&1
+           rc=$?; tail -1 ${O}_smoke.log ;;
+    bench) timeout -k 10 900 python -u bench.py --out ${O}_bench.json > ${O}_bench.log 2>&1; rc=$?
+           [ $rc -eq 0 ] && line ${O}_bench.log ;;
+    quick) timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-single-user --steps 3 --out ${O}_quick.json \
+             > ${O}_quick.log 2>&1; rc=$?; [ $rc -eq 0 ] && line ${O}_quick.log ;;
+    prof)  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof -o bench -f csv -- \
+             python3 $ROOTD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-single-user) > ${O}_prof.log 2>&1; rc=$? ;;
+    fetch) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gemm_xs -d $ROOTD/${O}_pmc \
+             -o fetch -f csv -- python3 $ROOTD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-single-user) \
+             > ${O}_pmc.log 2>&1; rc=$? ;;
+    tts)   (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_tts -o tts -f csv -- \
+             python3 $ROOTD/scripts/tts_step_time.py 8 multi) > ${O}_prof_tts.log 2>&1; rc=$? ;;
+    text)  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_text -o text -f csv -- \
+             python3 $ROOTD/scripts/text_step_time.py) > ${O}_prof_text.log 2>&1; rc=$? ;;
+    duplex) timeout -k 10 400 python -u bench.py --scenario duplex --out ${O}_duplex.json > ${O}_duplex.log 2>&1; rc=$?
+            [ $rc -eq 0 ] && line ${O}_duplex.log ;;
+    rehearsal) FO_DIST_REHEARSAL=1 timeout -k 10 600 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu-baseline \
+             --no-single-user --out ${O}_rehearsal_n2.json > ${O}_rehearsal_n2.log 2>&1; rc=$? ;;
+    n2guard) timeout -k 10 120 python -u bench.py --gpus 2 --steps 1 > ${O}_n2guard.log 2>&1; rc=$?
+             if [ $rc -eq 2 ] && grep -q refusing ${O}_n2guard.log; then echo "n2guard ok: $(tail -1 ${O}_n2guard.log)"; rc=0
+             else echo "n2guard: expected a refusal, got rc $rc"; tail -5 ${O}_n2guard.log; [ $rc -eq 0 ] && rc=1; fi ;;
+    ab)    : > ${O}_ab.txt
+           for i in 1 2; do for AB in A B; do
+             E=ENV_$AB; timeout -k 10 300 env ${!E} python -u bench.py --no-cpu-baseline --no-single-user --steps 3 \
+               > ${O}_ab_$AB$i.log 2>&1 || { rc=$?; tail -20 ${O}_ab_$AB$i.log; break 2; }
+             echo "$AB$i [${!E}] $(line ${O}_ab_$AB$i.log)" >> ${O}_ab.txt; rc=0
+           done; done; cat ${O}_ab.txt ;;
+    py:*)  timeout -k 10 200 python -u scripts/${S#py:} > ${O}_$(basename ${S#py:} .py | cut -d' ' -f1).log 2>&1; rc=$?
+           tail -40 ${O}_$(basename ${S#py:} .py | cut -d' ' -f1).log ;;
+    *) echo "unknown step $S"; rc=1 ;;
+  esac
+  echo "step $S rc $rc" >&2
+  [ $rc -eq 0 ] || { echo "EXIT $rc at $S"; exit $rc; }
+done
+echo "EXIT 0"

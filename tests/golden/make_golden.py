@@ -910,6 +910,36 @@ def gold_codec(cfg, tts_model):
     np.savez_compressed(os.path.join(HERE, "silence_cut.npz"), **cases)
 
 
+def gold_codec_gst(cfg):
+    """VQVAE.forward with NON-default global style tokens (models/decoder/ticodec/vqvae.py:37-42, embed_gst
+    models.py:703-715): three rows each with its own global tokens ([3, 1, n], as VQVAE.encode returns them), and a
+    [1, 1, n] token broadcast over two rows.  Same tiny codec weights as codec_tiny.npz (the config seed)."""
+    from models.decoder.ticodec.models import Generator, Quantizer
+    from models.decoder.ticodec.vqvae import VQVAE, AttrDict
+    h = AttrDict(cfg["codec_json"])
+    vq = VQVAE.__new__(VQVAE)
+    torch.nn.Module.__init__(vq)
+    vq.h = h
+    vq.quantizer = Quantizer(h)
+    vq.generator = Generator(h)
+    vq.generator.remove_weight_norm()
+    init_module(vq.quantizer, cfg["seed"], "codec.quantizer.")
+    init_module(vq.generator, cfg["seed"], "codec.generator.")
+    vq.eval()
+    rng = np.random.default_rng(23)
+    n = h.global_code_num
+    ids = torch.from_numpy(rng.integers(0, h.n_codes, size=(3, 24, 1)))
+    gst = torch.from_numpy(rng.integers(0, h.n_codes, size=(3, 1, n)))
+    gst[0, 0] = torch.tensor(h.global_tokens)          # row 0: the default tokens
+    with torch.no_grad():
+        pcm = vq(ids, gst)
+        gst1 = torch.from_numpy(rng.integers(0, h.n_codes, size=(1, 1, n)))
+        pcm_b = vq(ids[:2], gst1)                      # one token set broadcast over the batch
+    np.savez_compressed(os.path.join(HERE, "codec_gst_tiny.npz"), ids=ids[..., 0].numpy(), gst=gst.numpy(),
+                        pcm=pcm[:, 0].numpy(), gst_b=gst1.numpy(), pcm_b=pcm_b[:, 0].numpy())
+    print("codec gst: pcm", tuple(pcm.shape), "gst", gst[:, 0].tolist(), "broadcast", gst1[0, 0].tolist())
+
+
 def gold_text():
     sys.argv = ["golden"]
     from models.pipeline import inferencePipeline
@@ -949,6 +979,7 @@ def main():
     gold_real_t2()
     gold_real_qwen2()
     gold_adapter_variants(cfg["seed"])
+    gold_codec_gst(cfg)
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
         json.dump(SHAPES, f)
     total = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith((".npz", ".json")))
@@ -974,6 +1005,9 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["real_t2"]:
         install_shims()
         gold_real_t2()
+    elif sys.argv[1:] == ["codec_gst"]:
+        install_shims()
+        gold_codec_gst(C.get("tiny"))
     elif sys.argv[1:] == ["real_qwen2"]:
         install_shims()
         gold_real_qwen2()

@@ -168,6 +168,29 @@ def test_codec_matches_golden(dev, src, W):
     close(pcm[1], nets.Codec(W, CFG)(g["ids"][::-1]), atol=5e-5)
 
 
+def test_vqvae_global_style_tokens_match_reference(dev, src):
+    """VQVAE.__call__ embeds the global style tokens passed on each call, per row (reference vqvae.py:37-42,
+    embed_gst models.py:703-715): three rows with their own tokens, one token set broadcast over two rows, and the
+    configured tokens (None, as llm2TTS.run's default) unchanged.  Golden: codec_gst_tiny.npz, the reference's own
+    VQVAE.forward (make_golden.py codec_gst).  Tolerance 1e-4 abs (fp32 PCM)."""
+    from fo.codec import CodecEngine
+    from models.decoder.ticodec.vqvae import VQVAE
+    g = np.load(os.path.join(G, "codec_gst_tiny.npz"))
+    eng = CodecEngine(src, CFG["codec_json"], dev)
+    vq = VQVAE(eng)
+    ids = torch.from_numpy(g["ids"]).unsqueeze(-1)
+    pcm = vq(ids, torch.from_numpy(g["gst"]))
+    assert pcm.shape == (3, 1, g["pcm"].shape[1])
+    close(pcm[:, 0], g["pcm"], atol=1e-4)
+    close(vq(ids[:2], torch.from_numpy(g["gst_b"]))[:, 0], g["pcm_b"], atol=1e-4)
+    # row 0 holds the configured tokens: the default path (no tokens) reproduces it, after a custom call on the
+    # same cached (B, T) buffers
+    close(vq(ids[:1], None)[0, 0], g["pcm"][0], atol=1e-4)
+    close(vq(ids, torch.from_numpy(g["gst"]))[:, 0], g["pcm"], atol=1e-4)
+    with pytest.raises(IndexError):
+        vq(ids, torch.full((3, 1, g["gst"].shape[-1]), 10 ** 6))
+
+
 def test_silence_cut_kernel_matches_golden(dev):
     from fo import ops
     g = np.load(os.path.join(G, "silence_cut.npz"))

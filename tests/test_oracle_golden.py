@@ -141,6 +141,14 @@ def test_codec_matches_golden(W):
     np.testing.assert_allclose(pcm, g["pcm"], atol=2e-5, rtol=1e-3)
 
 
+def test_codec_global_style_tokens_match_golden(W):
+    """embed_gst with per-row, non-default global tokens (codec_gst_tiny.npz, make_golden.py codec_gst)."""
+    g = load("codec_gst_tiny.npz")
+    for b in range(3):
+        np.testing.assert_allclose(nets.Codec(W, CFG)(g["ids"][b], g["gst"][b, 0]), g["pcm"][b], atol=2e-5, rtol=1e-3)
+    np.testing.assert_allclose(nets.Codec(W, CFG)(g["ids"][1], g["gst_b"][0, 0]), g["pcm_b"][1], atol=2e-5, rtol=1e-3)
+
+
 def test_silence_cut_matches_golden():
     g = load("silence_cut.npz")
     for ci in range(4):

@@ -122,6 +122,34 @@ def test_server_streams_session_events_and_tm_chunks():
         _close(srv, dialog)
 
 
+def test_task_manager_reregisters_after_its_connection_drops():
+    import time
+
+    from bin.server import DialogClient
+
+    srv, dialog, _ = _serve()
+    host, port = srv.server_address
+    c = DialogClient(host, port)
+    try:
+        c.send("start", {})
+        st = c.wait("started")
+        tm = DialogClient(host, port)
+        tm.send("register_tm", {"sid": c.sid, "token": st["token"]})
+        assert tm.wait("registered")["sid"] == c.sid
+        tm.close()   # the task manager's connection drops: its registration goes with it
+        deadline = time.monotonic() + 10
+        while getattr(dialog.sessions[c.sid], "tm_sid", None) is not None and time.monotonic() < deadline:
+            time.sleep(0.01)
+        assert dialog.sessions[c.sid].tm_sid is None
+        tm2 = DialogClient(host, port)
+        tm2.send("register_tm", {"sid": c.sid, "token": st["token"]})
+        assert tm2.wait("registered")["sid"] == c.sid
+        tm2.close()
+    finally:
+        c.close()
+        _close(srv, dialog)
+
+
 def test_server_max_users_errors_and_timeout():
     from bin.server import DialogClient
 
