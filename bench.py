@@ -22,6 +22,7 @@ device; no checkpoint is on the box.  `--gpus N` (N > 1) starts N ranks itself (
 per GPU, RCCL); under an outer torch.distributed.run each process is one rank and --gpus must equal WORLD_SIZE.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -823,7 +824,7 @@ def duplex_plan(seconds, offset, speech=3.0, silence=1.5, answer=3.75):
     return user, system
 
 
-def run_duplex(eng, args, seconds, sync):
+def run_duplex(eng, args, seconds, sync, probe=False):
     """Config 5 on one replica: args.users duplex sessions (framing B, 224 ms chunks) with scripted VAD,
     system audio re-encoded and prefilled, user barge-in; all sessions' chunks per tick in one batched
     prefill (fo.duplex.DuplexScheduler).  Returns per-tick wall times and counts."""
@@ -848,6 +849,8 @@ def run_duplex(eng, args, seconds, sync):
             counts[d["identity"]] += 1
             counts["dialog_ss"] += st == "dialog_ss"
 
+    from fo import _lib
+    stages = []   # per tick: host gating ms + GPU spans of the batched prefill (engine stage probe)
     t_all = time.perf_counter()
     for k in range(n):
         # chunk k of both parties arrives for every session; the tick that follows carries the VAD,
@@ -857,8 +860,31 @@ def run_duplex(eng, args, seconds, sync):
             for ident in ("user", "system"):
                 s.enqueue_audio_data(ident, {"audio": chunks[u][k][ident], "sr": 16000, "enc": "s16le",
                                              "time_stamp": k * ch / 16000.0})
+        if probe:
+            for s in sch.sessions:   # the host stages of tick() (VAD, gating + fbank, serialisation), timed apart
+                s.pump()
+            t_host = time.perf_counter()
+            eng.stage_probe = []
         done = sch.tick()
         ticks.append(time.perf_counter() - t)
+        if probe:
+            marks, eng.stage_probe = eng.stage_probe, None
+            st = {"host_gating": (t_host - t) * 1e3, "items": len(done), "tick": ticks[-1] * 1e3}
+            # algorithmic bytes of the tick (DESIGN §5 U1 at framing B): each identity's encoder + adapter weights
+            # once, the Qwen2 layers once, every prefilled session's KV read
+            llm = eng.llm
+            kv_tok = llm.stack.n * llm.KVH * llm.hd * 2 * 4
+            idents = {d["identity"] for _, d, _ in done}
+            st["bytes"] = (sum(eng.enc[i].weight_bytes + eng.ada[i].weight_bytes for i in idents) +
+                           llm.stack.weight_bytes + sum(ss.past_key_values.length for ss, _, _ in done) * kv_tok)
+            for (a, ea), (b, eb) in zip(marks, marks[1:]):
+                ms = ctypes.c_float()
+                _lib.call("fo_event_elapsed_ms", ea, eb, ctypes.byref(ms))
+                st[b] = st.get(b, 0.0) + ms.value
+            for _, e in marks:
+                _lib.call("fo_event_destroy", e)
+            if marks:
+                stages.append(st)
         account(done)
     while True:   # features still queued behind the last chunk
         done = sch.tick()
@@ -869,7 +895,8 @@ def run_duplex(eng, args, seconds, sync):
     wall = time.perf_counter() - t_all
     for s in sch.sessions:
         s.release()
-    return {"wall": wall, "ticks": ticks, "counts": counts, "audio_s": args.users * n * ch / 16000.0}
+    return {"wall": wall, "ticks": ticks, "counts": counts, "audio_s": args.users * n * ch / 16000.0,
+            "stages": stages}
 
 
 def topology(world):
@@ -878,6 +905,36 @@ def topology(world):
     rehearsal = os.environ.get("FO_DIST_REHEARSAL") == "1"
     return {"n_gpus": 1 if rehearsal else world, "ranks": world, "physical_gpus": 1 if rehearsal else world,
             "rehearsal": "one-GPU rehearsal: every rank on cuda:0 over gloo" if rehearsal else None}
+
+
+def duplex_stage_split(pr):
+    """Median per tick of the probed run, over the ticks that prefilled something: host gating (VAD, fbank, gating,
+    serialisation), each identity's encoder + adapter, the LLM input gather, the Qwen2 layers, the state head, and
+    the tick's wall time; p50 over the ticks that ran each stage."""
+    if not pr:
+        return None
+    keys = sorted({k for st in pr for k in st if k not in ("items", "bytes")})
+    out = {k: round(float(np.median([st[k] for st in pr if k in st])), 3) for k in keys}
+    out["ticks_probed"] = len(pr)
+    out["items_p50"] = float(np.median([st["items"] for st in pr]))
+    return out
+
+
+def duplex_roofline(pr, eng, bw=8.0e12):
+    """The tick against its own bound (config 5): algorithmic bytes of the tick (encoder + adapter
+    weights per identity present, Qwen2 layers, KV read) / 8 TB/s vs the tick's wall time, median over probed ticks."""
+    if not pr:
+        return None
+    fr = [st["bytes"] / bw * 1e3 / st["tick"] for st in pr]
+    gpu = [st["bytes"] / bw * 1e3 / max(1e-6, sum(v for k, v in st.items() if k in
+                                                    ("encoder_user", "encoder_system", "gather", "qwen2", "state_head")))
+           for st in pr]
+    b = float(np.median([st["bytes"] for st in pr]))
+    return {"bound": "hbm", "unit": "GB/s", "peak": 8000.0,
+            "achieved": round(b / (float(np.median([st["tick"] for st in pr])) * 1e-3) / 1e9, 1),
+            "frac": round(float(np.median(fr)), 4), "frac_gpu_spans": round(float(np.median(gpu)), 4),
+            "tick_bytes_p50": round(b), "tick_roofline_ms": round(b / bw * 1e3, 3), "traffic": None,
+            "source": "untimed probed run of the same script (engine stage probe); frac = roofline ms / tick wall ms"}
 
 
 def main_duplex(args, eng, dev, dist, world, rank, load_s):
@@ -891,6 +948,9 @@ def main_duplex(args, eng, dev, dist, world, rank, load_s):
     if dist is not None:
         dist.barrier()
     runs = [run_duplex(eng, args, args.duplex_sec, sync) for _ in range(args.steps)]
+    # untimed: the same script with the per-tick stage probe (HIP events on the engine stream, host gating timed
+    # apart) -- the split and the tick roofline come from here, the headline numbers from the runs above
+    pr = run_duplex(eng, args, min(args.duplex_sec, 30.0), sync, probe=True)["stages"]
     wall = sum(r["wall"] for r in runs)
     audio = sum(r["audio_s"] for r in runs)
     ticks = [t * 1e3 for r in runs for t in r["ticks"]]
@@ -920,7 +980,9 @@ def main_duplex(args, eng, dev, dist, world, rank, load_s):
             "chunk_period_ms": 224.0,
             "ticks": len(runs[-1]["ticks"]), "user_chunks": c["user"], "system_chunks": c["system"],
             "dialog_ss": c["dialog_ss"], "load_s": round(load_s, 2),
-            "roofline": None, "cpu_baseline": None,
+            "roofline": duplex_roofline(pr, eng),
+            "tick_stage_ms": duplex_stage_split(pr),
+            "cpu_baseline": None,
         }
         s = json.dumps(line)
         print(s, flush=True)

@@ -877,6 +877,113 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
   }
 }
 
+// X-stationary weight stream for 17..64 fp32 rows (RB = 2..4 row blocks): k_gemm_xs's design with the K range
+// split over workgroups, because RB row blocks of X split into bf16 hi + lo no longer fit one CU for the whole K
+// (16 rows x 3584 x 4 B = 229 KB per row block).  Split s owns k-steps [s * NW * KPW, (s + 1) * NW * KPW); wave w
+// of it KPW of them, whose X fragments of all RB row blocks it loads once (hi in VGPRs, lo in its LDS region).
+// Units are packed tile pairs (a gate/up pair, or two adjacent plain / RoPE tiles), double buffered as in
+// k_gemm_xs; per unit the NW partial tiles are reduced through LDS and stored as split s's partial slab, and
+// k_gemm_reduce (the next launch) sums the slabs in split order and runs the epilogue (SwiGLU, RMSNorm rstd,
+// RoPE + paged-KV append, residual, row statistics).  k-steps past K (the last split of a long-K layer) load
+// nothing and multiply zero X.
+template <int NW, int KPW, int RB>
+__global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
+  __shared__ bf16x8 xlo[NW][RB][KPW][64];
+  __shared__ float part[NW][2][RB * 16][17];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int KW = NW * KPW;
+  constexpr int ROWS = RB * 16;
+  const int KS = a.K >> 5;
+  const int sp = blockIdx.y;
+  const int ub = (int)((long)units * blockIdx.x / gridDim.x);
+  const int ue = (int)((long)units * (blockIdx.x + 1) / gridDim.x);
+  const int ks0 = sp * KW + wave * KPW;                 // this wave's first k-step
+  const int nj = max(0, min(KPW, KS - ks0));            // its k-steps inside K (wave-uniform)
+  const unsigned long long wbase = (unsigned long long)a.Wp;
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(wbase >> 32)) << 32) |
+                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)wbase)),
+      (short)0, __builtin_amdgcn_readfirstlane(a.ntiles * KS * 1024), 0x00020000);
+  const int voff = (ks0 * 64 + lane) * 16;
+  bf16x8 w0[KPW], w1[KPW];
+  auto issue = [&](bf16x8 (&w)[KPW], int tile) {
+#pragma unroll
+    for (int j = 0; j < KPW; ++j)
+      if (j < nj)
+        w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024, 2));
+  };
+  issue(w0, ub < ue ? 2 * ub : a.ntiles);
+  issue(w1, ub < ue ? 2 * ub + 1 : a.ntiles);
+  bf16x8 xh[RB][KPW];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int row = min(r * 16 + (lane & 15), a.M - 1);   // rows >= M: computed, never stored by the reduce
+    const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4) + (size_t)ks0 * 32;
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      bf16x8 hi, lo;
+      if (j < nj) {
+        const float4 p0 = reinterpret_cast<const float4*>(xp + j * 32)[0];
+        const float4 p1 = reinterpret_cast<const float4*>(xp + j * 32)[1];
+        const float f[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const __bf16 h = (__bf16)f[i];
+          hi[i] = h;
+          lo[i] = (__bf16)(f[i] - (float)h);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          hi[i] = (__bf16)0.f;
+          lo[i] = (__bf16)0.f;
+        }
+        w0[j] = hi;   // k-steps past K: no weights loaded, zero fragments
+        w1[j] = hi;
+      }
+      xh[r][j] = hi;
+      xlo[wave][r][j][lane] = lo;
+    }
+  }
+  auto compute = [&](bf16x8 (&w)[KPW], f32x4 (&acc)[RB]) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KPW; ++j)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[r][j], w[j], acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xlo[wave][r][j][lane], w[j], acc[r], 0, 0, 0);
+      }
+  };
+  const int Ncols = a.ntiles * 16;
+  float* slab = a.ws + (size_t)sp * ROWS * Ncols;
+  for (int u = ub; u < ue; ++u) {
+    const int nxt = u + 1 < ue ? 2 * (u + 1) : a.ntiles;
+    f32x4 c0[RB], c1[RB];
+    compute(w0, c0);
+    issue(w0, nxt);
+    compute(w1, c1);
+    issue(w1, nxt + (u + 1 < ue ? 1 : 0));
+    __syncthreads();  // the previous unit's reduction has read part[]
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        part[wave][0][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c0[r][i];
+        part[wave][1][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c1[r][i];
+      }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * ROWS * 16; e += NW * 64) {
+      const int t = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += part[w][t][rr][c];
+      slab[(size_t)rr * Ncols + (2 * u + t) * 16 + c] = v;
+    }
+  }
+}
+
 // in-launch split-K merge: 0 off, 1 every eligible split, 2 (default) splits of small weights only -- measured
 // (profiles/r02t_*): the TTS down (8.7 MB) 184.8 -> 181.5 us per AR step, the Qwen2 down (136 MB) slower
 // (LLM stage 3313 -> 3340 us: every one of its 224 workgroups drains write-through partials before exiting),
@@ -898,6 +1005,14 @@ inline bool xs_mode() {
     g_xs = (e && e[0] == '0') ? 0 : 1;
   }
   return g_xs == 1;
+}
+int g_xsk = -1;  // X-stationary split-K kernel for eligible 17..64-row GEMMs: -1 = FO_GEMM_XSK (default on)
+inline bool xsk_mode() {
+  if (g_xsk < 0) {
+    const char* e = getenv("FO_GEMM_XSK");
+    g_xsk = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_xsk == 1;
 }
 // K split of the 8-tile long-K weight stream (Qwen2 down: 28 column groups x S workgroups); -1 = FO_DOWN_S
 // (4-16) decides at first use, default 8 (224 workgroups)
@@ -1085,6 +1200,33 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (sout) FO_REQUIRE(!swiglu && !rope, "fo_gemm: statistics with a paired epilogue");
     hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
     return fo::check_launch("fo_gemm/xs");
+  }
+  // 17..64 rows on large weights (duplex ticks: 8 sessions x 4 framing-B tokens, the assistant prefix 8 x 5, prefixed
+  // first chunks): the X-stationary stream with K split over workgroups (k_gemm_xsk) + k_gemm_reduce
+  const bool big_w0 = (long long)a.ntiles * 16 * K >= (8ll << 20);
+  if (x_f32 && M > 16 && M <= 64 && !lnw && (a.ntiles % 2) == 0 && splitk <= 1 && xsk_mode() && !g_force_nt &&
+      !g_force_nw && big_w0 && ldx % 4 == 0 && !sout1 && (K >> 5) >= ((M + 15) / 16 == 2 ? 56 : 28)) {
+    const int RBk = (M + 15) / 16;
+    const int NWk = RBk == 2 ? 8 : 4, KPWk = 7;   // every split has work: K >= NW * KPW k-steps
+    const int KSk = K >> 5;
+    const int S = (KSk + NWk * KPWk - 1) / (NWk * KPWk);
+    const int units = a.ntiles / 2;
+    const int per_split = max(1, num_cus() / S);
+    const int per = (units + per_split - 1) / per_split;
+    const int G = (units + per - 1) / per;
+    const long long need = (long long)S * RBk * 16 * a.ntiles * 16;
+    FO_REQUIRE(ws && need <= ws_floats, "fo_gemm/xsk: split-K workspace too small (%lld > %lld)", need, ws_floats);
+    a.S = S;
+    a.counters = nullptr;
+    if (sgroups) *sgroups = (N + 255) / 256;
+    dim3 grid(G, S);
+    if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2>), grid, dim3(512), 0, stream, a, units);
+    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<4, 7, 3>), grid, dim3(256), 0, stream, a, units);
+    else hipLaunchKernelGGL((k_gemm_xsk<4, 7, 4>), grid, dim3(256), 0, stream, a, units);
+    int rc = fo::check_launch("fo_gemm/xsk");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, RBk * 16);
+    return fo::check_launch("fo_gemm/xsk reduce");
   }
   // mid-size row counts on large weights (the Qwen2 prefills of a turn: assistant prefix, the first
   // chunk with its chat prefix, the system prompt; 17..64 rows): one row tile of ceil(M/16) row blocks

@@ -268,7 +268,18 @@ class FreezeOmniEngine:
         """A ListenPipe over this engine (encoder stage of chunk c+1 overlapped with the LLM of chunk c)."""
         return ListenPipe(self)
 
+    # stage probe (bench.py --scenario duplex): a list to append (name, HIP event) marks to on the engine stream, or None
+    stage_probe = None
+
+    def _mark(self, name):
+        if self.stage_probe is not None:
+            ev = ctypes.c_void_p()
+            _lib.call("fo_event_create", ctypes.byref(ev))
+            _lib.call("fo_event_record", ev, ops.stream(self.device))
+            self.stage_probe.append((name, ev))
+
     def _listen_eager(self, items):
+        self._mark("start")
         for it in items:
             if it["identity"] not in ("user", "system"):
                 raise ValueError(f"Unknown identity: {it['identity']}. Must be 'user' or 'system'.")
@@ -289,6 +300,7 @@ class FreezeOmniEngine:
             for j, i in enumerate(idx):
                 results[i].update(enc_cache=ecs[j], ada_cache=acs[j], pe_index=pes[j])
                 rows[i] = (emb, j * To, To)
+            self._mark("encoder_" + ident)
         # assemble LLM input rows: [chat prefix (ipu_sl)] + adapter rows, all rounded to fp16 (.half())
         n_tok, pre_ids, pre_pos, ada_src, ada_pos = [], [], [], [], []
         r = 0
@@ -319,11 +331,15 @@ class FreezeOmniEngine:
                 meta = torch.tensor(list(range(r0, r0 + To)) + ada_pos[k:k + To], dtype=I32).to(self.device)
                 ops.gather_rows(e, meta[:To], out=x, round_fp16=True, out_rows=meta[To:])
                 k += To
+        self._mark("gather")
         h, bm = self.llm.forward(x, [(it["kv"], n) for it, n in zip(items, n_tok)])
+        self._mark("qwen2")
         pred = [i for i, it in enumerate(items) if it["identity"] == "user" and self.predict_usr_state]
         probs = None
         if pred:
-            probs = self.llm.state_probs(h, [bm.last_rows_host[i] for i in pred]).cpu().numpy()
+            sp = self.llm.state_probs(h, [bm.last_rows_host[i] for i in pred])
+            self._mark("state_head")
+            probs = sp.cpu().numpy()
         for i in range(len(items)):
             results[i]["probs"] = None
             results[i]["hidden_row"] = (h, bm.last_rows_host[i])

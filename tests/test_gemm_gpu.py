@@ -83,12 +83,14 @@ def test_gemm_fp32_activations_split(dev, M, N, K):
     assert err < 2e-4 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("M", [17, 40, 56, 64])
+@pytest.mark.parametrize("M", [17, 32, 40, 48, 56, 64])
 @pytest.mark.parametrize("N,K,sw", [(3584, 3584, False), (3584, 18944, False), (4096, 3584, True), (1024, 4096, False),
-                                    (3072, 1024, False)])
+                                    (3072, 1024, False), (2304, 1856, False), (1152, 3584, True)])
 def test_gemm_mid_rows(dev, M, N, K, sw):
-    """17..64 fp32 rows on Qwen2-sized weights (the turn's prefills): one row tile of ceil(M/16) row
-    blocks, K split for narrow layers; vs an fp64 reference (hi/lo split accuracy)."""
+    """17..64 fp32 rows on Qwen2-sized weights (the duplex ticks and the turn's prefills): the X-stationary
+    split-K stream (k_gemm_xsk + k_gemm_reduce; K = 1856 = 58 k-steps leaves the last split 2 k-steps, the other
+    waves' past-K steps predicated off) or, for K < 56 k-steps, one row tile of ceil(M/16) row blocks; vs an fp64
+    reference (hi/lo split accuracy)."""
     from fo.ops import PackedLinear
     g = torch.Generator().manual_seed(M * 31 + N + K)
     w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
@@ -108,6 +110,13 @@ def test_gemm_mid_rows(dev, M, N, K, sw):
         ref = x.double() @ w.double().t() + b.double() + r.double()
     err = (y - ref).abs().max().item()
     assert err < 2e-4 * ref.abs().max().item(), err
+    # deterministic: the split partials are summed in split order
+    if sw:
+        assert torch.equal(lin(x.to(dev)).cpu().double(), y)
+    else:
+        out2 = r.clone().to(dev)
+        lin(x.to(dev), out=out2, residual=True)
+        assert torch.equal(out2.cpu().double(), y)
 
 
 @pytest.mark.parametrize("M", [8, 16, 40, 56])

@@ -64,6 +64,12 @@ def _check_logits(lg, gold, first, what):
 
 
 def test_qwen2_real_geometry_matches_reference(dev, llm, gold):
+    check_llm_against_golden(llm, dev, gold)
+
+
+def check_llm_against_golden(llm, dev, gold):
+    """The golden's prefill, two chunks and three text steps through `llm` (an LLMEngine at the golden's
+    geometry: synthetic weights here, the reference's file formats in test_real_ingestion_gpu.py)."""
     from fo import _lib, ops
     from fo.engine import TextGraph
     lib = _lib.load()
