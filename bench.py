@@ -876,7 +876,7 @@ def run_duplex(eng, args, seconds, sync, probe=False):
             kv_tok = llm.stack.n * llm.KVH * llm.hd * 2 * 4
             idents = {d["identity"] for _, d, _ in done}
             st["bytes"] = (sum(eng.enc[i].weight_bytes + eng.ada[i].weight_bytes for i in idents) +
-                           llm.stack.weight_bytes + sum(ss.past_key_values.length for ss, _, _ in done) * kv_tok)
+                           llm.stack.weight_bytes + sum(ss.past_key_values.get_seq_length() for ss, _, _ in done) * kv_tok)
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
                 ms = ctypes.c_float()
                 _lib.call("fo_event_elapsed_ms", ea, eb, ctypes.byref(ms))

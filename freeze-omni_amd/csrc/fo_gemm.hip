@@ -708,9 +708,9 @@ inline int pipe_mode() {
 }
 // the pipelining fo_gemm chose for the launch it is issuing (0 none, 1 U-step, 2 two-step groups)
 thread_local int g_launch_pipe = 0;
-template <int NT, int RB, int NW>
+template <int NT, int RB, int NW, int U = 4>
 __global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
-  gemm_body<NT, RB, true, NW, 4, false, true>(a);
+  gemm_body<NT, RB, true, NW, U, false, true>(a);
 }
 
 template <int NT, int RB, int NW, int U, bool SW>
@@ -1162,8 +1162,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.trc = g_trc;
   FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
   if (lnw) {
-    FO_REQUIRE(lnb && x_f32 && M <= 32 && !swiglu && rstats && rstats1 && rgroups > 0 && !rope && ldx % 4 == 0,
-               "fo_gemm_ln: fp32 X, M <= 32, producer statistics, plain epilogue only (M=%d K=%d)", M, K);
+    FO_REQUIRE(lnb && x_f32 && M <= 64 && !swiglu && rstats && rstats1 && rgroups > 0 && !rope && ldx % 4 == 0,
+               "fo_gemm_ln: fp32 X, M <= 64, producer statistics, plain epilogue only (M=%d K=%d)", M, K);
   }
   if (rope) {
     FO_REQUIRE(!swiglu && !sout && !residual && !out_bf16 && act == 0 && !scale, "fo_gemm_qkv_rope: plain epilogue only");
@@ -1338,9 +1338,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (RB == 1) {
       if (NT == 2) { if (nw == 16) FO_LN(2, 1, 16); else FO_LN(2, 1, 8); }
       else { if (nw == 16) FO_LN(1, 1, 16); else FO_LN(1, 1, 8); }
-    } else {
+    } else if (RB == 2) {
       if (NT == 2) { if (nw == 16) FO_LN(2, 2, 16); else FO_LN(2, 2, 8); }
       else { if (nw == 16) FO_LN(1, 2, 16); else FO_LN(1, 2, 8); }
+    } else {   // 33..64 rows (the duplex encoder: 8 sessions x 7 framing-B frames): 2 k-steps in flight per wave
+      if (NT == 2) hipLaunchKernelGGL((k_gemm_ln<2, 4, 8, 2>), grid, dim3(512), 0, stream, a);
+      else hipLaunchKernelGGL((k_gemm_ln<1, 4, 8, 2>), grid, dim3(512), 0, stream, a);
     }
 #undef FO_LN
   } else if (mid) {

@@ -197,7 +197,7 @@ class PackedLinear:
 
 
     def ln(self, x, lnw, lnb, stats, eps=1e-5, out=None, act="none", M=None, splitk=0):
-        """act(LayerNorm(x) W^T + b) with the norm applied as X is loaded (fo_gemm_ln; M <= 32); stats:
+        """act(LayerNorm(x) W^T + b) with the norm applied as X is loaded (fo_gemm_ln; M <= 64); stats:
         the RowStats(with_sums=True) a rowstats() producer filled for x."""
         _check_dev(x)
         M = x.shape[0] if M is None else M

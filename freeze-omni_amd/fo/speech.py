@@ -227,7 +227,7 @@ class SpeechEncoderEngine:
         h, qkv, att, f = bufs["h"], bufs["qkv"], bufs["att"], bufs["f"]
         scale = 1.0 / math.sqrt(self.dk)
         # pre-norms applied by the GEMMs on load (fo_gemm_ln) from the residual producers' row sums
-        fuse_ln = B * T <= 32 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
+        fuse_ln = B * T <= 64 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
         sA, sB = bufs["sA"], bufs["sB"]
         last = len(self.layers) - 1
         for i, L in enumerate(self.layers):

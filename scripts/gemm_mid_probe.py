@@ -16,7 +16,7 @@ for name, N, K, sw in [("qwen_qkv", 4608, 3584, False), ("qwen_o", 3584, 3584, F
     w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     lin = PackedLinear(w, swiglu_up=w if sw else None)
     r = []
-    for M in (16, 24, 40, 56, 64):
+    for M in (16, 24, 32, 40, 48, 56, 64):
         x = torch.randn(M, K, device=dev)
         out = torch.empty(M, N, device=dev)
         t = timeit(lambda: lin(x, out=out), reps=20)

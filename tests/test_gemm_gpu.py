@@ -207,7 +207,9 @@ def test_gemm_qkv_rope(dev, M, H, KVH, hd, K, splitk):
 
 @pytest.mark.parametrize("M,N,K,act,splitk,psplit", [(32, 3072, 1024, "none", 0, 0), (32, 4096, 1024, "relu", 0, 4),
                                                      (17, 1024, 1024, "none", 2, 0), (8, 96, 32, "relu", 0, 0),
-                                                     (1, 64, 64, "none", 0, 2), (32, 64, 32, "none", 0, 0)])
+                                                     (1, 64, 64, "none", 0, 2), (32, 64, 32, "none", 0, 0),
+                                                     (56, 3072, 1024, "none", 0, 0), (56, 4096, 1024, "relu", 0, 4),
+                                                     (40, 1024, 1024, "none", 2, 0), (64, 64, 32, "relu", 0, 0)])
 def test_gemm_layernorm_on_load(dev, M, N, K, act, splitk, psplit):
     """fo_gemm_rowstats (residual producer writing row sums / sums of squares) -> fo_gemm_ln (LayerNorm
     applied to X on load from those statistics) vs residual + LayerNorm + Linear in fp64."""
