@@ -317,18 +317,18 @@ class FreezeOmniEngine:
             n_tok.append(len(p) + To)
         x = torch.empty(r, self.llm.D, dtype=F32, device=self.device)
         if pre_ids:
-            meta = torch.tensor(pre_ids + pre_pos, dtype=I32).to(self.device)
+            meta = ops.h2d(np.asarray(pre_ids + pre_pos, np.int32), self.device)
             ops.gather_rows(self.llm.embed_tokens, meta[:len(pre_ids)], out=x, round_fp16=True,
                             out_rows=meta[len(pre_ids):])
         emb0 = ada_src[0][0]
         if all(e is emb0 for e, _, _ in ada_src):
             src_rows = [r0 + k for _, r0, To in ada_src for k in range(To)]
-            meta = torch.tensor(src_rows + ada_pos, dtype=I32).to(self.device)
+            meta = ops.h2d(np.asarray(src_rows + ada_pos, np.int32), self.device)
             ops.gather_rows(emb0, meta[:len(src_rows)], out=x, round_fp16=True, out_rows=meta[len(src_rows):])
         else:
             k = 0
             for (e, r0, To) in ada_src:
-                meta = torch.tensor(list(range(r0, r0 + To)) + ada_pos[k:k + To], dtype=I32).to(self.device)
+                meta = ops.h2d(np.asarray(list(range(r0, r0 + To)) + ada_pos[k:k + To], np.int32), self.device)
                 ops.gather_rows(e, meta[:To], out=x, round_fp16=True, out_rows=meta[To:])
                 k += To
         self._mark("gather")

@@ -12,6 +12,8 @@ import threading
 import numpy as np
 import torch
 
+from . import ops
+
 
 class KVPool:
     def __init__(self, n_layers, n_kv, hd, n_pages, page_size, device):
@@ -224,7 +226,7 @@ class BatchMeta:
         self.uniform = self.n_items == len(entries) and len({n for _, n, _, _ in entries}) == 1
         host = np.concatenate([tok_seq, tok_pos, tok_slot, tok_nvis, np.asarray(last_rows, np.int32), bt.ravel(),
                                np.asarray(items, np.int32)])
-        dev = torch.from_numpy(host).to(device, non_blocking=True)
+        dev = ops.h2d(host, device)   # pinned staging, no stream synchronisation
         S = len(entries)
         self.T, self.S, self.maxb, self.max_keys = T, S, maxb, max_keys
         self.tok_seq = dev[0:T]

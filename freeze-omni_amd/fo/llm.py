@@ -3,6 +3,7 @@
 Reference: AudioLLM._llm_forward_core -> Qwen2Model (models/audioLLM.py:479-484), the dialog-state
 head (models/audioLLM.py:486-527) and the sampler _post_decode (models/audioLLM.py:431-477).
 """
+import numpy as np
 import torch
 
 from . import ops, tables
@@ -41,8 +42,10 @@ class LLMEngine:
         return KVSeq(self.pool)
 
     def embed(self, ids, out=None, round_fp16=False):
-        ids_d = ids if torch.is_tensor(ids) else torch.tensor(list(ids), dtype=I32)
-        ids_d = ids_d.to(device=self.device, dtype=I32)
+        if torch.is_tensor(ids):
+            ids_d = ids.to(device=self.device, dtype=I32)
+        else:
+            ids_d = ops.h2d(np.asarray(list(ids), np.int32), self.device)
         return ops.gather_rows(self.embed_tokens, ids_d, out=out, round_fp16=round_fp16)
 
     def forward(self, x, entries):
@@ -55,7 +58,7 @@ class LLMEngine:
 
     def state_probs(self, hidden, rows):
         """softmax over the first 3 predictor-head logits at the given rows -> device [S, 3]."""
-        rows_d = rows if torch.is_tensor(rows) else torch.tensor(list(rows), dtype=I32).to(self.device)
+        rows_d = rows if torch.is_tensor(rows) else ops.h2d(np.asarray(list(rows), np.int32), self.device)
         out = torch.empty(rows_d.numel(), 3, dtype=F32, device=self.device)
         return ops.state_head(hidden, rows_d, self.head_w, self.head_b, out)
 

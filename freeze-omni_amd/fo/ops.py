@@ -6,6 +6,7 @@ below is a hand-written gfx950 kernel in libfo_hip.so.
 import os
 import threading
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -295,6 +296,22 @@ class RowStats:
     def set(self, gamma, yg):
         self.gamma, self.yg = gamma, yg
         return self
+
+
+def h2d(a, device, dtype=None):
+    """Host values -> a new device tensor WITHOUT a stream synchronisation (a plain `.to(device)` of pageable
+    memory synchronises the stream, which on the eager paths -- duplex ticks, prefills -- stalls the host's launch
+    queue behind the GPU): the values are staged in pinned memory from PyTorch's caching host allocator (which keeps
+    the block until the copy recorded on the stream has run) and copied asynchronously on the current stream.
+    Never used while a graph is being captured (a captured copy would keep reading a recycled staging block)."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ops.h2d inside a graph capture")
+    t = a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    p.copy_(t)
+    return p.to(device, non_blocking=True)
 
 
 # ---------------------------------------------------------------- kernel wrappers

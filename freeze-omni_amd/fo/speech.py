@@ -70,10 +70,10 @@ class FbankGPU:
         """windows: np.float32 [B][n_samples]; firsts: list[bool] -> device feats [B, R, 80]."""
         B = len(firsts)
         host = np.concatenate([np.ascontiguousarray(windows, np.float32).reshape(-1),
-                               np.asarray([self.ov if f else 0 for f in firsts], np.float32)])
-        dev = torch.from_numpy(host).to(self.device)
+                               np.asarray([self.ov if f else 0 for f in firsts], np.int32).view(np.float32)])
+        dev = ops.h2d(host, self.device)   # samples + the per-row zero-row counts (int32 bits), one async copy
         samples = dev[:B * self.n_samples].view(B, self.n_samples)
-        zero_rows = dev[B * self.n_samples:].to(I32)
+        zero_rows = dev[B * self.n_samples:].view(I32)
         out = torch.empty(B, self.R * 80, dtype=F32, device=self.device)
         ops.fbank(samples, B, self.n_samples, self.wl, self.ws, self.nfft, self.window, self.tw_cos, self.tw_sin,
                   self.mel, out, 0, zero_rows)
@@ -258,7 +258,7 @@ class SpeechEncoderEngine:
         B, R, _ = feats.shape
         bufs = self.buffers(B, R)
         meta, new_pe = self.host_meta(caches, pe_indices)
-        bufs["meta"].copy_(torch.from_numpy(meta))
+        bufs["meta"].copy_(ops.h2d(meta, self.device))
         x, T = self.run(feats, B, R, bufs)
         self.advance(caches, T)
         return x, T, new_pe
