@@ -304,11 +304,13 @@ def h2d(a, device, dtype=None):
     queue behind the GPU): the values are staged in pinned memory from PyTorch's caching host allocator (which keeps
     the block until the copy recorded on the stream has run) and copied asynchronously on the current stream.
     Never used while a graph is being captured (a captured copy would keep reading a recycled staging block)."""
-    if torch.cuda.is_current_stream_capturing():
-        raise RuntimeError("ops.h2d inside a graph capture")
     t = a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))
     if dtype is not None:
         t = t.to(dtype)
+    if torch.device(device).type != "cuda":   # host-only bookkeeping tests (tests/test_host_cpu.py)
+        return t.clone()
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ops.h2d inside a graph capture")
     p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     p.copy_(t)
     return p.to(device, non_blocking=True)
