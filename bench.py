@@ -927,7 +927,8 @@ def duplex_roofline(pr, eng, bw=8.0e12):
         return None
     fr = [st["bytes"] / bw * 1e3 / st["tick"] for st in pr]
     gpu = [st["bytes"] / bw * 1e3 / max(1e-6, sum(v for k, v in st.items() if k in
-                                                    ("encoder_user", "encoder_system", "gather", "qwen2", "state_head")))
+                                                    ("encoder_user", "encoder_system", "encoders_both", "gather",
+                                                     "qwen2", "state_head")))
            for st in pr]
     b = float(np.median([st["bytes"] for st in pr]))
     return {"bound": "hbm", "unit": "GB/s", "peak": 8000.0,

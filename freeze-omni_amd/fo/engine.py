@@ -7,6 +7,7 @@ loads train.yaml + final.pt + Qwen2; speech_dialogue -> AudioLLM.set_system_role
 Where the reference runs one user per call with ~hundreds of small launches, every primitive here
 takes a list of sessions and issues one launch sequence for all of them.
 """
+import contextlib
 import ctypes
 import json
 import os
@@ -287,20 +288,41 @@ class FreezeOmniEngine:
                 raise AssertionError("must set system role first!!!")
         results = [dict() for _ in items]
         rows = {}
-        for ident in ("user", "system"):
+        idents = [d for d in ("user", "system") if any(it["identity"] == d for it in items)]
+        # both parties in one call (a duplex tick): the two identities' encoders + adapters are independent, so the
+        # second runs on its own stream beside the first (latency-bound launch chains overlap) and the LLM input
+        # gather waits for both
+        main = torch.cuda.current_stream()
+        s2 = ops.engine_stream(self.device, name="enc2") if len(idents) == 2 else None
+        if s2 is not None:
+            ev_in = torch.cuda.Event()
+            ev_in.record(main)
+        for k, ident in enumerate(idents):
             idx = [i for i, it in enumerate(items) if it["identity"] == ident]
-            if not idx:
-                continue
-            enc, ada = self.enc[ident], self.ada[ident]
-            ecs = [items[i]["enc_cache"] or enc.new_cache() for i in idx]
-            acs = [items[i]["ada_cache"] or ada.new_cache() for i in idx]
-            feats = torch.stack([items[i]["feats"] for i in idx]) if len(idx) > 1 else items[idx[0]]["feats"][None]
-            out, T, pes = enc.infer(feats.contiguous(), ecs, [items[i]["pe_index"] or 0 for i in idx])
-            emb, To = ada(out, T, acs)
+            side = s2 is not None and k == 1
+            with torch.cuda.stream(s2) if side else contextlib.nullcontext():
+                if side:
+                    s2.wait_event(ev_in)
+                    for i in idx:
+                        items[i]["feats"].record_stream(s2)
+                enc, ada = self.enc[ident], self.ada[ident]
+                ecs = [items[i]["enc_cache"] or enc.new_cache() for i in idx]
+                acs = [items[i]["ada_cache"] or ada.new_cache() for i in idx]
+                feats = torch.stack([items[i]["feats"] for i in idx]) if len(idx) > 1 else items[idx[0]]["feats"][None]
+                out, T, pes = enc.infer(feats.contiguous(), ecs, [items[i]["pe_index"] or 0 for i in idx])
+                emb, To = ada(out, T, acs)
+                if side:
+                    emb.record_stream(main)
+                    ev_out = torch.cuda.Event()
+                    ev_out.record(s2)
             for j, i in enumerate(idx):
                 results[i].update(enc_cache=ecs[j], ada_cache=acs[j], pe_index=pes[j])
                 rows[i] = (emb, j * To, To)
-            self._mark("encoder_" + ident)
+            if s2 is None:
+                self._mark("encoder_" + ident)
+        if s2 is not None:
+            main.wait_event(ev_out)
+            self._mark("encoders_both")
         # assemble LLM input rows: [chat prefix (ipu_sl)] + adapter rows, all rounded to fp16 (.half())
         n_tok, pre_ids, pre_pos, ada_src, ada_pos = [], [], [], [], []
         r = 0
