@@ -886,13 +886,14 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
 // k_gemm_reduce (the next launch) sums the slabs in split order and runs the epilogue (SwiGLU, RMSNorm rstd,
 // RoPE + paged-KV append, residual, row statistics).  k-steps past K (the last split of a long-K layer) load
 // nothing and multiply zero X.
-template <int NW, int KPW, int RB>
+template <int NW, int KPW, int RB, int UA>   // UA units (2 UA tile buffers) of weights in flight per wave
 __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
   __shared__ bf16x8 xlo[NW][RB][KPW][64];
   __shared__ float part[NW][2][RB * 16][17];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int KW = NW * KPW;
   constexpr int ROWS = RB * 16;
+  constexpr int NB = 2 * UA;
   const int KS = a.K >> 5;
   const int sp = blockIdx.y;
   const int ub = (int)((long)units * blockIdx.x / gridDim.x);
@@ -905,15 +906,27 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
                               (unsigned)__builtin_amdgcn_readfirstlane((unsigned)wbase)),
       (short)0, __builtin_amdgcn_readfirstlane(a.ntiles * KS * 1024), 0x00020000);
   const int voff = (ks0 * 64 + lane) * 16;
-  bf16x8 w0[KPW], w1[KPW];
-  auto issue = [&](bf16x8 (&w)[KPW], int tile) {
+  // the weight stream's depth sets its rate (a CU's share of HBM ~ its bytes in flight): k_gemm_xs keeps 2 x 14 KiB
+  // per wave in flight; with KPW = 7 k-steps per wave this kernel keeps 2 UA tiles' fragments in flight instead
+  bf16x8 wb[NB][KPW];
+  auto issue = [&](bf16x8 (&w)[KPW], int tile) {   // tile >= 2 ue: past the workgroup's range -> no load issued
+    if (tile < 2 * ue) {
+#pragma unroll
+      for (int j = 0; j < KPW; ++j)
+        if (j < nj)
+          w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024, 2));
+    }
+  };
+  bf16x8 zero;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) zero[i] = (__bf16)0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
 #pragma unroll
     for (int j = 0; j < KPW; ++j)
-      if (j < nj)
-        w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024, 2));
-  };
-  issue(w0, ub < ue ? 2 * ub : a.ntiles);
-  issue(w1, ub < ue ? 2 * ub + 1 : a.ntiles);
+      if (j >= nj) wb[b][j] = zero;   // k-steps past K: no weights loaded, zero fragments
+#pragma unroll
+  for (int b = 0; b < NB; ++b) issue(wb[b], 2 * ub + b);
   bf16x8 xh[RB][KPW];
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
@@ -921,7 +934,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
     const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4) + (size_t)ks0 * 32;
 #pragma unroll
     for (int j = 0; j < KPW; ++j) {
-      bf16x8 hi, lo;
+      bf16x8 hi = zero, lo = zero;
       if (j < nj) {
         const float4 p0 = reinterpret_cast<const float4*>(xp + j * 32)[0];
         const float4 p1 = reinterpret_cast<const float4*>(xp + j * 32)[1];
@@ -932,14 +945,6 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
           hi[i] = h;
           lo[i] = (__bf16)(f[i] - (float)h);
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          hi[i] = (__bf16)0.f;
-          lo[i] = (__bf16)0.f;
-        }
-        w0[j] = hi;   // k-steps past K: no weights loaded, zero fragments
-        w1[j] = hi;
       }
       xh[r][j] = hi;
       xlo[wave][r][j][lane] = lo;
@@ -958,28 +963,33 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
   };
   const int Ncols = a.ntiles * 16;
   float* slab = a.ws + (size_t)sp * ROWS * Ncols;
-  for (int u = ub; u < ue; ++u) {
-    const int nxt = u + 1 < ue ? 2 * (u + 1) : a.ntiles;
-    f32x4 c0[RB], c1[RB];
-    compute(w0, c0);
-    issue(w0, nxt);
-    compute(w1, c1);
-    issue(w1, nxt + (u + 1 < ue ? 1 : 0));
-    __syncthreads();  // the previous unit's reduction has read part[]
+  for (int u0 = ub; u0 < ue; u0 += UA) {
 #pragma unroll
-    for (int r = 0; r < RB; ++r)
+    for (int q = 0; q < UA; ++q) {
+      const int u = u0 + q;
+      if (u < ue) {   // workgroup-uniform: the barriers below are reached by every wave
+        f32x4 c0[RB], c1[RB];
+        compute(wb[2 * q], c0);
+        issue(wb[2 * q], 2 * (u + UA));
+        compute(wb[2 * q + 1], c1);
+        issue(wb[2 * q + 1], 2 * (u + UA) + 1);
+        __syncthreads();  // the previous unit's reduction has read part[]
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        part[wave][0][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c0[r][i];
-        part[wave][1][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c1[r][i];
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            part[wave][0][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c0[r][i];
+            part[wave][1][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c1[r][i];
+          }
+        __syncthreads();
+        for (int e = threadIdx.x; e < 2 * ROWS * 16; e += NW * 64) {
+          const int t = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) v += part[w][t][rr][c];
+          slab[(size_t)rr * Ncols + (2 * u + t) * 16 + c] = v;
+        }
       }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 2 * ROWS * 16; e += NW * 64) {
-      const int t = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) v += part[w][t][rr][c];
-      slab[(size_t)rr * Ncols + (2 * u + t) * 16 + c] = v;
     }
   }
 }
@@ -1203,7 +1213,9 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   }
   // 17..64 rows on large weights (duplex ticks: 8 sessions x 4 framing-B tokens, the assistant prefix 8 x 5, prefixed
   // first chunks): the X-stationary stream with K split over workgroups (k_gemm_xsk) + k_gemm_reduce
-  const bool big_w0 = (long long)a.ntiles * 16 * K >= (8ll << 20);
+  // only the weight streams (>= 64 MB: Qwen2 gate/up, down): on the 26-33 MB q|k|v / o the one-row-tile kernels
+  // below are faster (r04d probe: o 14.8 vs 18.5 us, q|k|v 19.2 vs 24.4 us at 32 rows)
+  const bool big_w0 = (long long)a.ntiles * 16 * K >= (64ll << 20);
   if (x_f32 && M > 16 && M <= 64 && !lnw && (a.ntiles % 2) == 0 && splitk <= 1 && xsk_mode() && !g_force_nt &&
       !g_force_nw && big_w0 && ldx % 4 == 0 && !sout1 && (K >> 5) >= ((M + 15) / 16 == 2 ? 56 : 28)) {
     const int RBk = (M + 15) / 16;
@@ -1220,9 +1232,9 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.counters = nullptr;
     if (sgroups) *sgroups = (N + 255) / 256;
     dim3 grid(G, S);
-    if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2>), grid, dim3(512), 0, stream, a, units);
-    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<4, 7, 3>), grid, dim3(256), 0, stream, a, units);
-    else hipLaunchKernelGGL((k_gemm_xsk<4, 7, 4>), grid, dim3(256), 0, stream, a, units);
+    if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2, 2>), grid, dim3(512), 0, stream, a, units);
+    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<4, 7, 3, 4>), grid, dim3(256), 0, stream, a, units);
+    else hipLaunchKernelGGL((k_gemm_xsk<4, 7, 4, 4>), grid, dim3(256), 0, stream, a, units);
     int rc = fo::check_launch("fo_gemm/xsk");
     if (rc) return rc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, RBk * 16);

@@ -10,6 +10,7 @@
 #   fetch      FETCH_SIZE pass on the dominant kernel                    -> <tag>_pmc/
 #   tts        rocprofv3 kernel stats of the AR decode step alone        -> <tag>_prof_tts/
 #   text       rocprofv3 kernel stats of the text step alone             -> <tag>_prof_text/
+#   steptrace  per-node timeline of the AR decode step (kernel trace)   -> <tag>_step_timeline.txt
 #   duplex     the config-5 duplex line                                  -> <tag>_duplex.json
 #   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
 #   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
@@ -45,6 +46,9 @@ for S in "$@"; do
              > ${O}_pmc.log 2>&1; rc=$? ;;
     tts)   (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_tts -o tts -f csv -- \
              python3 $ROOTD/scripts/tts_step_time.py 8 multi) > ${O}_prof_tts.log 2>&1; rc=$? ;;
+    steptrace) (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace -d $ROOTD/${O}_steptrace -o tts -f csv -- \
+             python3 $ROOTD/scripts/tts_step_time.py 8 multi) > ${O}_steptrace.log 2>&1 && \
+             python3 scripts/step_timeline.py ${O}_steptrace > ${O}_step_timeline.txt 2>&1; rc=$?; cat ${O}_step_timeline.txt ;;
     text)  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_text -o text -f csv -- \
              python3 $ROOTD/scripts/text_step_time.py) > ${O}_prof_text.log 2>&1; rc=$? ;;
     duplex) timeout -k 10 400 python -u bench.py --scenario duplex --out ${O}_duplex.json > ${O}_duplex.log 2>&1; rc=$?
