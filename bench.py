@@ -877,11 +877,12 @@ def run_duplex(eng, args, seconds, sync, probe=False):
             idents = {d["identity"] for _, d, _ in done}
             st["bytes"] = (sum(eng.enc[i].weight_bytes + eng.ada[i].weight_bytes for i in idents) +
                            llm.stack.weight_bytes + sum(ss.past_key_values.get_seq_length() for ss, _, _ in done) * kv_tok)
-            for (a, ea), (b, eb) in zip(marks, marks[1:]):
+            for (a, ea, ha), (b, eb, hb) in zip(marks, marks[1:]):
                 ms = ctypes.c_float()
                 _lib.call("fo_event_elapsed_ms", ea, eb, ctypes.byref(ms))
                 st[b] = st.get(b, 0.0) + ms.value
-            for _, e in marks:
+                st["host_" + b] = st.get("host_" + b, 0.0) + (hb - ha) * 1e3   # host time to enqueue the stage
+            for _, e, _ in marks:
                 _lib.call("fo_event_destroy", e)
             if marks:
                 stages.append(st)

@@ -11,6 +11,7 @@ import contextlib
 import ctypes
 import json
 import os
+import time
 from types import SimpleNamespace
 
 import numpy as np
@@ -277,7 +278,7 @@ class FreezeOmniEngine:
             ev = ctypes.c_void_p()
             _lib.call("fo_event_create", ctypes.byref(ev))
             _lib.call("fo_event_record", ev, ops.stream(self.device))
-            self.stage_probe.append((name, ev))
+            self.stage_probe.append((name, ev, time.perf_counter()))
 
     def _listen_eager(self, items):
         self._mark("start")
