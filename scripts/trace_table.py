@@ -1,11 +1,14 @@
-"""Per (kernel, grid, block) totals from a rocprofv3 kernel_trace.csv: python scripts/trace_table.py DIR [N]"""
+"""Per (kernel, grid, block) totals from a rocprofv3 kernel_trace.csv: python scripts/trace_table.py DIR [N] [prefix]"""
 import csv
 import re
 import sys
 from collections import defaultdict
 
 d = defaultdict(lambda: [0, 0.0])
-path = sys.argv[1].rstrip("/") + "/bench_kernel_trace.csv"
+import glob
+pref = sys.argv[3] if len(sys.argv) > 3 else "bench"
+path = sorted(glob.glob(sys.argv[1].rstrip("/") + f"/**/{pref}_kernel_trace.csv", recursive=True) +
+              glob.glob(sys.argv[1].rstrip("/") + f"/{pref}_kernel_trace.csv"))[0]
 for r in csv.DictReader(open(path)):
     n = r["Kernel_Name"]
     m = re.search(r"::(k_\w+(<[^>]*>)?)", n)
