@@ -11,9 +11,9 @@ import torch
 # captured-graph caches a warm-up fills lazily (decode / text / listen graphs, vocoder buffers, fbank tables),
 # so a replica that has run work before the broadcast walks the same storage list as one that has not
 _SKIP_CLASSES = {"KVPool", "KVSeq", "Runtime", "SlotPool", "EncoderCache", "AdapterCache", "Framer", "DecodeGraph",
-                 "TextGraph", "ListenGraph", "ListenPipe", "FbankGPU", "HostBuffer", "SampleCheck", "_HostRing"}
+                 "TextGraph", "ListenGraph", "EncoderGraph", "ListenPipe", "FbankGPU", "HostBuffer", "SampleCheck", "_HostRing"}
 _FOREIGN = {"torch", "numpy", "builtins", "ctypes", "transformers", "tokenizers", "threading", "logging"}
-_SKIP_ATTRS = {"ws", "counters", "part_ml", "part_o", "scratch", "src", "_graphs", "_lgraphs", "_tgraphs", "_fbank",
+_SKIP_ATTRS = {"ws", "counters", "part_ml", "part_o", "scratch", "src", "_graphs", "_lgraphs", "_egraphs", "_tgraphs", "_fbank",
                "host", "meta_d", "hist", "err"}
 
 

@@ -373,5 +373,5 @@ class AdapterEngine:
         """x: device [B*T, d]; returns (out [B*To, L], To)."""
         B = len(caches)
         bufs = self.buffers(B, T)
-        bufs["slots"].copy_(torch.tensor([c.slot for c in caches], dtype=I32))
+        bufs["slots"].copy_(ops.h2d(np.asarray([c.slot for c in caches], np.int32), self.device))
         return self.run(x, B, T, bufs)
