@@ -888,8 +888,10 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
 // nothing and multiply zero X.
 template <int NW, int KPW, int RB, int UA>   // UA units (2 UA tile buffers) of weights in flight per wave
 __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
+  // the per-unit cross-wave reduction holds both tiles when the LDS allows, else one tile at a time
+  constexpr int PT = (NW * RB * KPW * 1024 + NW * 2 * RB * 16 * 17 * 4 <= 160 * 1024) ? 2 : 1;
   __shared__ bf16x8 xlo[NW][RB][KPW][64];
-  __shared__ float part[NW][2][RB * 16][17];
+  __shared__ float part[NW][PT][RB * 16][17];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int KW = NW * KPW;
   constexpr int ROWS = RB * 16;
@@ -968,26 +970,28 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
     for (int q = 0; q < UA; ++q) {
       const int u = u0 + q;
       if (u < ue) {   // workgroup-uniform: the barriers below are reached by every wave
-        f32x4 c0[RB], c1[RB];
-        compute(wb[2 * q], c0);
+        f32x4 c[2][RB];
+        compute(wb[2 * q], c[0]);
         issue(wb[2 * q], 2 * (u + UA));
-        compute(wb[2 * q + 1], c1);
+        compute(wb[2 * q + 1], c[1]);
         issue(wb[2 * q + 1], 2 * (u + UA) + 1);
-        __syncthreads();  // the previous unit's reduction has read part[]
 #pragma unroll
-        for (int r = 0; r < RB; ++r)
+        for (int t0 = 0; t0 < 2; t0 += PT) {
+          __syncthreads();  // the previous reduction has read part[]
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            part[wave][0][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c0[r][i];
-            part[wave][1][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c1[r][i];
+          for (int p = 0; p < PT; ++p)
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) part[wave][p][r * 16 + 4 * (lane >> 4) + i][lane & 15] = c[t0 + p][r][i];
+          __syncthreads();
+          for (int e = threadIdx.x; e < PT * ROWS * 16; e += NW * 64) {
+            const int p = e / (ROWS * 16), rr = (e >> 4) % ROWS, cc = e & 15;
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) v += part[w][p][rr][cc];
+            slab[(size_t)rr * Ncols + (2 * u + t0 + p) * 16 + cc] = v;
           }
-        __syncthreads();
-        for (int e = threadIdx.x; e < 2 * ROWS * 16; e += NW * 64) {
-          const int t = e / (ROWS * 16), rr = (e >> 4) % ROWS, c = e & 15;
-          float v = 0.f;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) v += part[w][t][rr][c];
-          slab[(size_t)rr * Ncols + (2 * u + t) * 16 + c] = v;
         }
       }
     }
@@ -1217,9 +1221,11 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   // below are faster (r04d probe: o 14.8 vs 18.5 us, q|k|v 19.2 vs 24.4 us at 32 rows)
   const bool big_w0 = (long long)a.ntiles * 16 * K >= (64ll << 20);
   if (x_f32 && M > 16 && M <= 64 && !lnw && (a.ntiles % 2) == 0 && splitk <= 1 && xsk_mode() && !g_force_nt &&
-      !g_force_nw && big_w0 && ldx % 4 == 0 && !sout1 && (K >> 5) >= ((M + 15) / 16 == 2 ? 56 : 28)) {
+      !g_force_nw && big_w0 && ldx % 4 == 0 && !sout1 && (K >> 5) >= 56) {
     const int RBk = (M + 15) / 16;
-    const int NWk = RBk == 2 ? 8 : 4, KPWk = 7;   // every split has work: K >= NW * KPW k-steps
+    // 8 waves x KPW k-steps of X per split (hi in VGPRs, lo in LDS: KPW shrinks as the row blocks grow), UA units of
+    // weights in flight per wave (~28 KiB, k_gemm_xs's depth); every split has work (K >= 56 k-steps)
+    const int NWk = 8, KPWk = RBk == 2 ? 7 : (RBk == 3 ? 4 : 3);
     const int KSk = K >> 5;
     const int S = (KSk + NWk * KPWk - 1) / (NWk * KPWk);
     const int units = a.ntiles / 2;
@@ -1233,8 +1239,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (sgroups) *sgroups = (N + 255) / 256;
     dim3 grid(G, S);
     if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2, 2>), grid, dim3(512), 0, stream, a, units);
-    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<4, 7, 3, 4>), grid, dim3(256), 0, stream, a, units);
-    else hipLaunchKernelGGL((k_gemm_xsk<4, 7, 4, 4>), grid, dim3(256), 0, stream, a, units);
+    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<8, 4, 3, 3>), grid, dim3(512), 0, stream, a, units);
+    else hipLaunchKernelGGL((k_gemm_xsk<8, 3, 4, 4>), grid, dim3(512), 0, stream, a, units);
     int rc = fo::check_launch("fo_gemm/xsk");
     if (rc) return rc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, RBk * 16);
