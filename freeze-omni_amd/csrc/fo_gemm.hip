@@ -1217,9 +1217,11 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   }
   // 17..64 rows on large weights (duplex ticks: 8 sessions x 4 framing-B tokens, the assistant prefix 8 x 5, prefixed
   // first chunks): the X-stationary stream with K split over workgroups (k_gemm_xsk) + k_gemm_reduce
-  // only the weight streams (>= 64 MB: Qwen2 gate/up, down): on the 26-33 MB q|k|v / o the one-row-tile kernels
-  // below are faster (r04d probe: o 14.8 vs 18.5 us, q|k|v 19.2 vs 24.4 us at 32 rows)
-  const bool big_w0 = (long long)a.ntiles * 16 * K >= (64ll << 20);
+  // only the weight streams: >= 64 MB (Qwen2 gate/up, down) or long-K >= 16 MB (the speech encoder's subsampling
+  // output linear, 19,456 x 1024 = 40 MB: 48.8 us per chunk on the split-K grid kernel, r04i); on the 26-33 MB
+  // q|k|v / o the one-row-tile kernels below are faster (r04d probe: o 14.8 vs 18.5 us, q|k|v 19.2 vs 24.4 us at 32 rows)
+  const long long wbytes0 = (long long)a.ntiles * 16 * K * 2;
+  const bool big_w0 = wbytes0 >= (128ll << 20) || (K >= 8192 && wbytes0 >= (32ll << 20));
   if (x_f32 && M > 16 && M <= 64 && !lnw && (a.ntiles % 2) == 0 && splitk <= 1 && xsk_mode() && !g_force_nt &&
       !g_force_nw && big_w0 && ldx % 4 == 0 && !sout1 && (K >> 5) >= 56) {
     const int RBk = (M + 15) / 16;
