@@ -1324,7 +1324,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     const int wg = a.ntiles / 4 * mt;
     if (wg < 256 && KS >= 128) S_auto = KS >= 256 ? 4 : 2;
   }
-  if (rope) NT = 2;  // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds
+  // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds; a 17..64-row RoPE projection on large
+  // weights (the Qwen2 q|k|v of a duplex tick or a prefill) keeps the 4-tile column groups of the plain path and
+  // always splits K, so k_gemm_reduce (which pairs the tiles itself) runs that epilogue: one X read per 4 tiles
+  // instead of per pair (r04g trace: the 2-tile split q|k|v 33.9 + 5 us at 33..48 rows)
+  const bool rope4 = rope && mid && NT == 4 && splitk <= 1 && !g_force_nt;
+  if (rope && !rope4) NT = 2;
   if (lnw && NT > 2) NT = 2;
   const int groups = a.ntiles / NT;
   if (mid) {  // split K: 2 ways on wide layers (Qwen2 gate/up), until the grid covers the chip on narrow ones
@@ -1335,6 +1340,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   int S = splitk > 0 ? splitk : (S_auto && !g_force_nt ? S_auto : (mid ? 1 : fo_gemm_pick_split(M, groups, K)));
   if (rstats && !lnw && !mid) S = 1;  // (split RMSNorm consumers: k_gemm_reduce applies the rstd)
   if (S > (K >> 5)) S = K >> 5;
+  if (rope4 && S < 2) S = 2;   // the pair epilogue needs the reduce launch
   a.S = S;
   if (S > 1) {
     const long long need = (long long)S * mt * RB * 16 * a.ntiles * 16;
