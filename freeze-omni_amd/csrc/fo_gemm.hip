@@ -1369,7 +1369,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       else { if (nw == 16) FO_LN(1, 2, 16); else FO_LN(1, 2, 8); }
     } else {   // 33..64 rows (the duplex encoder: 8 sessions x 7 framing-B frames): 2 k-steps in flight per wave
       if (NT == 2) hipLaunchKernelGGL((k_gemm_ln<2, 4, 8, 2>), grid, dim3(512), 0, stream, a);
-      else hipLaunchKernelGGL((k_gemm_ln<1, 4, 8, 2>), grid, dim3(512), 0, stream, a);
+      else hipLaunchKernelGGL((k_gemm_ln<1, 4, 8, 4>), grid, dim3(512), 0, stream, a);
     }
 #undef FO_LN
   } else if (mid) {
