@@ -16,6 +16,7 @@
 #   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
 #   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
 #   ab         ENV_A / ENV_B (e.g. 'FO_X=0') alternated twice on the quick bench -> <tag>_ab.txt
+#   sweep      SWEEP='A=1|B=2|' settings ('|'-separated, empty = default), two rounds on the quick bench -> <tag>_sweep.txt
 #   py:<script args>   any scripts/ probe, e.g. 'py:llm_stage_time.py' (200 s limit)
 set -o pipefail
 R=$1; shift
@@ -68,6 +69,13 @@ for S in "$@"; do
                > ${O}_ab_$AB$i.log 2>&1 || { rc=$?; tail -20 ${O}_ab_$AB$i.log; break 2; }
              echo "$AB$i [${!E}] $(line ${O}_ab_$AB$i.log)" >> ${O}_ab.txt; rc=0
            done; done; cat ${O}_ab.txt ;;
+    sweep) : > ${O}_sweep.txt   # SWEEP='A=1|B=2 C=3|' : each setting (empty = default) on the quick bench, two rounds
+           IFS='|' read -ra SET <<< "$SWEEP"; rc=0
+           for i in 1 2; do for k in "${!SET[@]}"; do
+             timeout -k 10 300 env ${SET[$k]} python -u bench.py --no-cpu-baseline --no-single-user --steps 3 \
+               > ${O}_sweep_$k$i.log 2>&1 || { rc=$?; tail -20 ${O}_sweep_$k$i.log; break 2; }
+             echo "$i [${SET[$k]:-default}] $(line ${O}_sweep_$k$i.log)" >> ${O}_sweep.txt
+           done; done; cat ${O}_sweep.txt ;;
     py:*)  timeout -k 10 200 python -u scripts/${S#py:} > ${O}_$(basename ${S#py:} .py | cut -d' ' -f1).log 2>&1; rc=$?
            tail -40 ${O}_$(basename ${S#py:} .py | cut -d' ' -f1).log ;;
     *) echo "unknown step $S"; rc=1 ;;
