@@ -43,22 +43,6 @@ MAIN_STREAM_PRIORITY = int(os.environ.get("FO_MAIN_PRIORITY", "0"))
 # FO_ENC_CUS=k (probe): the side stream (the pipelined listen's encoder stage, fbank) runs on k CUs spread over the
 # device's 32-CU blocks and the engine stream on the others, so no Qwen2 workgroup shares a CU with the encoder's
 ENC_CUS = int(os.environ.get("FO_ENC_CUS", "0"))
-# probe knobs (A/B): FO_SPEECH_CUS=N confines the speech lane's streams (tts, tts1, voc: the sentences whose speech
-# runs beside the text decode) to N CUs spread over the 8 XCDs; FO_SPEECH_EXCL=1 also keeps the engine / side streams
-# off those CUs.  The response's last sentence (tts2 / voc2, after the text decode) keeps the whole chip.
-SPEECH_CUS = int(os.environ.get("FO_SPEECH_CUS", "0"))
-SPEECH_EXCL = os.environ.get("FO_SPEECH_EXCL", "0") == "1"
-_LANE_STREAMS = ("tts", "tts1", "voc")
-
-
-def _speech_partition(idx):
-    if SPEECH_CUS <= 0:
-        return None
-    n = torch.cuda.get_device_properties(idx).multi_processor_count
-    blk = n // 8
-    per = max(1, SPEECH_CUS // 8)
-    sp = sorted({x * blk + blk - 1 - j for x in range(8) for j in range(per)})
-    return [c for c in range(n) if c not in set(sp)], sp, n
 
 
 def _enc_partition(idx):
@@ -86,16 +70,9 @@ def engine_stream(device, side=False, name=None):
         h = ctypes.c_void_p()
         with torch.cuda.device(idx):
             part = _enc_partition(idx) if name is None else None
-            spart = _speech_partition(idx)
-            cus = None
             if part is not None:   # listen-stage CU partition: side stream on the encoder's CUs, engine on the rest
-                cus, n = (part[1] if side else part[0]), part[2]
-            elif spart is not None and name in _LANE_STREAMS:
-                cus, n = spart[1], spart[2]
-            elif spart is not None and SPEECH_EXCL and name is None:
-                cus, n = spart[0], spart[2]
-            if cus is not None:
-                words = (n + 31) // 32
+                cus = part[1] if side else part[0]
+                words = (part[2] + 31) // 32
                 m = (ctypes.c_uint * words)()
                 for c in cus:
                     m[c // 32] |= 1 << (c % 32)
