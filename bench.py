@@ -219,7 +219,13 @@ def run_turn(engine, base_kv, pcms, args, sync):
             feats = fb(np.stack(wins), firsts)
         items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=feats[b], kv=t.kv,
                       enc_cache=t.enc_cache, ada_cache=t.ada_cache, pe_index=t.pe) for b, t in enumerate(turns)]
-        if pipe is not None and c > 0:
+        if pipe is not None and c == 0:
+            # the chat prefix comes from the shared-context prefix cache (exact by causality), after which chunk 0
+            # is a steady-state chunk: it enters the pipe, so its LLM stage overlaps chunk 1's encoder stage
+            items = engine.apply_chat_prefix(items)
+            for t, it in zip(turns, items):
+                t.enc_cache, t.ada_cache = it["enc_cache"], it["ada_cache"]
+        if pipe is not None and (c > 0 or engine._graphable(items)):
             # steady state: this chunk's encoder stage overlaps the previous chunk's LLM stage
             pe_next, _ = pipe.push(items)
             for t, pe in zip(turns, pe_next):
@@ -228,7 +234,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
             for t, r in zip(turns, engine.listen(items)):
                 t.enc_cache, t.ada_cache, t.pe = r["enc_cache"], r["ada_cache"], r["pe_index"]
         if c == 0:
-            t_c0 = time.perf_counter()   # chunk 0 (chat prefix, eager) has been read back
+            t_c0 = time.perf_counter()   # chunk 0 submitted (pipe) or read back (--no-pipeline)
     if pipe is not None:
         pipe.flush()
     # ---- dialog_ss (benchmark policy forces it at end of input, as bin/inference.py:138 does)

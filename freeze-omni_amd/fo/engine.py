@@ -196,6 +196,12 @@ class FreezeOmniEngine:
                 return self._listen_graph(items)
             return self._listen_eager(items)
 
+    def apply_chat_prefix(self, items):
+        """The first chunk's chat-prefix rows applied ahead of its listen (the shared-context prefix cache below):
+        afterwards the items are steady-state chunks with open caches, so a ListenPipe can take them too."""
+        with torch.cuda.stream(ops.engine_stream(self.device)):
+            return self._apply_cached_prefixes(items)
+
     PREFIX_CACHE = 8
     use_prefix_cache = True
 

@@ -52,8 +52,9 @@ def test_listen_graph_matches_eager(eng, dev):
             np.testing.assert_allclose(a, b, atol=2e-5, rtol=1e-5)
 
 
-def _session_pipe(eng, feats_seq, n_users):
-    """Chunk 0 through listen() (chat prefix), the rest through a ListenPipe."""
+def _session_pipe(eng, feats_seq, n_users, first_in_pipe=False):
+    """Chunk 0 through listen() (chat prefix), the rest through a ListenPipe; first_in_pipe: chunk 0 too, after
+    engine.apply_chat_prefix (the bench's order)."""
     base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
     kvs = [base.fork() for _ in range(n_users)]
     state = [dict(enc_cache=None, ada_cache=None, pe_index=0) for _ in range(n_users)]
@@ -68,7 +69,11 @@ def _session_pipe(eng, feats_seq, n_users):
     for c, f in enumerate(feats_seq):
         items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=f[u], kv=kvs[u], **state[u])
                  for u in range(n_users)]
-        if c == 0:
+        if c == 0 and first_in_pipe:
+            items = eng.apply_chat_prefix(items)
+            for u, it in enumerate(items):
+                state[u] = dict(enc_cache=it["enc_cache"], ada_cache=it["ada_cache"], pe_index=it["pe_index"])
+        elif c == 0:
             res = eng.listen(items)
             for u, r in enumerate(res):
                 state[u] = dict(enc_cache=r["enc_cache"], ada_cache=r["ada_cache"], pe_index=r["pe_index"])
@@ -87,14 +92,16 @@ def _session_pipe(eng, feats_seq, n_users):
     return out, lens
 
 
-def test_listen_pipe_matches_sequential(eng, dev):
-    """Encoder stage of chunk c+1 overlapped with the LLM stage of chunk c gives the sequential results."""
+@pytest.mark.parametrize("first_in_pipe", [False, True])
+def test_listen_pipe_matches_sequential(eng, dev, first_in_pipe):
+    """Encoder stage of chunk c+1 overlapped with the LLM stage of chunk c gives the sequential results; with
+    first_in_pipe chunk 0 (its chat prefix from the shared-context prefix cache) enters the pipe too."""
     g = np.load(os.path.join(G, "fbank.npz"))
     n_users = 3
     feats = torch.from_numpy(g["A_feats"]).to(dev)
     seq = [torch.stack([feats[(c + 5 * u) % 13] for u in range(n_users)]) for c in range(9)]
     ref = _session_run(eng, seq, True, n_users)
-    got, lens = _session_pipe(eng, seq, n_users)
+    got, lens = _session_pipe(eng, seq, n_users, first_in_pipe)
     assert len(got) == len(ref)
     assert lens == ref[-1][2]
     for (pe, he, _, qe), (pg, hg, _, qg) in zip(ref, got):
