@@ -1316,7 +1316,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (g_force_nt == 1 || g_force_nt == 2) NT = swiglu ? 2 : g_force_nt;
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
   }
-  if (RB == 4 && !swiglu && mt >= 4 && a.ntiles % 4 == 0 && a.ntiles >= 64) {
+  int nw_pref4 = 0;
+  if (RB == 4 && g_force_nt && x_f32 && !lnw && !rope) {   // sweeps (fo_gemm_tune): forced tiles per workgroup
+    NT = g_force_nt;
+    if (swiglu && NT < 2) NT = 2;
+    if (a.ntiles % NT) NT = swiglu ? 2 : 1;
+  } else if (RB == 4 && !swiglu && mt >= 4 && a.ntiles % 4 == 0 && a.ntiles >= 64) {
     // many row tiles (im2col convolutions, long prefills): X traffic (fp32, re-read by every column
     // group) dominates the weights', so 4 column tiles share each X read; long K is split over
     // workgroups until the grid covers the chip
@@ -1413,10 +1418,20 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     else launch_nw<1, 2, false>(nw, wstream, x_f32, grid, a, stream);
   } else {
     if (x_f32) {
-      if (swiglu) launch_gemm<2, 4, 4, 2, true>(wstream, x_f32, grid, a, stream);
-      else if (NT == 4) launch_gemm<4, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
-      else if (NT == 2) launch_gemm<2, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
-      else launch_gemm<1, 4, 4, 2, false>(wstream, x_f32, grid, a, stream);
+      // 64-row tiles (prefills of 65+ rows, im2col convolutions): waves split K inside the workgroup (nw4), the
+      // column tiles per workgroup share each X read; fo_gemm_tune forces (waves, tiles) for sweeps
+      int nw4 = nw_pref4 ? nw_pref4 : 4;
+      if (g_force_nw) nw4 = g_force_nw;
+#define FO_B4(NT_, NW_, SW_) launch_gemm<NT_, 4, NW_, 2, SW_>(wstream, x_f32, grid, a, stream)
+      if (swiglu) {
+        if (NT == 8) FO_B4(8, 4, true);
+        else if (NT == 4) { if (nw4 >= 8) FO_B4(4, 8, true); else FO_B4(4, 4, true); }
+        else { if (nw4 >= 16) FO_B4(2, 16, true); else if (nw4 == 8) FO_B4(2, 8, true); else FO_B4(2, 4, true); }
+      } else if (NT == 8) FO_B4(8, 4, false);
+      else if (NT == 4) { if (nw4 >= 8) FO_B4(4, 8, false); else FO_B4(4, 4, false); }
+      else if (NT == 2) { if (nw4 >= 16) FO_B4(2, 16, false); else if (nw4 == 8) FO_B4(2, 8, false); else FO_B4(2, 4, false); }
+      else { if (nw4 >= 16) FO_B4(1, 16, false); else if (nw4 == 8) FO_B4(1, 8, false); else FO_B4(1, 4, false); }
+#undef FO_B4
     } else {
       if (swiglu) launch_gemm<2, 4, 4, 4, true>(wstream, x_f32, grid, a, stream);
       else if (NT == 4) launch_gemm<4, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
