@@ -1321,13 +1321,21 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     NT = g_force_nt;
     if (swiglu && NT < 2) NT = 2;
     if (a.ntiles % NT) NT = swiglu ? 2 : 1;
-  } else if (RB == 4 && !swiglu && mt >= 4 && a.ntiles % 4 == 0 && a.ntiles >= 64) {
-    // many row tiles (im2col convolutions, long prefills): X traffic (fp32, re-read by every column
-    // group) dominates the weights', so 4 column tiles share each X read; long K is split over
-    // workgroups until the grid covers the chip
-    NT = 4;
-    const int wg = a.ntiles / 4 * mt;
-    if (wg < 256 && KS >= 128) S_auto = KS >= 256 ? 4 : 2;
+  } else if (RB == 4 && !mid && x_f32 && !lnw && M > 64) {
+    // 64-row tiles (prefills of 65+ rows: the AR decoder's sentence prefill at 8 sessions x 32-40 sub-token rows, the
+    // speech encoder's im2col convolutions).  Measured (scripts/gemm_big_sweep.py, profiles/r04q_gemm_big_sweep.txt):
+    // 8 waves splitting K inside the workgroup everywhere but the K = 32 conv1 (4); 4 column tiles per X read when
+    // that still gives >= 128 workgroups or K is long (then split K over workgroups until the grid nears 256); else
+    // one tile (pair) per workgroup.  AR prefill down 67.8 -> 26.3 us, gate/up 56.2 -> 40.3 us, q|k|v 20.3 -> 16.4,
+    // o 12.2 -> 10.4; conv2 130.9 -> 96.8 us, conv1 28.5 -> 15.3 us
+    nw_pref4 = KS <= 2 ? 4 : 8;
+    const int wg4 = a.ntiles / 4 * mt;
+    if (a.ntiles % 4 == 0 && KS > 2 && (wg4 >= 128 || KS >= 128)) {
+      NT = 4;
+      if (KS >= 128) S_auto = wg4 * 4 <= 256 ? 4 : (wg4 * 2 <= 256 ? 2 : 1);
+    } else {
+      NT = swiglu ? 2 : 1;
+    }
   }
   // the epilogue rotates the (i, i + hd/2) tile pair a workgroup holds; a 17..64-row RoPE projection on large
   // weights (the Qwen2 q|k|v of a duplex tick or a prefill) keeps the 4-tile column groups of the plain path and
