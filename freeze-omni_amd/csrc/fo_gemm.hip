@@ -1327,12 +1327,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     // 8 waves splitting K inside the workgroup everywhere but the K = 32 conv1 (4); 4 column tiles per X read when
     // that still gives >= 128 workgroups or K is long (then split K over workgroups until the grid nears 256); else
     // one tile (pair) per workgroup.  AR prefill down 67.8 -> 26.3 us, gate/up 56.2 -> 40.3 us, q|k|v 20.3 -> 16.4,
-    // o 12.2 -> 10.4; conv2 130.9 -> 96.8 us, conv1 28.5 -> 15.3 us
+    // o 12.2 -> 10.4; conv2 130.9 -> 89.6 us, conv1 28.5 -> 15.3 us
     nw_pref4 = KS <= 2 ? 4 : 8;
     const int wg4 = a.ntiles / 4 * mt;
     if (a.ntiles % 4 == 0 && KS > 2 && (wg4 >= 128 || KS >= 128)) {
       NT = 4;
-      if (KS >= 128) S_auto = wg4 * 4 <= 256 ? 4 : (wg4 * 2 <= 256 ? 2 : 1);
+      if (KS >= 128) S_auto = (KS >= 256 || wg4 * 4 <= 256) ? 4 : (wg4 * 2 <= 256 ? 2 : 1);
     } else {
       NT = swiglu ? 2 : 1;
     }
