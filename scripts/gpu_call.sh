@@ -13,6 +13,7 @@
 #   steptrace  per-node timeline of the AR decode step (kernel trace)   -> <tag>_step_timeline.txt
 #   duplex     the config-5 duplex line                                  -> <tag>_duplex.json
 #   profdup    rocprofv3 kernel trace + stats of a 20 s duplex run       -> <tag>_profdup/, <tag>_profdup_table.txt
+#   profstage  rocprofv3 kernel trace of scripts/llm_stage_time.py (LLM / encoder stage replays) -> <tag>_profstage_table.txt
 #   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
 #   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
 #   ab         ENV_A / ENV_B (e.g. 'FO_X=0') alternated twice on the quick bench -> <tag>_ab.txt
@@ -54,6 +55,9 @@ for S in "$@"; do
     profdup) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_profdup -o duplex -f csv -- \
              python3 $ROOTD/bench.py --scenario duplex --duplex-sec 20 --steps 1 --warmup 1) > ${O}_profdup.log 2>&1; rc=$?
              [ $rc -eq 0 ] && python3 scripts/trace_table.py ${O}_profdup 40 duplex > ${O}_profdup_table.txt 2>&1; cat ${O}_profdup_table.txt | head -45 ;;
+    profstage) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_profstage -o stage -f csv -- \
+             python3 $ROOTD/scripts/llm_stage_time.py) > ${O}_profstage.log 2>&1; rc=$?
+             [ $rc -eq 0 ] && python3 scripts/trace_table.py ${O}_profstage 45 stage > ${O}_profstage_table.txt 2>&1; head -48 ${O}_profstage_table.txt ;;
     text)  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_text -o text -f csv -- \
              python3 $ROOTD/scripts/text_step_time.py) > ${O}_prof_text.log 2>&1; rc=$? ;;
     duplex) timeout -k 10 400 python -u bench.py --scenario duplex --out ${O}_duplex.json > ${O}_duplex.log 2>&1; rc=$?
