@@ -182,6 +182,9 @@ __device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
 }
 
 // NT packed 16-column tiles per workgroup (SW: NT/2 interleaved gate/up pairs -> NT/2 output tiles)
+// zero words a lane loads instead of an operand that does not exist (branch-free prologues)
+__device__ float g_zeros[4];
+
 template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false, bool PIPE = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
@@ -202,72 +205,78 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       a.trc ? a.trc + (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 24 : nullptr;
   if (trc && threadIdx.x == 0) trc[0] = wall_clock64();
 
-  // Epilogue operands prefetched before the weight stream when every output element of the workgroup
-  // has its own thread (the small-M, latency-bound shapes): the residual, bias and next-norm gamma (plain
-  // path) or the token's slot / position, its cos / sin and the q|k|v bias (RoPE path) arrive while the
-  // weights stream, instead of costing one or two dependent memory round trips after the K reduction.
+  // Epilogue operands prefetched when every output element of the workgroup has its own thread (the small-M,
+  // latency-bound shapes): the residual, bias and next-norm gamma (plain path) or the token's slot / position,
+  // its cos / sin and the q|k|v bias (RoPE path) arrive while the weights stream, instead of costing one or two
+  // dependent memory round trips after the K reduction.  Ordering matters because a wave's vector-memory
+  // counter retires in issue order: the independent operands (level 1) and the RMSNorm partial sums are
+  // issued first, then the wave's first group of weights and X, and only then the loads whose ADDRESS needs a
+  // level-1 value (cos / sin at the token's position, level 2) -- so no wait in the prologue ever waits for
+  // the weight stream, and the weight stream never waits for a prologue round trip.
   constexpr int LT = SW ? NT / 2 : NT;  // logical output tiles
   constexpr bool EPRE = !SW && !LN && NT <= 2 && LT * ROWS * 16 <= NTH;
   const int ee = threadIdx.x;
   const int e_lt = ee / (ROWS * 16), e_rr = (ee >> 4) % ROWS, e_c = ee & 15;
   float p_res = 0.f, p_bias = 0.f, p_b2 = 0.f, p_cos = 1.f, p_sin = 0.f, p_gn = 0.f;
-  int p_slot = 0;
+  bf16_t p_resh = f2bf(0.f);   // bf16 residual: raw bits, converted in the epilogue (no wait in the prologue)
+  int p_slot = 0, p_pos = 0;
   const bool e_rope = (NT == 2 && !SW) && a.rq != nullptr;
   // split over K with the in-launch merge (fo_gemm passes counters only for plain tiles): any split may be
   // the last to arrive, so every split prefetches the epilogue operands
   const bool merge = !SW && !LN && a.S > 1 && a.counters != nullptr;
-  if constexpr (EPRE) {
-    if ((a.S == 1 || merge) && ee < LT * ROWS * 16) {
-      const int m = m0 + e_rr;
-      if (e_rope) {
-        if (ee < ROWS * 16 && m < a.M) {
-          const int n = rope_col(a, tg, e_c), half = a.rhd >> 1;
-          const int h = n / a.rhd, i = n - h * a.rhd;
-          p_slot = a.rslot[m];
-          if (a.bias) {
-            p_bias = a.bias[n];
-            p_b2 = a.bias[n + half];
-          }
-          if (h < a.rH + a.rKVH) {
-            const int p = a.rpos[m];
-            p_cos = a.rcos[(size_t)p * half + i];
-            p_sin = a.rsin[(size_t)p * half + i];
-          }
-        }
-      } else {
-        const int n = (tg * LT + e_lt) * 16 + e_c;
-        if (m < a.M && n < a.N) {
-          const size_t o = (size_t)m * a.ldy + n;
-          if (a.residual) p_res = a.out_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(a.Y)[o])
-                                             : reinterpret_cast<const float*>(a.Y)[o];
-          if (a.bias) p_bias = a.bias[n];
-        }
-      }
-    }
-    if ((a.S == 1 || merge) && !e_rope && a.yg) {
-      const int n0 = tg * LT * 16;
-      if (lane < min(LT * 16, a.N - n0)) p_gn = a.gnext[n0 + lane];
-    }
+  // level 1 is branch-free: a lane whose operand does not exist loads a zero word instead (g_zeros), so no
+  // divergent branch leaves a register with a pending load that a later write would have to wait for
+  bool p_rot = false;   // this lane's output column is a rotated q / k column (level 2 loads its cos / sin)
+  if constexpr (EPRE) {   // straight-line code: every operand load is issued, from g_zeros when it does not apply
+    const bool on = (a.S == 1 || merge) && ee < LT * ROWS * 16;
+    const int m = m0 + e_rr;
+    const float* z = g_zeros;
+    const int rhd = e_rope ? a.rhd : 32;   // (no division by a zero head size on the plain path)
+    const int half = rhd >> 1;
+    const int nrope = (tg / (rhd >> 5)) * rhd + (tg % (rhd >> 5)) * 16 + e_c;   // rope_col
+    const int nplain = (tg * LT + e_lt) * 16 + e_c;
+    const bool okr = e_rope && on && ee < ROWS * 16 && m < a.M;
+    const bool okp = !e_rope && on && m < a.M && nplain < a.N;
+    p_rot = okr && nrope / rhd < a.rH + a.rKVH;
+    const size_t o = (size_t)m * a.ldy + nplain;
+    p_slot = *(okr ? a.rslot + m : reinterpret_cast<const int*>(z));
+    p_pos = *(p_rot ? a.rpos + m : reinterpret_cast<const int*>(z));
+    p_bias = *(a.bias && (okr || okp) ? a.bias + (e_rope ? nrope : nplain) : z);
+    p_b2 = *(a.bias && okr ? a.bias + nrope + half : z);
+    p_resh = *(okp && a.residual && a.out_bf16 ? reinterpret_cast<const bf16_t*>(a.Y) + o
+                                                : reinterpret_cast<const bf16_t*>(z));
+    p_res = *(okp && a.residual && !a.out_bf16 ? reinterpret_cast<const float*>(a.Y) + o : z);
+    const int n0 = tg * LT * 16;
+    p_gn = *(!e_rope && a.yg && (a.S == 1 || merge) && lane < min(LT * 16, a.N - n0) ? a.gnext + n0 + lane : z);
   }
 
-  // post-scaled RMSNorm: prefetch the producer's partial sums of this workgroup's rows now, reduce
-  // them after the main loop (their latency hides behind the weight stream)
+  // post-scaled RMSNorm: the producer's partial sums of this workgroup's rows (the first 64 per row, one
+  // load per lane) are loaded now and reduced after the main loop (their latency hides behind the weight stream)
   constexpr int RPWV = (ROWS + NW - 1) / NW;  // rows per wave
   // wide variants are at the VGPR edge of their occupancy step: they load the partials after the loop
   constexpr bool RPRE = NT * U <= 8;
   float rpart[RPWV];
-  auto load_rpart = [&]() {
+  auto load_rpart = [&](int j0) {   // partial sums j0, j0 + 64, ... added to rpart
 #pragma unroll
     for (int i = 0; i < RPWV; ++i) {
       const int rr = wave + i * NW;
       const int m = min(m0 + rr, a.M - 1);
       float v = 0.f;
       if (rr < ROWS)
-        for (int j = lane; j < a.rgroups; j += 64) v += a.rstats[(size_t)m * a.rgroups + j];
-      rpart[i] = v;
+        for (int j = j0 + lane; j < a.rgroups; j += 64) v += a.rstats[(size_t)m * a.rgroups + j];
+      rpart[i] += v;
     }
   };
-  if (RPRE && a.rstats && !LN) load_rpart();
+#pragma unroll
+  for (int i = 0; i < RPWV; ++i) rpart[i] = 0.f;
+  if (RPRE && a.rstats && !LN) {
+#pragma unroll
+    for (int i = 0; i < RPWV; ++i) {
+      const int rr = wave + i * NW;
+      const int m = min(m0 + rr, a.M - 1);
+      rpart[i] = *(rr < ROWS && lane < a.rgroups ? a.rstats + (size_t)m * a.rgroups + lane : g_zeros);
+    }
+  }
 
   f32x4 acc[NT][RB];
 #pragma unroll
@@ -287,18 +296,52 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
   float ln_mu[RB], ln_rs[RB];
+  // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
+  // together); the < U leftover steps go one per wave, so no wave runs a serial tail.
+  const int G = len / U, rem = len - G * U;
+  const int gb = G * wave / NW, ge = G * (wave + 1) / NW;
+  // LayerNorm on load: the producer's partial row sums are loaded first, then the wave's first group of weight
+  // fragments and raw X rows, and only then does the wave wait for the sums (vmcnt retires in issue order, so
+  // loads issued after the sums do not delay them): the statistics round trip and barrier overlap the weight
+  // stream's first round trip instead of running before it
+  bf16x8 lnbv[LN ? U : 1][NT];
+  float4 lnxv[LN ? U : 1][RB][2];
+  auto ln_issue = [&](int ks) {
+    if constexpr (LN) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = min(ks + u, KS - 1);   // in bounds for a wave without a group (its loads go unused)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) lnbv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)k * 64);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
+          lnxv[u][r][0] = q[0];
+          lnxv[u][r][1] = q[1];
+        }
+      }
+    }
+  };
   if constexpr (LN) {
     // per-row mean / rstd of this workgroup's rows from the producer's partial sums
+    constexpr int LRPW = (ROWS + NW - 1) / NW;
     __shared__ float ln_s[2][ROWS];
-    for (int rr = wave; rr < ROWS; rr += NW) {
+    float st1[LRPW], st2[LRPW];
+#pragma unroll
+    for (int i = 0; i < LRPW; ++i) {
+      const int rr = wave + i * NW;
       const int m = min(m0 + rr, a.M - 1);
-      float s1 = 0.f, s2 = 0.f;
-      for (int j = lane; j < a.rgroups; j += 64) {
-        s1 += a.rstats1[(size_t)m * a.rgroups + j];
-        s2 += a.rstats[(size_t)m * a.rgroups + j];
-      }
-      const float mean = wave_sum(s1) / (float)a.K;
-      const float var = fmaxf(wave_sum(s2) / (float)a.K - mean * mean, 0.f);
+      const bool on = rr < ROWS && lane < a.rgroups;
+      st1[i] = on ? a.rstats1[(size_t)m * a.rgroups + lane] : 0.f;
+      st2[i] = on ? a.rstats[(size_t)m * a.rgroups + lane] : 0.f;
+    }
+    ln_issue(kb + min(gb, max(G - 1, 0)) * U);
+#pragma unroll
+    for (int i = 0; i < LRPW; ++i) {
+      const int rr = wave + i * NW;
+      if (rr >= ROWS) break;
+      const float mean = wave_sum(st1[i]) / (float)a.K;   // (fo_gemm_ln: at most 64 producer groups)
+      const float var = fmaxf(wave_sum(st2[i]) / (float)a.K - mean * mean, 0.f);
       if (lane == 0) {
         ln_s[0][rr] = mean;
         ln_s[1][rr] = 1.0f / sqrtf(var + a.lneps);
@@ -334,10 +377,55 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     }
   };
 
-  // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
-  // together); the < U leftover steps go one per wave, so no wave runs a serial tail.
-  const int G = len / U, rem = len - G * U;
-  const int gb = G * wave / NW, ge = G * (wave + 1) / NW;
+  // level-2 epilogue operands (see EPRE above): cos / sin at the token's position (p_rot: a rotated q / k
+  // column), issued once the wave's first group of weights is in flight
+  auto level2 = [&]() {
+    if constexpr (EPRE) {
+      if (e_rope) {
+        const int n = rope_col(a, tg, e_c), half = a.rhd >> 1;
+        const int i = n - (n / a.rhd) * a.rhd;
+        int pp = p_pos;
+        asm volatile("" : "+v"(pp));   // (keeps the position's use -- and its wait -- behind the weight issue)
+        const size_t o = (size_t)pp * half + i;
+        const float c = *(p_rot ? a.rcos + o : g_zeros), sn = *(p_rot ? a.rsin + o : g_zeros);
+        p_cos = p_rot ? c : 1.f;
+        p_sin = p_rot ? sn : 0.f;
+      }
+    }
+  };
+  if constexpr (LN) {
+    for (int g = gb; g < ge; ++g) {
+      const int ks = kb + g * U;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k0 = (ks + u) * 32 + 8 * (lane >> 4);
+        const float4 w0 = *reinterpret_cast<const float4*>(a.lnw + k0), w1 = *reinterpret_cast<const float4*>(a.lnw + k0 + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(a.lnb + k0), b1 = *reinterpret_cast<const float4*>(a.lnb + k0 + 4);
+        const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          if (r < rbeff) {
+            const float f[8] = {lnxv[u][r][0].x, lnxv[u][r][0].y, lnxv[u][r][0].z, lnxv[u][r][0].w,
+                                lnxv[u][r][1].x, lnxv[u][r][1].y, lnxv[u][r][1].z, lnxv[u][r][1].w};
+            bf16x8 hi, lo;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float v = (f[j] - ln_mu[r]) * ln_rs[r] * w[j] + b[j];
+              const __bf16 h = (__bf16)v;
+              hi[j] = h;
+              lo[j] = (__bf16)(v - (float)h);
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hi, lnbv[u][t], acc[t][r], 0, 0, 0);
+              acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lo, lnbv[u][t], acc[t][r], 0, 0, 0);
+            }
+          }
+      }
+      if (g + 1 < ge) ln_issue(ks + U);
+    }
+  } else
   if constexpr (PIPE && XF32 && !LN) {
     // Software-pipelined weight stream: group g + 1's weight fragments AND raw X rows are issued
     // before group g's MFMAs, so a wave always has one group of loads in flight while it computes
@@ -383,6 +471,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     };
     int g = gb;
     if (g < ge) issue(w0, x0, kb + g * U);
+    level2();
     for (; g + 1 < ge; g += 2) {
       issue(w1, x1, kb + (g + 1) * U);
       compute(w0, x0);
@@ -390,31 +479,86 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       compute(w1, x1);
     }
     if (g < ge) compute(w0, x0);
-  } else
-  for (int g = gb; g < ge; ++g) {
-    const int ks = kb + g * U;
-    bf16x8 bv[U][NT];
-    bf16x8 ah[U][RB], al[U][RB];
+  } else {
+    // the wave's FIRST group of weights and X goes into its own registers and is issued before the level-2
+    // epilogue loads (cos / sin, below), unconditionally -- a wave without a group loads another wave's first
+    // group again (same lines: L2 hits, no extra HBM bytes), so no wave-divergent branch or loop-carried
+    // register makes the compiler's vmcnt accounting wait for the weights in the prologue; the wave's further
+    // groups load at the top of their iteration
+    bf16x8 bv0[U][NT];
+    float4 xf0[XF32 ? U : 1][RB][2];
+    bf16x8 xb0[XF32 ? 1 : U][RB];
+    {
+      const int ks = kb + min(gb, max(G - 1, 0)) * U;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u) {
+        const int k = min(ks + u, KS - 1);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) bv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)(ks + u) * 64);
+        for (int t = 0; t < NT; ++t) bv0[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)k * 64);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+        for (int r = 0; r < RB; ++r) {
+          if constexpr (XF32) {
+            const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
+            xf0[u][r][0] = q[0];
+            xf0[u][r][1] = q[1];
+          } else {
+            xb0[u][r] = *reinterpret_cast<const bf16x8*>(xr[r] + (size_t)k * 32);
+          }
+        }
+      }
+    }
+    level2();
+    if (gb < ge) {
 #pragma unroll
-      for (int r = 0; r < RB; ++r)
-        if (r < rbeff) ldx(r, ks + u, ah[u][r], al[u][r]);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < RB; ++r)
           if (r < rbeff) {
-            acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[u][r], bv[u][t], acc[t][r], 0, 0, 0);
-            if constexpr (XF32)
-              acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+            bf16x8 hi, lo;
+            if constexpr (XF32) {
+              const float f[8] = {xf0[u][r][0].x, xf0[u][r][0].y, xf0[u][r][0].z, xf0[u][r][0].w,
+                                  xf0[u][r][1].x, xf0[u][r][1].y, xf0[u][r][1].z, xf0[u][r][1].w};
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const __bf16 h = (__bf16)f[j];
+                hi[j] = h;
+                lo[j] = (__bf16)(f[j] - (float)h);
+              }
+            } else {
+              hi = xb0[u][r];
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hi, bv0[u][t], acc[t][r], 0, 0, 0);
+              if constexpr (XF32) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lo, bv0[u][t], acc[t][r], 0, 0, 0);
+            }
           }
+    }
+    for (int g = gb + 1; g < ge; ++g) {
+      const int ks = kb + g * U;
+      bf16x8 bv[U][NT];
+      bf16x8 ah[U][RB], al[U][RB];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)(ks + u) * 64);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          if (r < rbeff) ldx(r, ks + u, ah[u][r], al[u][r]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < RB; ++r)
+            if (r < rbeff) {
+              acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+              if constexpr (XF32)
+                acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[u][r], bv[u][t], acc[t][r], 0, 0, 0);
+            }
+    }
   }
   for (int ks = kb + G * U + wave; ks < ke; ks += NW) {
 #pragma unroll
@@ -503,7 +647,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     __syncthreads();
   }
   if (a.rstats && !LN && (a.S == 1 || merge)) {  // (split without the merge: k_gemm_reduce scales the sums)
-    if (!RPRE) load_rpart();
+    if (!RPRE) load_rpart(0);
+    else if (a.rgroups > 64) load_rpart(64);
     __shared__ float rstd_s[ROWS];
 #pragma unroll
     for (int i = 0; i < RPWV; ++i) {
@@ -541,7 +686,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       if (m < a.M && n < a.N) {
         float v = red[0][e_lt][e_rr][e_c] + p_bias;
         if (a.scale) v = v * a.scale[n] + a.shift[n];
-        v = apply_act(v, a.act) + p_res;
+        float pr = p_res;
+        if (a.out_bf16) {   // (the barrier keeps the conversion, and its wait for the load, here)
+          unsigned rb = p_resh;
+          asm volatile("" : "+v"(rb));
+          pr = bf2f((bf16_t)rb);
+        }
+        v = apply_act(v, a.act) + pr;
         const size_t o = (size_t)m * a.ldy + n;
         if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(v);
         else reinterpret_cast<float*>(a.Y)[o] = v;
@@ -1176,7 +1327,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.trc = g_trc;
   FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
   if (lnw) {
-    FO_REQUIRE(lnb && x_f32 && M <= 64 && !swiglu && rstats && rstats1 && rgroups > 0 && !rope && ldx % 4 == 0,
+    FO_REQUIRE(lnb && x_f32 && M <= 64 && !swiglu && rstats && rstats1 && rgroups > 0 && rgroups <= 64 && !rope &&
+               ldx % 4 == 0,
                "fo_gemm_ln: fp32 X, M <= 64, producer statistics, plain epilogue only (M=%d K=%d)", M, K);
   }
   if (rope) {

@@ -80,8 +80,8 @@ for S in "$@"; do
                > ${O}_sweep_$k$i.log 2>&1 || { rc=$?; tail -20 ${O}_sweep_$k$i.log; break 2; }
              echo "$i [${SET[$k]:-default}] $(line ${O}_sweep_$k$i.log)" >> ${O}_sweep.txt
            done; done; cat ${O}_sweep.txt ;;
-    py:*)  timeout -k 10 200 python -u scripts/${S#py:} > ${O}_$(basename ${S#py:} .py | cut -d' ' -f1).log 2>&1; rc=$?
-           tail -40 ${O}_$(basename ${S#py:} .py | cut -d' ' -f1).log ;;
+    py:*)  P=${S#py:}; L=${O}_$(basename ${P%% *} .py).log
+           timeout -k 10 200 python -u scripts/$P > $L 2>&1; rc=$?; tail -40 $L ;;
     *) echo "unknown step $S"; rc=1 ;;
   esac
   echo "step $S rc $rc" >&2
