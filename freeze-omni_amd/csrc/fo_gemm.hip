@@ -746,20 +746,43 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
   const int m = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
-  // epilogue operands first: their loads overlap the statistics and slab loads below instead of
-  // costing dependent round trips after the sum
-  float p_res = 0.f, p_bias = 0.f, p_gn = 0.f;
-  if (!a.rq && !sw && n < a.N) {
-    const size_t o = (size_t)m * a.ldy + n;
-    if (a.residual) p_res = a.out_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(a.Y)[o]) : reinterpret_cast<const float*>(a.Y)[o];
-    if (a.bias) p_bias = a.bias[n];
-    if (a.yg) p_gn = a.gnext[n];
+  // Every load of the launch is issued up front -- up to 8 slabs' partials, the epilogue operands and the
+  // producer's RMSNorm partial sums -- so the kernel pays ONE dependent memory round trip before its sum
+  // (the slabs are still summed in slab order: the same result bit for bit).  The epilogue operand loads are
+  // branch-free (g_zeros when an operand does not apply), so no divergent branch makes the compiler's vmcnt
+  // accounting wait early.
+  constexpr int SQ = 8;
+  const bool rope = a.rq != nullptr;
+  const int ncol = rope ? a.N / 2 : a.N;
+  const bool live = n < ncol;
+  const int col = rope ? (n >> 4) * 32 + (n & 15) : (sw ? (n >> 4) * 32 + (n & 15) : n);
+  const bool pair = rope || sw;   // two partial columns per thread (the tile pair / gate-up pair, 16 apart)
+  const float* p = a.ws + (size_t)m * Ncols + (live ? col : 0);
+  float tv[SQ], tu[SQ];
+#pragma unroll
+  for (int j = 0; j < SQ; ++j) {
+    tv[j] = 0.f;
+    tu[j] = 0.f;
+    if (j < a.S) {
+      tv[j] = p[j * slab];
+      if (pair) tu[j] = p[j * slab + 16];
+    }
   }
+  const float* z = g_zeros;
+  const bool plain = !rope && !sw && live;
+  const size_t o = (size_t)m * a.ldy + n;
+  bf16_t p_resh = *(plain && a.residual && a.out_bf16 ? reinterpret_cast<const bf16_t*>(a.Y) + o
+                                                      : reinterpret_cast<const bf16_t*>(z));
+  const float p_res = *(plain && a.residual && !a.out_bf16 ? reinterpret_cast<const float*>(a.Y) + o : z);
+  const float p_bias = *(plain && a.bias ? a.bias + n : z);
+  const float p_gn = *(plain && a.yg ? a.gnext + n : z);
+  const bool rms = a.rstats && !a.lnw;   // RMSNorm consumer split over K: the row's rstd scales the summed partials
+  const float st = *(rms && threadIdx.x < 64 && threadIdx.x < a.rgroups ? a.rstats + (size_t)m * a.rgroups + threadIdx.x : z);
   float rs = 1.f;
-  if (a.rstats && !a.lnw) {  // RMSNorm consumer split over K: the row's rstd scales the summed partials
+  if (rms) {
     if (threadIdx.x < 64) {  // lane-strided + wave_sum: the order gemm_body's unsplit path uses
-      float ss = 0.f;
-      for (int j = threadIdx.x; j < a.rgroups; j += 64) ss += a.rstats[(size_t)m * a.rgroups + j];
+      float ss = st;
+      for (int j = threadIdx.x + 64; j < a.rgroups; j += 64) ss += a.rstats[(size_t)m * a.rgroups + j];
       ss = wave_sum(ss);
       if (threadIdx.x == 0) red_s[0] = rsqrtf(ss / (float)a.K + a.reps);
     }
@@ -767,69 +790,47 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
     rs = red_s[0];
     __syncthreads();
   }
-  if (a.rq) {  // rope: one thread per column pair, packed tiles (2P, 2P + 1)
-    if (n < a.N / 2) {
-      const int P = n >> 4, c = n & 15;
-      float x1 = 0.f, x2 = 0.f;
-      const float* p = a.ws + (size_t)m * Ncols + P * 32 + c;
-      for (int q0 = 0; q0 < a.S; q0 += 4) {  // four slabs' loads in flight, summed in slab order
-        float t1[4], t2[4];
+  float v = 0.f, u = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (q0 + j < a.S) {
-            t1[j] = p[(q0 + j) * slab];
-            t2[j] = p[(q0 + j) * slab + 16];
-          }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (q0 + j < a.S) {
-            x1 += t1[j];
-            x2 += t2[j];
-          }
-      }
-      rope_store(a, m, rope_col(a, P, c), x1 * rs, x2 * rs);
+  for (int j = 0; j < SQ; ++j)
+    if (j < a.S) {
+      v += tv[j];
+      u += tu[j];
     }
+  for (int q = SQ; q < a.S; ++q) {   // more than 8 slabs (not used by the policies in fo_gemm)
+    v += p[q * slab];
+    if (pair) u += p[q * slab + 16];
+  }
+  if (rope) {  // one thread per column pair, packed tiles (2P, 2P + 1)
+    if (live) rope_store(a, m, rope_col(a, n >> 4, n & 15), v * rs, u * rs);
     return;
   }
   float y = 0.f;
-  if (n < a.N) {
-    const int col = sw ? (n >> 4) * 32 + (n & 15) : n;
-    float v = 0.f, u = 0.f;
-    const float* p = a.ws + (size_t)m * Ncols + col;
-    for (int q0 = 0; q0 < a.S; q0 += 4) {  // four slabs' loads in flight (one round trip, not four), summed in
-      float tv[4], tu[4];                   // slab order: the same result bit for bit
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (q0 + j < a.S) {
-          tv[j] = p[(q0 + j) * slab];
-          tu[j] = sw ? p[(q0 + j) * slab + 16] : 0.f;
-        }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (q0 + j < a.S) {
-          v += tv[j];
-          if (sw) u += tu[j];
-        }
-    }
+  if (live) {
     if (sw) {
       y = epilogue_store(a, true, m, n, v * rs, u * rs);
     } else {
       y = v * rs + p_bias;
       if (a.scale) y = y * a.scale[n] + a.shift[n];
-      y = apply_act(y, a.act) + p_res;
-      const size_t o = (size_t)m * a.ldy + n;
+      float pr = p_res;
+      if (a.out_bf16) {   // (the barrier keeps the conversion, and its wait for the load, here)
+        unsigned rb = p_resh;
+        asm volatile("" : "+v"(rb));
+        pr = bf2f((bf16_t)rb);
+      }
+      y = apply_act(y, a.act) + pr;
       if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(y);
       else reinterpret_cast<float*>(a.Y)[o] = y;
     }
   }
   if (a.sout && !sw) {
-    const float ss = block_sum<4>(n < a.N ? y * y : 0.f, red_s);
+    const float ss = block_sum<4>(live ? y * y : 0.f, red_s);
     if (threadIdx.x == 0) a.sout[(size_t)m * gridDim.x + blockIdx.x] = ss;
     if (a.sout1) {
-      const float s1 = block_sum<4>(n < a.N ? y : 0.f, red_s);
+      const float s1 = block_sum<4>(live ? y : 0.f, red_s);
       if (threadIdx.x == 0) a.sout1[(size_t)m * gridDim.x + blockIdx.x] = s1;
     }
-    if (a.yg && n < a.N) a.yg[(size_t)m * a.ldy + n] = y * p_gn;
+    if (a.yg && live) a.yg[o] = y * p_gn;
   }
 }
 
