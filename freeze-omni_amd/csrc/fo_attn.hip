@@ -300,26 +300,60 @@ __global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq,
   const int st = start[b];
   const int ps = pstart[b];
   const int D4 = dk / 4;
-  for (int e = threadIdx.x; e < Lk * D4; e += blockDim.x) {
-    const int j = e / D4, c = (e % D4) * 4;
-    const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
-    float4 kk, vv;
-    if (j < Lold) {
-      kk = *reinterpret_cast<const float4*>(kr + ro);
-      vv = *reinterpret_cast<const float4*>(vr + ro);
-    } else {
-      const float* src = qkv + ((size_t)b * T + (j - Lold)) * ldq + hh * dk + c;
-      kk = *reinterpret_cast<const float4*>(src + d);
-      vv = *reinterpret_cast<const float4*>(src + 2 * d);
-      *reinterpret_cast<float4*>(kr + ro) = kk;
-      *reinterpret_cast<float4*>(vr + ro) = vv;
-    }
-    *reinterpret_cast<float4*>(k_s + j * KP + c) = kk;
-    *reinterpret_cast<float4*>(v_s + j * KP + c) = vv;
-    *reinterpret_cast<float4*>(p_s + j * KP + c) =
-        *reinterpret_cast<const float4*>(ptab + (size_t)(ps + j) * d + hh * dk + c);
+  // staging: each thread's key / value / position rows (up to RB_ per batch) are all loaded before any of them
+  // is stored to LDS -- one dependent memory round trip per batch instead of one per row (a chunk's new rows come
+  // from the q|k|v output through the same branch-free loads and are then appended to the ring)
+  constexpr int RB_ = 8;
+  // the chunk's query rows (+ the u / v position biases), at most 2 per thread, ride in the first batch
+  float qx[2], qbu[2], qbv[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int e = threadIdx.x + r * 256;
+    const int i = e < T * dk ? e / dk : 0, c = e < T * dk ? e % dk : 0;
+    qx[r] = qkv[((size_t)b * T + i) * ldq + hh * dk + c];
+    qbu[r] = bu[hh * dk + c];
+    qbv[r] = bv[hh * dk + c];
   }
-  for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+  for (int e0 = 0; e0 < Lk * D4; e0 += RB_ * 256) {
+    typedef float v4f __attribute__((ext_vector_type(4)));   // (a native vector: the arrays stay in VGPRs)
+    v4f kk[RB_], vv[RB_], pp[RB_];
+#pragma unroll
+    for (int q = 0; q < RB_; ++q) {
+      const int e = e0 + q * 256 + threadIdx.x;
+      const bool on = e < Lk * D4;
+      const int j = on ? e / D4 : 0, c = on ? (e % D4) * 4 : 0;
+      const bool old_row = j < Lold;
+      const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
+      const float* src = qkv + ((size_t)b * T + (old_row ? 0 : j - Lold)) * ldq + hh * dk + c;
+      kk[q] = *reinterpret_cast<const v4f*>(old_row ? kr + ro : src + d);
+      vv[q] = *reinterpret_cast<const v4f*>(old_row ? vr + ro : src + 2 * d);
+      pp[q] = *reinterpret_cast<const v4f*>(ptab + (size_t)(ps + j) * d + hh * dk + c);
+    }
+#pragma unroll
+    for (int q = 0; q < RB_; ++q) {
+      const int e = e0 + q * 256 + threadIdx.x;
+      if (e < Lk * D4) {
+        const int j = e / D4, c = (e % D4) * 4;
+        if (j >= Lold) {   // the chunk's new rows enter the ring
+          const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
+          *reinterpret_cast<v4f*>(kr + ro) = kk[q];
+          *reinterpret_cast<v4f*>(vr + ro) = vv[q];
+        }
+        *reinterpret_cast<v4f*>(k_s + j * KP + c) = kk[q];
+        *reinterpret_cast<v4f*>(v_s + j * KP + c) = vv[q];
+        *reinterpret_cast<v4f*>(p_s + j * KP + c) = pp[q];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int e = threadIdx.x + r * 256;
+    if (e < T * dk) {
+      qu[e] = qx[r] + qbu[r];
+      qv[e] = qx[r] + qbv[r];
+    }
+  }
+  for (int e = threadIdx.x + 512; e < T * dk; e += blockDim.x) {   // (T * dk > 512: not used at dk 64, T <= 8)
     const int i = e / dk, c = e % dk;
     const float x = qkv[((size_t)b * T + i) * ldq + hh * dk + c];
     qu[i * dk + c] = x + bu[hh * dk + c];

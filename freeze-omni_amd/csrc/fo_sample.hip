@@ -558,7 +558,7 @@ __global__ __launch_bounds__(1024) void k_sample(const float* logits, int ld, in
       int keep = 1;
       float z = 1.f;
       if (k > 1) {
-        float p[KMAXS];
+        float* p = sm.bv + 1024 - KMAXS;   // (LDS, free after the arg-max passes: a per-thread array would live in scratch)
         z = 0.f;
         for (int q = 0; q < k; ++q) {  // softmax over the (sorted) top-k = renormalised top-k probs
           p[q] = expf((sm.tv[q] - sm.tv[0]) / T);
