@@ -172,6 +172,7 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
 #pragma unroll
     for (int w = 0; w < DEC_NW; ++w) o += acc_s[w][d];
     orow[d] = o / sum;
+    if (a.oph) xpack_store(a.oph, a.opl, t0, h * HD + d, o / sum);
   }
 }
 
@@ -414,6 +415,9 @@ inline int attn_waves() {
   return g_attn_nw;
 }
 
+thread_local uint16_t* g_oph = nullptr;   // fo_attention_set_opack: the next launch's packed output
+thread_local uint16_t* g_opl = nullptr;
+
 inline int grid_for(long long n) {
   long long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -422,6 +426,13 @@ inline int grid_for(long long n) {
 }  // namespace
 
 extern "C" {
+
+int fo_attention_set_opack(void* hi, void* lo) {
+  FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_attention_set_opack: both halves or neither");
+  g_oph = reinterpret_cast<uint16_t*>(hi);
+  g_opl = reinterpret_cast<uint16_t*>(lo);
+  return 0;
+}
 
 int fo_attn_nsplit(int max_keys, int n_items, int KVH) {
   // enough work groups to cover the chip (~2 per CU) while every split keeps >= one 64-key tile
@@ -461,8 +472,12 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
-             tickets, keys_per_split, items ? 1 : T / n_items};
-  if (max_rows == 1 && (long long)maxb * PS <= DEC_MAXK) {  // one query row per (session, head): decode kernel
+             tickets, keys_per_split, items ? 1 : T / n_items, g_oph, g_opl};
+  g_oph = g_opl = nullptr;   // one launch
+  const bool dec = max_rows == 1 && (long long)maxb * PS <= DEC_MAXK;
+  FO_REQUIRE(!a.oph || (T <= 16 && (dec || nsplit == 1 || tickets)),
+             "fo_attention: packed output needs <= 16 tokens and no combine launch");
+  if (dec) {  // one query row per (session, head): decode kernel
     dim3 g1(n_items, H);
     if (hd == 128) hipLaunchKernelGGL((k_attn_decode<128>), g1, dim3(DEC_NT), 0, s, a);
     else if (hd == 64) hipLaunchKernelGGL((k_attn_decode<64>), g1, dim3(DEC_NT), 0, s, a);

@@ -39,6 +39,16 @@ int check_launch(const char* what);
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
+// Packed fp32 activations for the <= 16-row GEMMs: element (m < 16, n) of an fp32 matrix as bf16 hi + lo (the
+// split a GEMM would do on load: hi = bf16(v), lo = bf16(v - hi)) at its MFMA A-fragment position: k-step n / 32,
+// lane 16 (n % 32 / 8) + m, element n % 8 of the lane's 8.  [K/32][64][8] bf16 per half.
+__device__ __forceinline__ void xpack_store(uint16_t* hp, uint16_t* lp, int m, int n, float v) {
+  const int c = n & 31;
+  const size_t o = ((size_t)((n >> 5) * 64 + ((c >> 3) << 4) + m)) * 8 + (c & 7);
+  const __bf16 h = (__bf16)v;
+  hp[o] = __builtin_bit_cast(uint16_t, h);
+  lp[o] = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));
+}
 // round-to-nearest-even f32 -> bf16 (NaN kept NaN)
 __device__ __forceinline__ bf16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);

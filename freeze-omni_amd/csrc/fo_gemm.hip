@@ -69,6 +69,14 @@ struct GemmArgs {
   float* sout1;          // producer: [M][groups] partial sums of Y (with sout: LayerNorm statistics)
   const float* rstats1;  // LayerNorm consumer: the producer's partial sums (rstats: sums of squares)
   unsigned long long* trc;  // probes only (fo_gemm_set_trace): per-workgroup wall clocks, 24 slots
+  // fp32 X of <= 16 rows already split into bf16 hi / lo in MFMA A-fragment order ([K/32][64 lanes][8], lane l =
+  // row l & 15, columns 8 (l >> 4) .. + 8 of the k-step): a wave's X fragment is one contiguous 1 KiB read per half
+  // instead of 16 row segments per float4 (one-row-tile grid kernels only; nullptr: plain fp32 X)
+  const bf16x8* xph;
+  const bf16x8* xpl;
+  // producer of a next-norm input (yg): rows < 16 of yg also written packed the same way (fo_gemm_set_ypack)
+  bf16_t* ypkh;
+  bf16_t* ypkl;
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -185,7 +193,7 @@ __device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
 // zero words a lane loads instead of an operand that does not exist (branch-free prologues)
 __device__ float g_zeros[4];
 
-template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false, bool PIPE = false>
+template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false, bool PIPE = false, bool XPK = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
   static_assert(!LN || XF32, "LayerNorm on load needs fp32 X");
@@ -295,6 +303,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     if (row > a.M - 1) row = a.M - 1;  // clamp: rows >= M are computed but never stored
     xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
+  // X given packed (GemmArgs::xph / xpl): only the k_gemm_xp instantiations read it (the others compile as before)
+  static_assert(!XPK || (RB == 1 && XF32 && !LN && !SW && !PIPE), "packed X: one-row-tile plain / RoPE kernels");
+  const bool xpk = XPK && a.xph != nullptr;
   float ln_mu[RB], ln_rs[RB];
   // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
   // together); the < U leftover steps go one per wave, so no wave runs a serial tail.
@@ -373,7 +384,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         lo[j] = (__bf16)(v - (float)h);
       }
     } else {
-      load_x<XT, XF32>(xr[r] + (size_t)ks * 32, hi, lo);
+      if (XF32 && xpk) {
+        hi = a.xph[(size_t)ks * 64 + lane];
+        lo = a.xpl[(size_t)ks * 64 + lane];
+      } else {
+        load_x<XT, XF32>(xr[r] + (size_t)ks * 32, hi, lo);
+      }
     }
   };
 
@@ -498,9 +514,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           if constexpr (XF32) {
-            const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
-            xf0[u][r][0] = q[0];
-            xf0[u][r][1] = q[1];
+            if (xpk) {
+              xf0[u][r][0] = __builtin_bit_cast(float4, a.xph[(size_t)k * 64 + lane]);
+              xf0[u][r][1] = __builtin_bit_cast(float4, a.xpl[(size_t)k * 64 + lane]);
+            } else {
+              const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
+              xf0[u][r][0] = q[0];
+              xf0[u][r][1] = q[1];
+            }
           } else {
             xb0[u][r] = *reinterpret_cast<const bf16x8*>(xr[r] + (size_t)k * 32);
           }
@@ -516,13 +537,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
           if (r < rbeff) {
             bf16x8 hi, lo;
             if constexpr (XF32) {
-              const float f[8] = {xf0[u][r][0].x, xf0[u][r][0].y, xf0[u][r][0].z, xf0[u][r][0].w,
-                                  xf0[u][r][1].x, xf0[u][r][1].y, xf0[u][r][1].z, xf0[u][r][1].w};
+              if (xpk) {
+                hi = __builtin_bit_cast(bf16x8, xf0[u][r][0]);
+                lo = __builtin_bit_cast(bf16x8, xf0[u][r][1]);
+              } else {
+                const float f[8] = {xf0[u][r][0].x, xf0[u][r][0].y, xf0[u][r][0].z, xf0[u][r][0].w,
+                                    xf0[u][r][1].x, xf0[u][r][1].y, xf0[u][r][1].z, xf0[u][r][1].w};
 #pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const __bf16 h = (__bf16)f[j];
-                hi[j] = h;
-                lo[j] = (__bf16)(f[j] - (float)h);
+                for (int j = 0; j < 8; ++j) {
+                  const __bf16 h = (__bf16)f[j];
+                  hi[j] = h;
+                  lo[j] = (__bf16)(f[j] - (float)h);
+                }
               }
             } else {
               hi = xb0[u][r];
@@ -726,7 +752,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         const float v = c < cnt ? red[0][c >> 4][rr][c & 15] : 0.f;
         sq += v * v;
         sm += v;
-        if (a.yg && c < cnt) a.yg[(size_t)m * a.ldy + n0 + c] = v * (EPRE ? p_gn : a.gnext[n0 + c]);
+        if (a.yg && c < cnt) {
+          const float vg = v * (EPRE ? p_gn : a.gnext[n0 + c]);
+          a.yg[(size_t)m * a.ldy + n0 + c] = vg;
+          if (a.ypkh && m < 16) xpack_store(a.ypkh, a.ypkl, m, n0 + c, vg);
+        }
       }
       const float ss = wave_sum(sq);
       if (lane == 0) a.sout[(size_t)m * gridDim.x + tg] = ss;
@@ -830,7 +860,11 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       const float s1 = block_sum<4>(live ? y : 0.f, red_s);
       if (threadIdx.x == 0) a.sout1[(size_t)m * gridDim.x + blockIdx.x] = s1;
     }
-    if (a.yg && live) a.yg[o] = y * p_gn;
+    if (a.yg && live) {
+      const float vg = y * p_gn;
+      a.yg[o] = vg;
+      if (a.ypkh && m < 16) xpack_store(a.ypkh, a.ypkl, m, n, vg);
+    }
   }
 }
 
@@ -845,6 +879,11 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_wstream(GemmArgs a) {
 template <int NT, int RB, int NW, int U, bool SW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_wpipe(GemmArgs a) {
   gemm_body<NT, RB, true, NW, U, SW, false, true>(a);
+}
+// one-row-tile fp32-X GEMM reading X packed by its producer (GemmArgs::xph / xpl, ops.XPack)
+template <int NT, int NW, int U>
+__global__ __launch_bounds__(NW * 64) void k_gemm_xp(GemmArgs a) {
+  gemm_body<NT, 1, true, NW, U, false, false, false, true>(a);
 }
 
 // Software-pipelined one-row-tile fp32-X weight stream (k_gemm_wpipe).  Mode: 0 = plain loops
@@ -868,6 +907,12 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
 template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
   const size_t shm = 0;
+  if constexpr (RB == 1 && !SW) {
+    if (x_f32 && a.xph && !g_launch_pipe) {   // X packed by its producer
+      hipLaunchKernelGGL((k_gemm_xp<NT, NW, U>), grid, dim3(NW * 64), shm, s, a);
+      return;
+    }
+  }
   if constexpr (RB == 1) {
     if (x_f32 && g_launch_pipe) {
       if (g_launch_pipe == 2) hipLaunchKernelGGL((k_gemm_wpipe<NT, RB, NW, 2, SW>), grid, dim3(NW * 64), shm, s, a);
@@ -885,6 +930,10 @@ void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStre
 }
 
 thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
+thread_local const void* g_xph = nullptr;           // fo_gemm_set_xpack: the next launch's packed X
+thread_local const void* g_xpl = nullptr;
+thread_local void* g_ypkh = nullptr;                // fo_gemm_set_ypack: the next launch's packed yg output
+thread_local void* g_ypkl = nullptr;
 
 // forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
 thread_local int g_force_nw = 0, g_force_nt = 0;
@@ -1326,6 +1375,14 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.sout1 = sout1;
   a.rstats1 = rstats1;
   a.trc = g_trc;
+  a.xph = reinterpret_cast<const bf16x8*>(g_xph);
+  a.xpl = reinterpret_cast<const bf16x8*>(g_xpl);
+  a.ypkh = reinterpret_cast<bf16_t*>(g_ypkh);
+  a.ypkl = reinterpret_cast<bf16_t*>(g_ypkl);
+  g_xph = g_xpl = nullptr;   // one launch each
+  g_ypkh = g_ypkl = nullptr;
+  FO_REQUIRE(!a.xph || (x_f32 && M <= 16 && !lnw), "fo_gemm: packed X needs fp32 X of <= 16 rows");
+  FO_REQUIRE(!a.ypkh || (M <= 16 && yg), "fo_gemm: packed yg needs <= 16 rows and a yg output");
   FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
   if (lnw) {
     FO_REQUIRE(lnb && x_f32 && M <= 64 && !swiglu && rstats && rstats1 && rgroups > 0 && rgroups <= 64 && !rope &&
@@ -1693,6 +1750,20 @@ int fo_gemm_set_merge(int on) {
 
 int fo_gemm_set_trace(void* trace) {
   g_trc = reinterpret_cast<unsigned long long*>(trace);
+  return 0;
+}
+
+int fo_gemm_set_xpack(const void* hi, const void* lo) {
+  FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_gemm_set_xpack: both halves or neither");
+  g_xph = hi;
+  g_xpl = lo;
+  return 0;
+}
+
+int fo_gemm_set_ypack(void* hi, void* lo) {
+  FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_gemm_set_ypack: both halves or neither");
+  g_ypkh = hi;
+  g_ypkl = lo;
   return 0;
 }
 

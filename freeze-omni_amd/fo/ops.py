@@ -174,12 +174,14 @@ class PackedLinear:
     shift = None
 
     def __call__(self, x, out=None, act="none", residual=False, out_dtype=F32, splitk=0, M=None, norm=None,
-                 stats_out=None):
+                 stats_out=None, xpack=None, ypack=None):
         """x: fp32 or bf16 [M, >=Kp] (row stride x.stride(0)); returns out [M, N].
         norm: (RowStats, eps): x is the producer's yg (= residual * gamma) and rows are scaled by the
-        RMSNorm rstd from the producer's statistics; stats_out: RowStats this GEMM fills (see RowStats)."""
+        RMSNorm rstd from the producer's statistics; stats_out: RowStats this GEMM fills (see RowStats).
+        xpack: XPack holding x (<= 16 rows) pre-split in fragment order (written by its producer), read instead of
+        splitting x; ypack: XPack this GEMM fills with stats_out's yg (<= 16 rows)."""
         if norm is not None or stats_out is not None:
-            return self._call_norm(x, out, act, residual, out_dtype, splitk, M, norm, stats_out)
+            return self._call_norm(x, out, act, residual, out_dtype, splitk, M, norm, stats_out, xpack, ypack)
         _check_dev(x)
         if x.dtype not in (BF16, F32):
             raise TypeError("PackedLinear input must be fp32 or bf16")
@@ -189,11 +191,12 @@ class PackedLinear:
         if out is None:
             out = torch.empty(M, self.N, dtype=out_dtype, device=x.device)
         rt = Runtime.get(x.device)
-        _lib.call("fo_gemm", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
-                  self.packed.data_ptr(), self.N, 1 if self.swiglu else 0, ptr(self.bias), ptr(self.scale),
-                  ptr(self.shift), out.data_ptr(), out.stride(0), 1 if out.dtype == BF16 else 0, ACT[act],
-                  1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
-                  stream(x.device))
+        with _packed(xpack, None):
+            _lib.call("fo_gemm", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                      self.packed.data_ptr(), self.N, 1 if self.swiglu else 0, ptr(self.bias), ptr(self.scale),
+                      ptr(self.shift), out.data_ptr(), out.stride(0), 1 if out.dtype == BF16 else 0, ACT[act],
+                      1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
+                      stream(x.device))
         return out
 
 
@@ -233,7 +236,7 @@ class PackedLinear:
         stats.groups = sg.value
         return out
 
-    def qkv_rope(self, x, M, pos, slot, cos_t, sin_t, q_out, kc, vc, H, KVH, PS, norm=None, splitk=0):
+    def qkv_rope(self, x, M, pos, slot, cos_t, sin_t, q_out, kc, vc, H, KVH, PS, norm=None, splitk=0, xpack=None):
         """Fused q|k|v projection + bias + RoPE + paged-KV append (weight packed with rope_hd):
         q_out [M, H*hd] gets the rotated queries, kc/vc (one layer's pages) the token's K/V rows at slot[m]."""
         _check_dev(x)
@@ -245,14 +248,15 @@ class PackedLinear:
         rst, rg, eps = (None, 0, 0.0) if norm is None else (norm[0].buf.data_ptr(), norm[0].groups, float(norm[1]))
         if norm is not None and rg <= 0:
             raise RuntimeError("RowStats consumed before any GEMM produced them")
-        _lib.call("fo_gemm_qkv_rope", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
-                  self.packed.data_ptr(), self.N, ptr(self.bias), rt.ws.data_ptr(), rt.ws.numel(),
-                  rt.counters.data_ptr(), splitk, rst, rg, eps, pos.data_ptr(), slot.data_ptr(), cos_t.data_ptr(),
-                  sin_t.data_ptr(), q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(), H, KVH, self.rope_hd, PS,
-                  stream(x.device))
+        with _packed(xpack, None):
+            _lib.call("fo_gemm_qkv_rope", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                      self.packed.data_ptr(), self.N, ptr(self.bias), rt.ws.data_ptr(), rt.ws.numel(),
+                      rt.counters.data_ptr(), splitk, rst, rg, eps, pos.data_ptr(), slot.data_ptr(), cos_t.data_ptr(),
+                      sin_t.data_ptr(), q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(), H, KVH, self.rope_hd, PS,
+                      stream(x.device))
         return q_out
 
-    def _call_norm(self, x, out, act, residual, out_dtype, splitk, M, norm, stats_out):
+    def _call_norm(self, x, out, act, residual, out_dtype, splitk, M, norm, stats_out, xpack=None, ypack=None):
         import ctypes
         _check_dev(x)
         if x.stride(-1) != 1 or x.shape[-1] < self.Kp or out_dtype != F32:
@@ -270,15 +274,59 @@ class PackedLinear:
             if stats_out.yg.stride(0) != out.stride(0):
                 raise ValueError("yg must share the output's row stride")
         sg = ctypes.c_int(0)
-        _lib.call("fo_gemm_rms", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
-                  self.packed.data_ptr(), self.N, 1 if self.swiglu else 0, ptr(self.bias), out.data_ptr(),
-                  out.stride(0), ACT[act], 1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(),
-                  rt.counters.data_ptr(), splitk, rst, rg, eps, so, gn, yg, ctypes.byref(sg), stream(x.device))
+        if ypack is not None and stats_out is None:
+            raise ValueError("ypack packs the stats_out yg: pass stats_out")
+        with _packed(xpack, ypack):
+            _lib.call("fo_gemm_rms", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                      self.packed.data_ptr(), self.N, 1 if self.swiglu else 0, ptr(self.bias), out.data_ptr(),
+                      out.stride(0), ACT[act], 1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(),
+                      rt.counters.data_ptr(), splitk, rst, rg, eps, so, gn, yg, ctypes.byref(sg), stream(x.device))
         if stats_out is not None:
             if sg.value > stats_out.max_groups:
                 raise RuntimeError(f"RowStats holds {stats_out.max_groups} groups per row, GEMM wrote {sg.value}")
             stats_out.groups = sg.value
         return out
+
+
+# FO_XPACK=0 turns the packed <= 16-row activations off (A/B only)
+XPACK = os.environ.get("FO_XPACK", "1") != "0"
+
+
+class XPack:
+    """An fp32 activation of <= 16 rows also held as bf16 hi + lo in MFMA A-fragment order ([K/32][64][8] each;
+    lane l = row l & 15, columns 8 (l >> 4) .. + 8 of a 32-column k-step): its producer kernel writes it beside
+    the fp32 rows, and the consuming one-row-tile GEMM reads one contiguous 1 KiB per wave and half instead of 16
+    row segments per float4 (Qwen2 o 11.4 -> 9.2 us, q|k|v 13.7 -> 11.8 us at 16 rows, results bit-identical:
+    scripts/gemm_xpack_probe.py)."""
+
+    def __init__(self, K, device):
+        if K % 32:
+            raise ValueError("XPack needs K % 32 == 0")
+        self.K = K
+        self.hi = torch.empty(K * 16, dtype=BF16, device=device)
+        self.lo = torch.empty(K * 16, dtype=BF16, device=device)
+
+
+class _packed:
+    """Arms fo_gemm's packed-X input / packed-yg output for the one launch inside the block (thread-local in the
+    library, consumed by that launch); a launch that raises leaves nothing armed for the next one."""
+
+    def __init__(self, xpack, ypack):
+        self.x, self.y = xpack, ypack
+
+    def __enter__(self):
+        if self.x is not None:
+            _lib.call("fo_gemm_set_xpack", self.x.hi.data_ptr(), self.x.lo.data_ptr())
+        if self.y is not None:
+            _lib.call("fo_gemm_set_ypack", self.y.hi.data_ptr(), self.y.lo.data_ptr())
+
+    def __exit__(self, et, ev, tb):
+        if et is not None:
+            if self.x is not None:
+                _lib.call("fo_gemm_set_xpack", None, None)
+            if self.y is not None:
+                _lib.call("fo_gemm_set_ypack", None, None)
+        return False
 
 
 class RowStats:
@@ -430,7 +478,7 @@ ATTN_KEYS_PER_SPLIT = int(os.environ.get("FO_ATTN_KPS", "128"))
 
 
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,
-              part_ml, part_o, out, tickets=None, keys_per_split=ATTN_KEYS_PER_SPLIT):
+              part_ml, part_o, out, tickets=None, keys_per_split=ATTN_KEYS_PER_SPLIT, opack=None):
     """tickets: zeroed int32 [>= n_items * KVH] -> splits sized from each item's key count (at most
     nsplit) merged inside the launch; None -> nsplit static splits + a combine launch.
     items None: a uniform batch, T / n_items tokens per sequence in sequence order (item b = sequence b); a
@@ -439,9 +487,17 @@ def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc,
         raise ValueError("attention: items=None needs T / n_items tokens per sequence")
     if tickets is not None and tickets.numel() < n_items * KVH:
         raise ValueError("attention tickets buffer smaller than n_items * KVH")
-    _lib.call("fo_attention", q.data_ptr(), T, ptr(items), n_items, max_rows, tok_nvis.data_ptr(),
-              block_table.data_ptr(), block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd, float(scale),
-              nsplit, ptr(part_ml), ptr(part_o), out.data_ptr(), ptr(tickets), int(keys_per_split), stream(q.device))
+    if opack is not None:
+        _lib.call("fo_attention_set_opack", opack.hi.data_ptr(), opack.lo.data_ptr())
+    try:
+        _lib.call("fo_attention", q.data_ptr(), T, ptr(items), n_items, max_rows, tok_nvis.data_ptr(),
+                  block_table.data_ptr(), block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd,
+                  float(scale), nsplit, ptr(part_ml), ptr(part_o), out.data_ptr(), ptr(tickets), int(keys_per_split),
+                  stream(q.device))
+    except Exception:
+        if opack is not None:   # the launch did not consume it: never leave it for the next one
+            _lib.call("fo_attention_set_opack", None, None)
+        raise
     return out
 
 

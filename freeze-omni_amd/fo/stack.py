@@ -68,6 +68,9 @@ class DecoderStack:
               "sA": ops.RowStats(T, device), "sB": ops.RowStats(T, device),
               "xg": torch.empty(T, self.D, dtype=F32, device=device),
               "tickets": torch.zeros(max(T, 2) * KVH, dtype=torch.int32, device=device)}
+        if 8 < T <= 16 and ops.XPACK:   # packed activations for the q|k|v and o inputs (ops.XPack)
+            ws["xgp"] = ops.XPack(self.D, device)
+            ws["attp"] = ops.XPack(H * hd, device)
         if nsplit > 1:
             ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
@@ -93,6 +96,11 @@ class DecoderStack:
         # one token per sequence (decode) or the same count for every sequence, one work item each (a listen
         # chunk): the attention needs no item table (fo_attention items NULL)
         dense = ATTN_DENSE and (meta.n_items == T == meta.S or getattr(meta, "uniform", False))
+        # 9..16 rows (a listen chunk): the q|k|v input (the previous down projection's x*gamma) and the o input (the
+        # attention output) are also written packed by their producers and read packed (ops.XPack; layer 0's q|k|v
+        # input comes from the gather and stays fp32).  At <= 8 rows (text and AR decode steps) the X re-read is
+        # half as large and the extra stores cost more than the reads save (AR step 172.4 -> 177.1 us, r04zf)
+        xgp, attp = (ws.get("xgp"), ws.get("attp")) if 8 < T <= 16 else (None, None)
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
@@ -102,16 +110,17 @@ class DecoderStack:
             xin, norm = (h, None) if i == 0 else (xg, (sA, self.eps))
             if i == 0 and not pre_normed:
                 ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
-            L.qkv.qkv_rope(xin, T, *rope, norm=norm)
+            L.qkv.qkv_rope(xin, T, *rope, norm=norm, xpack=xgp if i > 0 else None)
             ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis,
                           meta.block_table, self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale,
-                          nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps)
-            L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg))
+                          nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps,
+                          opack=attp)
+            L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg), xpack=attp)
             L.gu(xg, out=m, M=T, norm=(sB, self.eps))
             if i == last and final_norm is None:
                 L.down(m, out=x, residual=True, M=T)
             elif i == last:
                 L.down(m, out=x, residual=True, M=T, stats_out=sA.set(final_norm, xg))
             else:
-                L.down(m, out=x, residual=True, M=T, stats_out=sA.set(self.layers[i + 1].ln1, xg))
+                L.down(m, out=x, residual=True, M=T, stats_out=sA.set(self.layers[i + 1].ln1, xg), ypack=xgp)
         return x

@@ -1,0 +1,122 @@
+"""Packed <= 16-row activations (ops.XPack): every producer (the split-K reduce, the unsplit GEMM epilogue, the
+in-launch split merge, the multi-row and decode attention) writes exactly the bf16 hi / lo split of its fp32 output
+in fragment order, and a GEMM reading the packed copy gives bit-identical results to the one splitting fp32 X."""
+import math
+
+import pytest
+import torch
+
+from fo import ops
+from fo.kv import BatchMeta, KVPool, KVSeq
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(x):
+    """fp32 [M <= 16, K] -> the (hi, lo) [K/32][64][8] bf16 fragment order of ops.XPack (rows >= M unchecked)."""
+    M, K = x.shape
+    xf = torch.zeros(16, K, dtype=torch.float32, device=x.device)
+    xf[:M] = x
+    hi = xf.to(torch.bfloat16)
+    lo = (xf - hi.float()).to(torch.bfloat16)
+    f = lambda t: t.view(16, K // 32, 4, 8).permute(1, 2, 0, 3).reshape(-1)  # noqa: E731
+    return f(hi), f(lo)
+
+
+def _rows(flat, M, K):
+    """the first M rows of a packed half back in [M, K] (bit patterns as int16)."""
+    return flat.view(K // 32, 4, 16, 8).permute(2, 0, 1, 3).reshape(16, K)[:M].view(torch.int16)
+
+
+def _check_packed(xp, y, M):
+    K = y.shape[1]
+    hi, lo = _pack(y)
+    assert torch.equal(_rows(xp.hi, M, K), _rows(hi, M, K))
+    assert torch.equal(_rows(xp.lo, M, K), _rows(lo, M, K))
+
+
+@pytest.mark.parametrize("M,N,K,splitk", [(16, 3584, 18944, 0), (12, 1024, 4096, 4), (16, 896, 896, 1), (9, 512, 256, 1)])
+def test_yg_producers_write_the_packed_split(dev, M, N, K, splitk):
+    """stats_out's yg also packed: k_gemm_reduce (split-K), the unsplit epilogue, the in-launch merge (small weights)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + splitk)
+    lin = ops.PackedLinear((torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(dev))
+    x = torch.randn(M, K, generator=g).to(dev)
+    res = torch.randn(M, N, generator=g).to(dev)
+    gamma = (1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    st = ops.RowStats(M, dev)
+    yg = torch.empty(M, N, device=dev)
+    xp = ops.XPack(N, dev)
+    xp.hi.fill_(0)
+    xp.lo.fill_(0)
+    out = res.clone()
+    lin(x, out=out, residual=True, M=M, splitk=splitk, stats_out=st.set(gamma, yg), ypack=xp)
+    torch.cuda.synchronize()
+    _check_packed(xp, yg, M)
+
+
+@pytest.mark.parametrize("M,N,K,rope", [(16, 3584, 3584, False), (11, 896, 896, False), (16, 4608, 3584, True)])
+def test_packed_x_gemm_is_bit_identical(dev, M, N, K, rope):
+    """The one-row-tile GEMM reading X packed equals the one splitting fp32 X, bit for bit (o-style residual
+    epilogue, and the q|k|v RoPE + paged-KV append epilogue)."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(dev)
+    x = torch.randn(M, K, generator=g).to(dev)
+    xp = ops.XPack(K, dev)
+    h, lo = _pack(x)
+    xp.hi.copy_(h)
+    xp.lo.copy_(lo)
+    if not rope:
+        lin = ops.PackedLinear(w)
+        y0 = torch.randn(M, N, generator=g).to(dev)
+        a, b = y0.clone(), y0.clone()
+        lin(x, out=a, residual=True, M=M)
+        lin(x, out=b, residual=True, M=M, xpack=xp)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        return
+    hd, H, KVH = 128, 28, 4
+    lin = ops.PackedLinear(w, rope_hd=hd)
+    pool = KVPool(1, KVH, hd, 64, 16, dev)
+    seqs = [KVSeq(pool) for _ in range(M)]
+    meta = BatchMeta([(s, 1, 0, True) for s in seqs], dev, gqa=H // KVH)
+    pos = torch.arange(M, dtype=torch.int32, device=dev)
+    inv = 1.0 / (1e6 ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+    ang = torch.arange(64, dtype=torch.float64)[:, None] * inv[None, :]
+    cos, sin = ang.cos().float().to(dev), ang.sin().float().to(dev)
+    outs = []
+    for pk in (None, xp):
+        q = torch.empty(M, H * hd, device=dev)
+        pool.k.zero_()
+        pool.v.zero_()
+        lin.qkv_rope(x, M, pos, meta.tok_slot, cos, sin, q, pool.k[0], pool.v[0], H, KVH, pool.PS, xpack=pk)
+        torch.cuda.synchronize()
+        outs.append((q.clone(), pool.k.clone(), pool.v.clone()))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("H,KVH,hd,tokens", [(28, 4, 128, 2), (14, 14, 64, 1)])
+def test_attention_writes_the_packed_split(dev, H, KVH, hd, tokens):
+    """fo_attention's packed output (multi-row kernel with the in-launch split merge; the decode kernel) equals
+    the split of its fp32 output."""
+    g = torch.Generator().manual_seed(H + hd)
+    pool = KVPool(1, KVH, hd, 256, 16, dev)
+    pool.k.copy_(torch.randn(pool.k.shape, generator=g))
+    pool.v.copy_(torch.randn(pool.v.shape, generator=g))
+    seqs = [KVSeq(pool) for _ in range(16 // tokens)]
+    for s, n in zip(seqs, [3, 40, 150, 300, 700, 1, 64, 65, 129, 9, 17, 33, 250, 5, 90, 400][:len(seqs)]):
+        BatchMeta([(s, n, 0, True)], dev)
+    meta = BatchMeta([(s, tokens, s.length, True) for s in seqs], dev, gqa=H // KVH)
+    T = meta.T
+    q = torch.randn(T, H * hd, generator=g).to(dev)
+    ns = ops.attn_nsplit(meta.max_keys, meta.n_items, KVH)
+    part_ml = torch.empty(T * H * ns * 2, device=dev)
+    part_o = torch.empty(T * H * ns * hd, device=dev)
+    tickets = torch.zeros(meta.n_items * KVH, dtype=torch.int32, device=dev)
+    out = torch.empty(T, H * hd, device=dev)
+    xp = ops.XPack(H * hd, dev)
+    ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0],
+                  pool.v[0], H, KVH, hd, 1 / math.sqrt(hd), ns, part_ml, part_o, out, tickets=tickets,
+                  keys_per_split=128, opack=xp)
+    torch.cuda.synchronize()
+    _check_packed(xp, out, T)
