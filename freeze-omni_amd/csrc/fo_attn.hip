@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq,
                                                       const int* start, const int* len, const int* ring,
                                                       const float* ptab, const int* pstart, const float* bu,
                                                       const float* bv, int T, int h, int dk, float scale, float* out,
-                                                      int ldo) {
+                                                      int ldo, uint16_t* oph, uint16_t* opl, int prb) {
   extern __shared__ float smem[];
   const int KP = dk + 4;  // padded rows: lanes on consecutive keys hit distinct banks
   float* k_s = smem;                  // [cap][KP]
@@ -399,6 +399,7 @@ __global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq,
     float acc = 0.f;
     for (int j = 0; j < Lk; ++j) acc += pr[j] * v_s[j * KP + c];
     out[((size_t)b * T + i) * ldo + hh * dk + c] = acc;
+    if (oph) xpack_store(oph, opl, b * T + i, hh * dk + c, acc, prb);   // the out projection's packed input
   }
 }
 
@@ -510,8 +511,11 @@ int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, i
   FO_REQUIRE(T >= 1 && T <= cap && dk % 4 == 0 && (ldq % 4) == 0, "fo_relpos_attention_fused: T=%d dk=%d", T, dk);
   const size_t lds = (size_t)(3 * cap * (dk + 4) + 2 * T * dk + T * cap) * sizeof(float);
   FO_REQUIRE(lds <= 160 * 1024, "fo_relpos_attention_fused: ring of %d x %d exceeds LDS", cap, dk);
+  uint16_t *oph = g_oph, *opl = g_opl;
+  g_oph = g_opl = nullptr;   // one launch
+  FO_REQUIRE(!oph || B * T <= 32, "fo_relpos_attention_fused: packed output needs <= 32 rows");
   hipLaunchKernelGGL(k_relpos_fused, dim3(B, h), dim3(256), lds, s, qkv, ldq, kr, vr, cap, start, len, ring, ptab,
-                     pstart, bu, bv, T, h, dk, scale, out, ldo);
+                     pstart, bu, bv, T, h, dk, scale, out, ldo, oph, opl, (B * T + 15) / 16);
   return fo::check_launch("fo_relpos_attention_fused");
 }
 

@@ -39,12 +39,13 @@ int check_launch(const char* what);
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-// Packed fp32 activations for the <= 16-row GEMMs: element (m < 16, n) of an fp32 matrix as bf16 hi + lo (the
+// Packed fp32 activations for the <= 32-row GEMMs: element (m < 16 rbs, n) of an fp32 matrix as bf16 hi + lo (the
 // split a GEMM would do on load: hi = bf16(v), lo = bf16(v - hi)) at its MFMA A-fragment position: k-step n / 32,
 // lane 16 (n % 32 / 8) + m, element n % 8 of the lane's 8.  [K/32][64][8] bf16 per half.
-__device__ __forceinline__ void xpack_store(uint16_t* hp, uint16_t* lp, int m, int n, float v) {
+// With rbs row blocks of 16 (<= 16 rows: 1; <= 32: 2) the k-step holds rbs fragments: [K/32][rbs][64][8].
+__device__ __forceinline__ void xpack_store(uint16_t* hp, uint16_t* lp, int m, int n, float v, int rbs = 1) {
   const int c = n & 31;
-  const size_t o = ((size_t)((n >> 5) * 64 + ((c >> 3) << 4) + m)) * 8 + (c & 7);
+  const size_t o = ((size_t)(((n >> 5) * rbs + (m >> 4)) * 64 + ((c >> 3) << 4) + (m & 15))) * 8 + (c & 7);
   const __bf16 h = (__bf16)v;
   hp[o] = __builtin_bit_cast(uint16_t, h);
   lp[o] = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));

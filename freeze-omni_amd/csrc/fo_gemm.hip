@@ -74,9 +74,10 @@ struct GemmArgs {
   // instead of 16 row segments per float4 (one-row-tile grid kernels only; nullptr: plain fp32 X)
   const bf16x8* xph;
   const bf16x8* xpl;
-  // producer of a next-norm input (yg): rows < 16 of yg also written packed the same way (fo_gemm_set_ypack)
+  // producer: yg (a next-norm input) or, without yg, Y also written packed the same way (fo_gemm_set_ypack)
   bf16_t* ypkh;
   bf16_t* ypkl;
+  int prb;   // packed row blocks of xph / ypkh: ceil(M / 16) (1 or 2)
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -304,7 +305,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
   // X given packed (GemmArgs::xph / xpl): only the k_gemm_xp instantiations read it (the others compile as before)
-  static_assert(!XPK || (RB == 1 && XF32 && !LN && !SW && !PIPE), "packed X: one-row-tile plain / RoPE kernels");
+  static_assert(!XPK || (RB <= 2 && XF32 && !LN && !SW && !PIPE), "packed X: <= 2-row-block plain / RoPE kernels");
   const bool xpk = XPK && a.xph != nullptr;
   float ln_mu[RB], ln_rs[RB];
   // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
@@ -385,8 +386,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       }
     } else {
       if (XF32 && xpk) {
-        hi = a.xph[(size_t)ks * 64 + lane];
-        lo = a.xpl[(size_t)ks * 64 + lane];
+        hi = a.xph[((size_t)ks * a.prb + r) * 64 + lane];
+        lo = a.xpl[((size_t)ks * a.prb + r) * 64 + lane];
       } else {
         load_x<XT, XF32>(xr[r] + (size_t)ks * 32, hi, lo);
       }
@@ -515,8 +516,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         for (int r = 0; r < RB; ++r) {
           if constexpr (XF32) {
             if (xpk) {
-              xf0[u][r][0] = __builtin_bit_cast(float4, a.xph[(size_t)k * 64 + lane]);
-              xf0[u][r][1] = __builtin_bit_cast(float4, a.xpl[(size_t)k * 64 + lane]);
+              xf0[u][r][0] = __builtin_bit_cast(float4, a.xph[((size_t)k * a.prb + r) * 64 + lane]);
+              xf0[u][r][1] = __builtin_bit_cast(float4, a.xpl[((size_t)k * a.prb + r) * 64 + lane]);
             } else {
               const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
               xf0[u][r][0] = q[0];
@@ -723,6 +724,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(v);
         else reinterpret_cast<float*>(a.Y)[o] = v;
         red[0][e_lt][e_rr][e_c] = v;
+        if (a.ypkh && !a.yg) xpack_store(a.ypkh, a.ypkl, m, n, v, a.prb);   // Y is the next GEMM's packed input
       }
     }
   } else
@@ -735,6 +737,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     if (SW) y = epilogue_store(a, true, m, n, red[0][2 * lt][rr][c], red[0][2 * lt + 1][rr][c]);
     else y = epilogue_store(a, false, m, n, red[0][lt][rr][c], 0.f);
     if (!SW) red[0][lt][rr][c] = y;
+    if (a.ypkh && !a.yg) xpack_store(a.ypkh, a.ypkl, m, n, y, a.prb);   // Y is the next GEMM's packed input
   }
   if (!SW && a.sout) {
     // row partial sums of squares of this workgroup's LT*16 output columns, for the next norm
@@ -755,7 +758,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         if (a.yg && c < cnt) {
           const float vg = v * (EPRE ? p_gn : a.gnext[n0 + c]);
           a.yg[(size_t)m * a.ldy + n0 + c] = vg;
-          if (a.ypkh && m < 16) xpack_store(a.ypkh, a.ypkl, m, n0 + c, vg);
+          if (a.ypkh) xpack_store(a.ypkh, a.ypkl, m, n0 + c, vg, a.prb);
         }
       }
       const float ss = wave_sum(sq);
@@ -851,6 +854,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       y = apply_act(y, a.act) + pr;
       if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(y);
       else reinterpret_cast<float*>(a.Y)[o] = y;
+      if (a.ypkh && !a.yg) xpack_store(a.ypkh, a.ypkl, m, n, y, a.prb);   // Y is the next GEMM's packed input
     }
   }
   if (a.sout && !sw) {
@@ -863,7 +867,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
     if (a.yg && live) {
       const float vg = y * p_gn;
       a.yg[o] = vg;
-      if (a.ypkh && m < 16) xpack_store(a.ypkh, a.ypkl, m, n, vg);
+      if (a.ypkh) xpack_store(a.ypkh, a.ypkl, m, n, vg, a.prb);
     }
   }
 }
@@ -881,9 +885,9 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_wpipe(GemmArgs a) {
   gemm_body<NT, RB, true, NW, U, SW, false, true>(a);
 }
 // one-row-tile fp32-X GEMM reading X packed by its producer (GemmArgs::xph / xpl, ops.XPack)
-template <int NT, int NW, int U>
+template <int NT, int RB, int NW, int U>
 __global__ __launch_bounds__(NW * 64) void k_gemm_xp(GemmArgs a) {
-  gemm_body<NT, 1, true, NW, U, false, false, false, true>(a);
+  gemm_body<NT, RB, true, NW, U, false, false, false, true>(a);
 }
 
 // Software-pipelined one-row-tile fp32-X weight stream (k_gemm_wpipe).  Mode: 0 = plain loops
@@ -907,9 +911,9 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
 template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
   const size_t shm = 0;
-  if constexpr (RB == 1 && !SW) {
-    if (x_f32 && a.xph && !g_launch_pipe) {   // X packed by its producer
-      hipLaunchKernelGGL((k_gemm_xp<NT, NW, U>), grid, dim3(NW * 64), shm, s, a);
+  if constexpr (RB <= 2 && !SW) {
+    if (x_f32 && a.xph && !(RB == 1 && g_launch_pipe)) {   // X packed by its producer
+      hipLaunchKernelGGL((k_gemm_xp<NT, RB, NW, U>), grid, dim3(NW * 64), shm, s, a);
       return;
     }
   }
@@ -1381,8 +1385,9 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.ypkl = reinterpret_cast<bf16_t*>(g_ypkl);
   g_xph = g_xpl = nullptr;   // one launch each
   g_ypkh = g_ypkl = nullptr;
-  FO_REQUIRE(!a.xph || (x_f32 && M <= 16 && !lnw), "fo_gemm: packed X needs fp32 X of <= 16 rows");
-  FO_REQUIRE(!a.ypkh || (M <= 16 && yg), "fo_gemm: packed yg needs <= 16 rows and a yg output");
+  a.prb = (M + 15) / 16;
+  FO_REQUIRE(!a.xph || (x_f32 && M <= 32 && !lnw), "fo_gemm: packed X needs fp32 X of <= 32 rows");
+  FO_REQUIRE(!a.ypkh || (M <= 32 && !swiglu && !rope), "fo_gemm: packed output needs <= 32 plain rows");
   FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
   if (lnw) {
     FO_REQUIRE(lnb && x_f32 && M <= 64 && !swiglu && rstats && rstats1 && rgroups > 0 && rgroups <= 64 && !rope &&

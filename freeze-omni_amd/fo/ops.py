@@ -200,7 +200,7 @@ class PackedLinear:
         return out
 
 
-    def ln(self, x, lnw, lnb, stats, eps=1e-5, out=None, act="none", M=None, splitk=0):
+    def ln(self, x, lnw, lnb, stats, eps=1e-5, out=None, act="none", M=None, splitk=0, ypack=None):
         """act(LayerNorm(x) W^T + b) with the norm applied as X is loaded (fo_gemm_ln; M <= 64); stats:
         the RowStats(with_sums=True) a rowstats() producer filled for x."""
         _check_dev(x)
@@ -212,13 +212,14 @@ class PackedLinear:
         if out is None:
             out = torch.empty(M, self.N, dtype=F32, device=x.device)
         rt = Runtime.get(x.device)
-        _lib.call("fo_gemm_ln", x.data_ptr(), x.stride(0), M, self.Kp, self.packed.data_ptr(), self.N, ptr(self.bias),
-                  lnw.data_ptr(), lnb.data_ptr(), float(eps), stats.buf1.data_ptr(), stats.buf.data_ptr(),
-                  stats.groups, out.data_ptr(), out.stride(0), ACT[act], rt.ws.data_ptr(), rt.ws.numel(), splitk,
-                  stream(x.device))
+        with _packed(None, ypack):
+            _lib.call("fo_gemm_ln", x.data_ptr(), x.stride(0), M, self.Kp, self.packed.data_ptr(), self.N,
+                      ptr(self.bias), lnw.data_ptr(), lnb.data_ptr(), float(eps), stats.buf1.data_ptr(),
+                      stats.buf.data_ptr(), stats.groups, out.data_ptr(), out.stride(0), ACT[act], rt.ws.data_ptr(),
+                      rt.ws.numel(), splitk, stream(x.device))
         return out
 
-    def rowstats(self, x, out, stats, residual=False, act="none", M=None, splitk=0):
+    def rowstats(self, x, out, stats, residual=False, act="none", M=None, splitk=0, xpack=None):
         """fp32 GEMM that also fills stats (per-row partial sums of out and out^2) for ln()."""
         import ctypes
         _check_dev(x)
@@ -227,10 +228,11 @@ class PackedLinear:
             raise ValueError("rowstats needs RowStats(with_sums=True)")
         rt = Runtime.get(x.device)
         sg = ctypes.c_int(0)
-        _lib.call("fo_gemm_rowstats", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
-                  self.packed.data_ptr(), self.N, ptr(self.bias), out.data_ptr(), out.stride(0), ACT[act],
-                  1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
-                  stats.buf1.data_ptr(), stats.buf.data_ptr(), ctypes.byref(sg), stream(x.device))
+        with _packed(xpack, None):
+            _lib.call("fo_gemm_rowstats", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
+                      self.packed.data_ptr(), self.N, ptr(self.bias), out.data_ptr(), out.stride(0), ACT[act],
+                      1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
+                      stats.buf1.data_ptr(), stats.buf.data_ptr(), ctypes.byref(sg), stream(x.device))
         if sg.value > stats.max_groups:
             raise RuntimeError(f"RowStats holds {stats.max_groups} groups per row, GEMM wrote {sg.value}")
         stats.groups = sg.value
@@ -293,18 +295,19 @@ XPACK = os.environ.get("FO_XPACK", "1") != "0"
 
 
 class XPack:
-    """An fp32 activation of <= 16 rows also held as bf16 hi + lo in MFMA A-fragment order ([K/32][64][8] each;
-    lane l = row l & 15, columns 8 (l >> 4) .. + 8 of a 32-column k-step): its producer kernel writes it beside
+    """An fp32 activation of <= 32 rows also held as bf16 hi + lo in MFMA A-fragment order ([K/32][row blocks][64][8]
+    each; lane l = row l & 15 of the row block, columns 8 (l >> 4) .. + 8 of a 32-column k-step): its producer kernel writes it beside
     the fp32 rows, and the consuming one-row-tile GEMM reads one contiguous 1 KiB per wave and half instead of 16
     row segments per float4 (Qwen2 o 11.4 -> 9.2 us, q|k|v 13.7 -> 11.8 us at 16 rows, results bit-identical:
     scripts/gemm_xpack_probe.py)."""
 
-    def __init__(self, K, device):
-        if K % 32:
-            raise ValueError("XPack needs K % 32 == 0")
-        self.K = K
-        self.hi = torch.empty(K * 16, dtype=BF16, device=device)
-        self.lo = torch.empty(K * 16, dtype=BF16, device=device)
+    def __init__(self, K, device, rows=16):
+        if K % 32 or not 1 <= rows <= 32:
+            raise ValueError("XPack needs K % 32 == 0 and <= 32 rows")
+        self.K, self.rows = K, rows
+        n = K * 16 * ((rows + 15) // 16)   # [K/32][row blocks][64][8]
+        self.hi = torch.empty(n, dtype=BF16, device=device)
+        self.lo = torch.empty(n, dtype=BF16, device=device)
 
 
 class _packed:
@@ -506,7 +509,19 @@ def enc_kv_write(k, v, B, T, d, start, length, ring, cap, kr, vr):
               length.data_ptr(), ptr(ring), cap, kr.data_ptr(), vr.data_ptr(), stream(k.device))
 
 
-def relpos_attention_fused(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out):
+def relpos_attention_fused(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out,
+                           opack=None):
+    if opack is not None:
+        _lib.call("fo_attention_set_opack", opack.hi.data_ptr(), opack.lo.data_ptr())
+    try:
+        _relpos_fused_call(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out)
+    except Exception:
+        if opack is not None:   # the launch did not consume it: never leave it for the next one
+            _lib.call("fo_attention_set_opack", None, None)
+        raise
+
+
+def _relpos_fused_call(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out):
     _lib.call("fo_relpos_attention_fused", qkv.data_ptr(), qkv.stride(0), kr.data_ptr(), vr.data_ptr(), cap,
               start.data_ptr(), length.data_ptr(), ptr(ring), ptab.data_ptr(), pstart.data_ptr(), bu.data_ptr(),
               bv.data_ptr(), B, T, h, dk, float(scale), out.data_ptr(), out.stride(0), stream(qkv.device))

@@ -187,7 +187,10 @@ class SpeechEncoderEngine:
                 "x": e(B * T, self.d), "h": e(B * T, self.d), "qkv": e(B * T, 3 * self.d),
                 "att": e(B * T, self.d), "f": e(B * T, self.layers[0]["ff1"].N),
                 "sA": ops.RowStats(B * T, dev, with_sums=True), "sB": ops.RowStats(B * T, dev, with_sums=True),
-                "meta": torch.empty(4 * B, dtype=I32, device=dev)}
+                "meta": torch.empty(4 * B, dtype=I32, device=dev),
+                # <= 32 rows: the out and FFN-down inputs also written packed by their producers (ops.XPack)
+                "attp": ops.XPack(self.d, dev, B * T) if B * T <= 32 and ops.XPACK else None,
+                "fp": ops.XPack(self.layers[0]["ff1"].N, dev, B * T) if B * T <= 32 and ops.XPACK else None}
 
     def host_meta(self, caches, pe_indices):
         """Per-user ring / position metadata [starts | lens | rings | pos starts] and the next pe_index."""
@@ -229,6 +232,7 @@ class SpeechEncoderEngine:
         # pre-norms applied by the GEMMs on load (fo_gemm_ln) from the residual producers' row sums
         fuse_ln = B * T <= 64 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
         sA, sB = bufs["sA"], bufs["sB"]
+        attp, fp = (bufs.get("attp"), bufs.get("fp")) if fuse_ln else (None, None)
         last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
             if fuse_ln and i > 0:
@@ -237,18 +241,18 @@ class SpeechEncoderEngine:
                 ops.layernorm(x, *L["ln1"], out=h)
                 L["qkv"](h, out=qkv)
             ops.relpos_attention_fused(qkv, self.kr[i], self.vr[i], self.cap, st, ln, rg, self.ptab[i], ps,
-                                       L["bu"], L["bv"], B, T, self.h, self.dk, scale, att)
+                                       L["bu"], L["bv"], B, T, self.h, self.dk, scale, att, opack=attp)
             if fuse_ln:
-                L["out"].rowstats(att, x, sB, residual=True)
-                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu")
+                L["out"].rowstats(att, x, sB, residual=True, xpack=attp)
+                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp)
             else:
                 L["out"](att, out=x, residual=True)
                 ops.layernorm(x, *L["ln2"], out=h)
                 L["ff1"](h, out=f, act="relu")
             if fuse_ln and i < last:
-                L["ff2"].rowstats(f, x, sA, residual=True)
+                L["ff2"].rowstats(f, x, sA, residual=True, xpack=fp)
             else:
-                L["ff2"](f, out=x, residual=True)
+                L["ff2"](f, out=x, residual=True, xpack=fp)
         ops.layernorm(x, *self.after, out=x)
         return x, T
 

@@ -101,15 +101,18 @@ int fo_gemm_set_merge(int on);
  * (100 MHz) to trace[wg * 24 + slot]: 0 start, 1 + w the end of wave w's weight stream, 17 the K reduce done,
  * 18 the epilogue issued.  nullptr turns it off (the default).  Returns 0. */
 int fo_gemm_set_trace(void* trace);
-/* probe hook: the calling thread's NEXT fo_gemm launch takes its <= 16 fp32 X rows also as bf16 hi / lo halves
- * packed in MFMA A-fragment order (hi, lo: [K/32][64][8] bf16, lane l = row l & 15, columns 8 (l >> 4) .. + 8 of
- * each 32-column k-step; one-row-tile grid kernels read them instead of splitting X).  Both or neither.  Returns 0. */
+/* the calling thread's NEXT fo_gemm launch takes its <= 32 fp32 X rows also as bf16 hi / lo halves packed in MFMA
+ * A-fragment order by their producer (hi, lo: [K/32][ceil(M/16)][64][8] bf16, lane l = row 16 b + (l & 15) of row
+ * block b, columns 8 (l >> 4) .. + 8 of each 32-column k-step; the <= 2-row-block grid kernels read them instead of
+ * splitting X, bit-identical).  Both or neither.  Returns 0. */
 int fo_gemm_set_xpack(const void* hi, const void* lo);
-/* the calling thread's NEXT fo_gemm launch, a producer of a next-norm input (yg, stats_out), also writes rows < 16
- * of yg packed as fo_gemm_set_xpack reads them (hi, lo: [N/32][64][8] bf16; <= 16 rows).  Both or neither. */
+/* the calling thread's NEXT fo_gemm launch (<= 32 rows, plain epilogue) also writes its next-norm input yg
+ * (stats_out) -- or, without one, its output Y -- packed as fo_gemm_set_xpack reads it (hi, lo: [N/32][ceil(M/16)][64][8]
+ * bf16).  Both or neither. */
 int fo_gemm_set_ypack(void* hi, void* lo);
-/* the calling thread's NEXT fo_attention launch also writes its output packed as fo_gemm_set_xpack reads it
- * (hi, lo: [H*hd/32][64][8] bf16; <= 16 tokens; not with the separate combine launch).  Both or neither. */
+/* the calling thread's NEXT fo_attention (<= 16 tokens, not with the separate combine launch) or
+ * fo_relpos_attention_fused (<= 32 rows) launch also writes its output packed as fo_gemm_set_xpack reads it (hi, lo:
+ * [cols/32][ceil(rows/16)][64][8] bf16).  Both or neither. */
 int fo_attention_set_opack(void* hi, void* lo);
 /* Software-pipelined one-row-tile fp32-X weight-stream GEMMs (M <= 16, >= 32 MB of weights: the next
  * k-group's weights + X in flight during this group's MFMAs).  3 (default): the measured policy; 0: plain

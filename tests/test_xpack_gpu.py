@@ -120,3 +120,51 @@ def test_attention_writes_the_packed_split(dev, H, KVH, hd, tokens):
                   keys_per_split=128, opack=xp)
     torch.cuda.synchronize()
     _check_packed(xp, out, T)
+
+
+def _pack_rb(x):
+    """fp32 [M <= 32, K] -> (hi, lo) [K/32][ceil(M/16)][64][8] bf16 (the two-row-block layout)."""
+    M, K = x.shape
+    rb = (M + 15) // 16
+    xf = torch.zeros(rb * 16, K, dtype=torch.float32, device=x.device)
+    xf[:M] = x
+    hi = xf.to(torch.bfloat16)
+    lo = (xf - hi.float()).to(torch.bfloat16)
+    f = lambda t: t.view(rb, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).reshape(-1)  # noqa: E731
+    return f(hi), f(lo), rb
+
+
+@pytest.mark.parametrize("M", [32, 27, 20])
+def test_two_row_block_packing_layernorm_producer_and_rowstats_consumer(dev, M):
+    """The speech encoder's 17..32-row blocks: the LayerNorm-on-load FFN-up GEMM writes its ReLU output packed
+    (two row blocks), the FFN-down reads it -- bit-identical to reading fp32 rows."""
+    g = torch.Generator(device="cpu").manual_seed(M)
+    D, F = 256, 1024
+    prod = ops.PackedLinear((torch.randn(D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(dev))
+    up = ops.PackedLinear((torch.randn(F, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(dev),
+                          torch.randn(F, generator=g).to(dev))
+    down = ops.PackedLinear((torch.randn(D, F, generator=g) / F ** 0.5).to(torch.bfloat16).to(dev))
+    x = torch.randn(M, D, generator=g).to(dev)
+    st = ops.RowStats(M, dev, with_sums=True)
+    xr = torch.randn(M, D, generator=g).to(dev)
+    prod.rowstats(x, xr, st, residual=True)
+    lnw = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    lnb = (0.1 * torch.randn(D, generator=g)).to(dev)
+    fp = ops.XPack(F, dev, M)
+    f = torch.empty(M, F, device=dev)
+    up.ln(xr, lnw, lnb, st, out=f, act="relu", ypack=fp)
+    torch.cuda.synchronize()
+    hi, lo, rb = _pack_rb(f)
+    n = F * 16 * rb
+    view = lambda t: t[:n].view(F // 32, rb, 4, 16, 8)  # noqa: E731
+    for a, b in ((fp.hi, hi), (fp.lo, lo)):   # rows < M only
+        A = view(a).permute(1, 3, 0, 2, 4).reshape(rb * 16, F)[:M].view(torch.int16)
+        B = view(b).permute(1, 3, 0, 2, 4).reshape(rb * 16, F)[:M].view(torch.int16)
+        assert torch.equal(A, B)
+    y0 = torch.randn(M, D, generator=g).to(dev)
+    st2 = ops.RowStats(M, dev, with_sums=True)
+    a, b = y0.clone(), y0.clone()
+    down.rowstats(f, a, st2, residual=True)
+    down.rowstats(f, b, st2, residual=True, xpack=fp)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
