@@ -172,7 +172,7 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
 #pragma unroll
     for (int w = 0; w < DEC_NW; ++w) o += acc_s[w][d];
     orow[d] = o / sum;
-    if (a.oph) xpack_store(a.oph, a.opl, t0, h * HD + d, o / sum);
+    if (a.oph) xpack_store(a.oph, a.opl, t0, h * HD + d, o / sum, a.prb);
   }
 }
 
@@ -473,11 +473,11 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
-             tickets, keys_per_split, items ? 1 : T / n_items, g_oph, g_opl};
+             tickets, keys_per_split, items ? 1 : T / n_items, g_oph, g_opl, (T + 15) / 16};
   g_oph = g_opl = nullptr;   // one launch
   const bool dec = max_rows == 1 && (long long)maxb * PS <= DEC_MAXK;
-  FO_REQUIRE(!a.oph || (T <= 16 && (dec || nsplit == 1 || tickets)),
-             "fo_attention: packed output needs <= 16 tokens and no combine launch");
+  FO_REQUIRE(!a.oph || (T <= 64 && (dec || nsplit == 1 || tickets)),
+             "fo_attention: packed output needs <= 64 tokens and no combine launch");
   if (dec) {  // one query row per (session, head): decode kernel
     dim3 g1(n_items, H);
     if (hd == 128) hipLaunchKernelGGL((k_attn_decode<128>), g1, dim3(DEC_NT), 0, s, a);
@@ -513,7 +513,7 @@ int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, i
   FO_REQUIRE(lds <= 160 * 1024, "fo_relpos_attention_fused: ring of %d x %d exceeds LDS", cap, dk);
   uint16_t *oph = g_oph, *opl = g_opl;
   g_oph = g_opl = nullptr;   // one launch
-  FO_REQUIRE(!oph || B * T <= 32, "fo_relpos_attention_fused: packed output needs <= 32 rows");
+  FO_REQUIRE(!oph || B * T <= 64, "fo_relpos_attention_fused: packed output needs <= 64 rows");
   hipLaunchKernelGGL(k_relpos_fused, dim3(B, h), dim3(256), lds, s, qkv, ldq, kr, vr, cap, start, len, ring, ptab,
                      pstart, bu, bv, T, h, dk, scale, out, ldo, oph, opl, (B * T + 15) / 16);
   return fo::check_launch("fo_relpos_attention_fused");

@@ -21,9 +21,10 @@ struct AttnArgs {
   int* cnt;        // nullable: static nsplit splits + k_attn_combine
   int kps;
   int tnu;         // items NULL: tokens per item (item b = sequence b, tokens b*tnu .. b*tnu + tnu - 1)
-  // out also written packed for the next GEMM (tokens < 16; xpack_store: fo_attention_set_opack), or nullptr
+  // out also written packed for the next GEMM (<= 64 tokens; xpack_store: fo_attention_set_opack), or nullptr
   uint16_t* oph;
   uint16_t* opl;
+  int prb;         // its row blocks: ceil(T / 16)
 };
 
 constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
@@ -105,7 +106,7 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
     for (int q = 0; q < ns; ++q)
       if (w[q] != 0.f) o += po[(size_t)q * HD] * w[q];
     a.out[th * HD + d] = o * w[KT];
-    if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, o * w[KT]);
+    if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, o * w[KT], a.prb);
   }
 }
 
@@ -345,7 +346,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
       const int d = 16 * dt + col;
       if (ns == 1) {
         a.out[th * HD + d] = acc[n][i] / l;
-        if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, acc[n][i] / l);
+        if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, acc[n][i] / l, a.prb);
       } else {
         a.part_o[(th * a.nsplit + sp) * HD + d] = acc[n][i];
       }

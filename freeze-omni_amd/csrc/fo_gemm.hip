@@ -77,7 +77,7 @@ struct GemmArgs {
   // producer: yg (a next-norm input) or, without yg, Y also written packed the same way (fo_gemm_set_ypack)
   bf16_t* ypkh;
   bf16_t* ypkl;
-  int prb;   // packed row blocks of xph / ypkh: ceil(M / 16) (1 or 2)
+  int prb;   // packed row blocks of xph / ypkh: ceil(M / 16) (1..4)
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -305,7 +305,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     xr[r] = reinterpret_cast<const XT*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4);
   }
   // X given packed (GemmArgs::xph / xpl): only the k_gemm_xp instantiations read it (the others compile as before)
-  static_assert(!XPK || (RB <= 2 && XF32 && !LN && !SW && !PIPE), "packed X: <= 2-row-block plain / RoPE kernels");
+  static_assert(!XPK || (RB <= 4 && XF32 && !LN && !SW && !PIPE), "packed X: <= 4-row-block plain / RoPE kernels");
   const bool xpk = XPK && a.xph != nullptr;
   float ln_mu[RB], ln_rs[RB];
   // Whole groups of U k-steps are dealt to waves (all U weight loads of a group in flight
@@ -911,7 +911,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_ln(GemmArgs a) {
 template <int NT, int RB, int NW, int U, bool SW>
 void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStream_t s) {
   const size_t shm = 0;
-  if constexpr (RB <= 2 && !SW) {
+  if constexpr (RB <= 4 && !SW) {
     if (x_f32 && a.xph && !(RB == 1 && g_launch_pipe)) {   // X packed by its producer
       hipLaunchKernelGGL((k_gemm_xp<NT, RB, NW, U>), grid, dim3(NW * 64), shm, s, a);
       return;
@@ -931,6 +931,18 @@ void launch_gemm(bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, hipStre
     if (x_f32) hipLaunchKernelGGL((k_gemm<NT, RB, true, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
     else hipLaunchKernelGGL((k_gemm<NT, RB, false, NW, U, SW>), grid, dim3(NW * 64), shm, s, a);
   }
+}
+
+// 17..64-row fp32-X grid kernels (gemm_impl's mid path): X packed by its producer takes k_gemm_xp
+template <int NT, int RB, int NW, bool SW>
+void launch_mid(dim3 grid, const GemmArgs& a, hipStream_t s) {
+  if constexpr (!SW) {
+    if (a.xph) {
+      hipLaunchKernelGGL((k_gemm_xp<NT, RB, NW, 2>), grid, dim3(NW * 64), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_gemm_wstream<NT, RB, true, NW, 2, SW>), grid, dim3(NW * 64), 0, s, a);
 }
 
 thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
@@ -1386,8 +1398,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   g_xph = g_xpl = nullptr;   // one launch each
   g_ypkh = g_ypkl = nullptr;
   a.prb = (M + 15) / 16;
-  FO_REQUIRE(!a.xph || (x_f32 && M <= 32 && !lnw), "fo_gemm: packed X needs fp32 X of <= 32 rows");
-  FO_REQUIRE(!a.ypkh || (M <= 32 && !swiglu && !rope), "fo_gemm: packed output needs <= 32 plain rows");
+  FO_REQUIRE(!a.xph || (x_f32 && M <= 64 && !lnw), "fo_gemm: packed X needs fp32 X of <= 64 rows");
+  FO_REQUIRE(!a.ypkh || (M <= 64 && !swiglu && !rope), "fo_gemm: packed output needs <= 64 plain rows");
   FO_REQUIRE(!sout1 || sout, "fo_gemm: row sums come with the sums of squares");
   if (lnw) {
     FO_REQUIRE(lnb && x_f32 && M <= 64 && !swiglu && rstats && rstats1 && rgroups > 0 && rgroups <= 64 && !rope &&
@@ -1603,7 +1615,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   } else if (mid) {
     // 2 k-steps in flight per wave keep the RB x NT accumulators and fragments within 4 waves / SIMD
     const int nw = (NT == 4 || wgs >= 384) ? 4 : 8;
-#define FO_MID(NT_, RB_, NW_, SW_) hipLaunchKernelGGL((k_gemm_wstream<NT_, RB_, true, NW_, 2, SW_>), grid, dim3(NW_ * 64), 0, stream, a)
+#define FO_MID(NT_, RB_, NW_, SW_) launch_mid<NT_, RB_, NW_, SW_>(grid, a, stream)
 #define FO_MID_RB(NT_, NW_, SW_) { if (RB == 2) FO_MID(NT_, 2, NW_, SW_); else if (RB == 3) FO_MID(NT_, 3, NW_, SW_); else FO_MID(NT_, 4, NW_, SW_); }
     if (swiglu) {
       if (NT == 4) FO_MID_RB(4, 4, true) else if (nw == 4) FO_MID_RB(2, 4, true) else FO_MID_RB(2, 8, true)

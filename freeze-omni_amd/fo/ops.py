@@ -295,15 +295,15 @@ XPACK = os.environ.get("FO_XPACK", "1") != "0"
 
 
 class XPack:
-    """An fp32 activation of <= 32 rows also held as bf16 hi + lo in MFMA A-fragment order ([K/32][row blocks][64][8]
+    """An fp32 activation of <= 64 rows also held as bf16 hi + lo in MFMA A-fragment order ([K/32][row blocks][64][8]
     each; lane l = row l & 15 of the row block, columns 8 (l >> 4) .. + 8 of a 32-column k-step): its producer kernel writes it beside
     the fp32 rows, and the consuming one-row-tile GEMM reads one contiguous 1 KiB per wave and half instead of 16
     row segments per float4 (Qwen2 o 11.4 -> 9.2 us, q|k|v 13.7 -> 11.8 us at 16 rows, results bit-identical:
     scripts/gemm_xpack_probe.py)."""
 
     def __init__(self, K, device, rows=16):
-        if K % 32 or not 1 <= rows <= 32:
-            raise ValueError("XPack needs K % 32 == 0 and <= 32 rows")
+        if K % 32 or not 1 <= rows <= 64:
+            raise ValueError("XPack needs K % 32 == 0 and <= 64 rows")
         self.K, self.rows = K, rows
         n = K * 16 * ((rows + 15) // 16)   # [K/32][row blocks][64][8]
         self.hi = torch.empty(n, dtype=BF16, device=device)

@@ -188,9 +188,9 @@ class SpeechEncoderEngine:
                 "att": e(B * T, self.d), "f": e(B * T, self.layers[0]["ff1"].N),
                 "sA": ops.RowStats(B * T, dev, with_sums=True), "sB": ops.RowStats(B * T, dev, with_sums=True),
                 "meta": torch.empty(4 * B, dtype=I32, device=dev),
-                # <= 32 rows: the out and FFN-down inputs also written packed by their producers (ops.XPack)
-                "attp": ops.XPack(self.d, dev, B * T) if B * T <= 32 and ops.XPACK else None,
-                "fp": ops.XPack(self.layers[0]["ff1"].N, dev, B * T) if B * T <= 32 and ops.XPACK else None}
+                # <= 64 rows: the out and FFN-down inputs also written packed by their producers (ops.XPack)
+                "attp": ops.XPack(self.d, dev, B * T) if B * T <= 64 and ops.XPACK else None,
+                "fp": ops.XPack(self.layers[0]["ff1"].N, dev, B * T) if B * T <= 64 and ops.XPACK else None}
 
     def host_meta(self, caches, pe_indices):
         """Per-user ring / position metadata [starts | lens | rings | pos starts] and the next pe_index."""

@@ -68,9 +68,9 @@ class DecoderStack:
               "sA": ops.RowStats(T, device), "sB": ops.RowStats(T, device),
               "xg": torch.empty(T, self.D, dtype=F32, device=device),
               "tickets": torch.zeros(max(T, 2) * KVH, dtype=torch.int32, device=device)}
-        if 8 < T <= 16 and ops.XPACK:   # packed activations for the q|k|v and o inputs (ops.XPack)
-            ws["xgp"] = ops.XPack(self.D, device)
-            ws["attp"] = ops.XPack(H * hd, device)
+        if 8 < T <= 64 and ops.XPACK:   # packed activations for the q|k|v and o inputs (ops.XPack)
+            ws["xgp"] = ops.XPack(self.D, device, T)
+            ws["attp"] = ops.XPack(H * hd, device, T)
         if nsplit > 1:
             ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
@@ -96,11 +96,14 @@ class DecoderStack:
         # one token per sequence (decode) or the same count for every sequence, one work item each (a listen
         # chunk): the attention needs no item table (fo_attention items NULL)
         dense = ATTN_DENSE and (meta.n_items == T == meta.S or getattr(meta, "uniform", False))
-        # 9..16 rows (a listen chunk): the q|k|v input (the previous down projection's x*gamma) and the o input (the
-        # attention output) are also written packed by their producers and read packed (ops.XPack; layer 0's q|k|v
-        # input comes from the gather and stays fp32).  At <= 8 rows (text and AR decode steps) the X re-read is
-        # half as large and the extra stores cost more than the reads save (AR step 172.4 -> 177.1 us, r04zf)
-        xgp, attp = (ws.get("xgp"), ws.get("attp")) if 8 < T <= 16 else (None, None)
+        # 9..64 rows (a listen chunk, a duplex tick, a prefill): the q|k|v input (the previous down projection's
+        # x*gamma) and the o input (the attention output) are also written packed by their producers and read packed
+        # (ops.XPack; layer 0's q|k|v input comes from the gather and stays fp32).  At <= 8 rows (text and AR decode
+        # steps) the X re-read is half as large and the extra stores cost more than the reads save (AR step 172.4 ->
+        # 177.1 us, r04zf)
+        xgp, attp = ws.get("xgp"), ws.get("attp")
+        if not 8 < T <= 64 or xgp is None or xgp.rows < T:
+            xgp = attp = None
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,

@@ -1,4 +1,4 @@
-"""Packed <= 16-row activations (ops.XPack): every producer (the split-K reduce, the unsplit GEMM epilogue, the
+"""Packed <= 64-row activations (ops.XPack): every producer (the split-K reduce, the unsplit GEMM epilogue, the
 in-launch split merge, the multi-row and decode attention) writes exactly the bf16 hi / lo split of its fp32 output
 in fragment order, and a GEMM reading the packed copy gives bit-identical results to the one splitting fp32 X."""
 import math
@@ -23,6 +23,18 @@ def _pack(x):
     return f(hi), f(lo)
 
 
+def _pack_rb(x):
+    """fp32 [M <= 32, K] -> (hi, lo) [K/32][ceil(M/16)][64][8] bf16 (the two-row-block layout)."""
+    M, K = x.shape
+    rb = (M + 15) // 16
+    xf = torch.zeros(rb * 16, K, dtype=torch.float32, device=x.device)
+    xf[:M] = x
+    hi = xf.to(torch.bfloat16)
+    lo = (xf - hi.float()).to(torch.bfloat16)
+    f = lambda t: t.view(rb, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).reshape(-1)  # noqa: E731
+    return f(hi), f(lo), rb
+
+
 def _rows(flat, M, K):
     """the first M rows of a packed half back in [M, K] (bit patterns as int16)."""
     return flat.view(K // 32, 4, 16, 8).permute(2, 0, 1, 3).reshape(16, K)[:M].view(torch.int16)
@@ -35,7 +47,8 @@ def _check_packed(xp, y, M):
     assert torch.equal(_rows(xp.lo, M, K), _rows(lo, M, K))
 
 
-@pytest.mark.parametrize("M,N,K,splitk", [(16, 3584, 18944, 0), (12, 1024, 4096, 4), (16, 896, 896, 1), (9, 512, 256, 1)])
+@pytest.mark.parametrize("M,N,K,splitk", [(16, 3584, 18944, 0), (12, 1024, 4096, 4), (16, 896, 896, 1), (9, 512, 256, 1),
+                                           (40, 3584, 18944, 0), (48, 1024, 4096, 4)])
 def test_yg_producers_write_the_packed_split(dev, M, N, K, splitk):
     """stats_out's yg also packed: k_gemm_reduce (split-K), the unsplit epilogue, the in-launch merge (small weights)."""
     g = torch.Generator(device="cpu").manual_seed(M + N + K + splitk)
@@ -45,24 +58,28 @@ def test_yg_producers_write_the_packed_split(dev, M, N, K, splitk):
     gamma = (1 + 0.1 * torch.randn(N, generator=g)).to(dev)
     st = ops.RowStats(M, dev)
     yg = torch.empty(M, N, device=dev)
-    xp = ops.XPack(N, dev)
+    xp = ops.XPack(N, dev, M)
     xp.hi.fill_(0)
     xp.lo.fill_(0)
     out = res.clone()
     lin(x, out=out, residual=True, M=M, splitk=splitk, stats_out=st.set(gamma, yg), ypack=xp)
     torch.cuda.synchronize()
-    _check_packed(xp, yg, M)
+    hi, lo, rb = _pack_rb(yg)
+    view = lambda t: t[:N * 16 * rb].view(N // 32, rb, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(rb * 16, N)[:M]  # noqa
+    assert torch.equal(view(xp.hi).view(torch.int16), view(hi).view(torch.int16))
+    assert torch.equal(view(xp.lo).view(torch.int16), view(lo).view(torch.int16))
 
 
-@pytest.mark.parametrize("M,N,K,rope", [(16, 3584, 3584, False), (11, 896, 896, False), (16, 4608, 3584, True)])
+@pytest.mark.parametrize("M,N,K,rope", [(16, 3584, 3584, False), (11, 896, 896, False), (16, 4608, 3584, True),
+                                        (48, 3584, 3584, False), (40, 4608, 3584, True), (56, 1024, 1024, False)])
 def test_packed_x_gemm_is_bit_identical(dev, M, N, K, rope):
-    """The one-row-tile GEMM reading X packed equals the one splitting fp32 X, bit for bit (o-style residual
-    epilogue, and the q|k|v RoPE + paged-KV append epilogue)."""
+    """The GEMM reading X packed equals the one splitting fp32 X, bit for bit (o-style residual epilogue, and the
+    q|k|v RoPE + paged-KV append epilogue; one-row-tile kernels and the 17..64-row ones)."""
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
     w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(dev)
     x = torch.randn(M, K, generator=g).to(dev)
-    xp = ops.XPack(K, dev)
-    h, lo = _pack(x)
+    xp = ops.XPack(K, dev, M)
+    h, lo, _ = _pack_rb(x)
     xp.hi.copy_(h)
     xp.lo.copy_(lo)
     if not rope:
@@ -120,18 +137,6 @@ def test_attention_writes_the_packed_split(dev, H, KVH, hd, tokens):
                   keys_per_split=128, opack=xp)
     torch.cuda.synchronize()
     _check_packed(xp, out, T)
-
-
-def _pack_rb(x):
-    """fp32 [M <= 32, K] -> (hi, lo) [K/32][ceil(M/16)][64][8] bf16 (the two-row-block layout)."""
-    M, K = x.shape
-    rb = (M + 15) // 16
-    xf = torch.zeros(rb * 16, K, dtype=torch.float32, device=x.device)
-    xf[:M] = x
-    hi = xf.to(torch.bfloat16)
-    lo = (xf - hi.float()).to(torch.bfloat16)
-    f = lambda t: t.view(rb, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).reshape(-1)  # noqa: E731
-    return f(hi), f(lo), rb
 
 
 @pytest.mark.parametrize("M", [32, 27, 20])
