@@ -50,6 +50,12 @@ __device__ __forceinline__ void xpack_store(uint16_t* hp, uint16_t* lp, int m, i
   hp[o] = __builtin_bit_cast(uint16_t, h);
   lp[o] = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));
 }
+// The same fragment order for an fp32 copy (a LayerNorm-on-load consumer needs the exact fp32 values): lane l of
+// k-step ks, row block b holds its 8 floats contiguously at ((ks * rbs + b) * 64 + l) * 8.
+__device__ __forceinline__ void xpack32_store(float* p, int m, int n, float v, int rbs) {
+  const int c = n & 31;
+  p[((size_t)(((n >> 5) * rbs + (m >> 4)) * 64 + ((c >> 3) << 4) + (m & 15))) * 8 + (c & 7)] = v;
+}
 // round-to-nearest-even f32 -> bf16 (NaN kept NaN)
 __device__ __forceinline__ bf16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);

@@ -78,6 +78,10 @@ struct GemmArgs {
   bf16_t* ypkh;
   bf16_t* ypkl;
   int prb;   // packed row blocks of xph / ypkh: ceil(M / 16) (1..4)
+  // the fp32 form of the same order for a LayerNorm-on-load consumer (the encoder's residual stream):
+  // producer yp32 (fo_gemm_set_ypack32, its output Y), consumer xp32 (fo_gemm_set_xpack32, k_gemm_ln only)
+  float* yp32;
+  const float* xp32;
 };
 
 // XF32: X is fp32 and is split per element into bf16 hi + bf16 lo (two MFMAs against the same
@@ -327,7 +331,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         for (int t = 0; t < NT; ++t) lnbv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)k * 64);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
+          const float4* q = a.xp32 ? reinterpret_cast<const float4*>(a.xp32 + (((size_t)k * a.prb + r) * 64 + lane) * 8)
+                                   : reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
           lnxv[u][r][0] = q[0];
           lnxv[u][r][1] = q[1];
         }
@@ -369,7 +374,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   // X fragment of row block r at k-step ks (LayerNorm applied on load when LN)
   auto ldx = [&](int r, int ks, bf16x8& hi, bf16x8& lo) {
     if constexpr (LN) {
-      const float* p = reinterpret_cast<const float*>(xr[r] + (size_t)ks * 32);
+      const float* p = a.xp32 ? a.xp32 + (((size_t)ks * a.prb + r) * 64 + lane) * 8
+                              : reinterpret_cast<const float*>(xr[r] + (size_t)ks * 32);
       const int k0 = ks * 32 + 8 * (lane >> 4);
       const float4 a0 = reinterpret_cast<const float4*>(p)[0], a1 = reinterpret_cast<const float4*>(p)[1];
       const float4 w0 = *reinterpret_cast<const float4*>(a.lnw + k0), w1 = *reinterpret_cast<const float4*>(a.lnw + k0 + 4);
@@ -725,6 +731,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         else reinterpret_cast<float*>(a.Y)[o] = v;
         red[0][e_lt][e_rr][e_c] = v;
         if (a.ypkh && !a.yg) xpack_store(a.ypkh, a.ypkl, m, n, v, a.prb);   // Y is the next GEMM's packed input
+        if (a.yp32) xpack32_store(a.yp32, m, n, v, a.prb);
       }
     }
   } else
@@ -738,6 +745,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
     else y = epilogue_store(a, false, m, n, red[0][lt][rr][c], 0.f);
     if (!SW) red[0][lt][rr][c] = y;
     if (a.ypkh && !a.yg) xpack_store(a.ypkh, a.ypkl, m, n, y, a.prb);   // Y is the next GEMM's packed input
+    if (a.yp32) xpack32_store(a.yp32, m, n, y, a.prb);
   }
   if (!SW && a.sout) {
     // row partial sums of squares of this workgroup's LT*16 output columns, for the next norm
@@ -855,6 +863,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       if (a.out_bf16) reinterpret_cast<bf16_t*>(a.Y)[o] = f2bf(y);
       else reinterpret_cast<float*>(a.Y)[o] = y;
       if (a.ypkh && !a.yg) xpack_store(a.ypkh, a.ypkl, m, n, y, a.prb);   // Y is the next GEMM's packed input
+      if (a.yp32) xpack32_store(a.yp32, m, n, y, a.prb);
     }
   }
   if (a.sout && !sw) {
@@ -950,6 +959,8 @@ thread_local const void* g_xph = nullptr;           // fo_gemm_set_xpack: the ne
 thread_local const void* g_xpl = nullptr;
 thread_local void* g_ypkh = nullptr;                // fo_gemm_set_ypack: the next launch's packed yg output
 thread_local void* g_ypkl = nullptr;
+thread_local float* g_yp32 = nullptr;               // fo_gemm_set_ypack32 / _xpack32: fp32 fragment-order copies
+thread_local const float* g_xp32 = nullptr;
 
 // forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
 thread_local int g_force_nw = 0, g_force_nt = 0;
@@ -1395,8 +1406,14 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.xpl = reinterpret_cast<const bf16x8*>(g_xpl);
   a.ypkh = reinterpret_cast<bf16_t*>(g_ypkh);
   a.ypkl = reinterpret_cast<bf16_t*>(g_ypkl);
+  a.yp32 = g_yp32;
+  a.xp32 = g_xp32;
   g_xph = g_xpl = nullptr;   // one launch each
   g_ypkh = g_ypkl = nullptr;
+  g_yp32 = nullptr;
+  g_xp32 = nullptr;
+  FO_REQUIRE(!a.xp32 || (lnw && M <= 64), "fo_gemm: the fp32 packed X is read by LayerNorm-on-load launches only");
+  FO_REQUIRE(!a.yp32 || (M <= 64 && !swiglu && !rope), "fo_gemm: fp32 packed output needs <= 64 plain rows");
   a.prb = (M + 15) / 16;
   FO_REQUIRE(!a.xph || (x_f32 && M <= 64 && !lnw), "fo_gemm: packed X needs fp32 X of <= 64 rows");
   FO_REQUIRE(!a.ypkh || (M <= 64 && !swiglu && !rope), "fo_gemm: packed output needs <= 64 plain rows");
@@ -1774,6 +1791,16 @@ int fo_gemm_set_xpack(const void* hi, const void* lo) {
   FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_gemm_set_xpack: both halves or neither");
   g_xph = hi;
   g_xpl = lo;
+  return 0;
+}
+
+int fo_gemm_set_ypack32(void* p) {
+  g_yp32 = reinterpret_cast<float*>(p);
+  return 0;
+}
+
+int fo_gemm_set_xpack32(const void* p) {
+  g_xp32 = reinterpret_cast<const float*>(p);
   return 0;
 }
 

@@ -64,6 +64,8 @@ _SIGS = {
     "fo_gemm_set_trace": (c_int, [c_vp]),
     "fo_gemm_set_xpack": (c_int, [c_vp, c_vp]),
     "fo_gemm_set_ypack": (c_int, [c_vp, c_vp]),
+    "fo_gemm_set_ypack32": (c_int, [c_vp]),
+    "fo_gemm_set_xpack32": (c_int, [c_vp]),
     "fo_attention_set_opack": (c_int, [c_vp, c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),

@@ -200,7 +200,7 @@ class PackedLinear:
         return out
 
 
-    def ln(self, x, lnw, lnb, stats, eps=1e-5, out=None, act="none", M=None, splitk=0, ypack=None):
+    def ln(self, x, lnw, lnb, stats, eps=1e-5, out=None, act="none", M=None, splitk=0, ypack=None, xpack32=None):
         """act(LayerNorm(x) W^T + b) with the norm applied as X is loaded (fo_gemm_ln; M <= 64); stats:
         the RowStats(with_sums=True) a rowstats() producer filled for x."""
         _check_dev(x)
@@ -212,14 +212,14 @@ class PackedLinear:
         if out is None:
             out = torch.empty(M, self.N, dtype=F32, device=x.device)
         rt = Runtime.get(x.device)
-        with _packed(None, ypack):
+        with _packed(None, ypack, xpack32):
             _lib.call("fo_gemm_ln", x.data_ptr(), x.stride(0), M, self.Kp, self.packed.data_ptr(), self.N,
                       ptr(self.bias), lnw.data_ptr(), lnb.data_ptr(), float(eps), stats.buf1.data_ptr(),
                       stats.buf.data_ptr(), stats.groups, out.data_ptr(), out.stride(0), ACT[act], rt.ws.data_ptr(),
                       rt.ws.numel(), splitk, stream(x.device))
         return out
 
-    def rowstats(self, x, out, stats, residual=False, act="none", M=None, splitk=0, xpack=None):
+    def rowstats(self, x, out, stats, residual=False, act="none", M=None, splitk=0, xpack=None, ypack32=None):
         """fp32 GEMM that also fills stats (per-row partial sums of out and out^2) for ln()."""
         import ctypes
         _check_dev(x)
@@ -228,7 +228,7 @@ class PackedLinear:
             raise ValueError("rowstats needs RowStats(with_sums=True)")
         rt = Runtime.get(x.device)
         sg = ctypes.c_int(0)
-        with _packed(xpack, None):
+        with _packed(xpack, None, None, ypack32):
             _lib.call("fo_gemm_rowstats", x.data_ptr(), 1 if x.dtype == F32 else 0, x.stride(0), M, self.Kp,
                       self.packed.data_ptr(), self.N, ptr(self.bias), out.data_ptr(), out.stride(0), ACT[act],
                       1 if residual else 0, rt.ws.data_ptr(), rt.ws.numel(), rt.counters.data_ptr(), splitk,
@@ -310,18 +310,34 @@ class XPack:
         self.lo = torch.empty(n, dtype=BF16, device=device)
 
 
+class XPack32:
+    """The fp32 form of XPack's fragment order ([K/32][row blocks][64][8] floats): the speech encoder's residual
+    stream for its LayerNorm-on-load GEMMs, which need the exact fp32 values (written by the out / FFN-down GEMMs
+    beside the row-major rows)."""
+
+    def __init__(self, K, device, rows):
+        if K % 32 or not 1 <= rows <= 64:
+            raise ValueError("XPack32 needs K % 32 == 0 and <= 64 rows")
+        self.K, self.rows = K, rows
+        self.buf = torch.empty(K * 16 * ((rows + 15) // 16), dtype=F32, device=device)
+
+
 class _packed:
     """Arms fo_gemm's packed-X input / packed-yg output for the one launch inside the block (thread-local in the
     library, consumed by that launch); a launch that raises leaves nothing armed for the next one."""
 
-    def __init__(self, xpack, ypack):
-        self.x, self.y = xpack, ypack
+    def __init__(self, xpack, ypack, xpack32=None, ypack32=None):
+        self.x, self.y, self.x32, self.y32 = xpack, ypack, xpack32, ypack32
 
     def __enter__(self):
         if self.x is not None:
             _lib.call("fo_gemm_set_xpack", self.x.hi.data_ptr(), self.x.lo.data_ptr())
         if self.y is not None:
             _lib.call("fo_gemm_set_ypack", self.y.hi.data_ptr(), self.y.lo.data_ptr())
+        if self.x32 is not None:
+            _lib.call("fo_gemm_set_xpack32", self.x32.buf.data_ptr())
+        if self.y32 is not None:
+            _lib.call("fo_gemm_set_ypack32", self.y32.buf.data_ptr())
 
     def __exit__(self, et, ev, tb):
         if et is not None:
@@ -329,6 +345,10 @@ class _packed:
                 _lib.call("fo_gemm_set_xpack", None, None)
             if self.y is not None:
                 _lib.call("fo_gemm_set_ypack", None, None)
+            if self.x32 is not None:
+                _lib.call("fo_gemm_set_xpack32", None)
+            if self.y32 is not None:
+                _lib.call("fo_gemm_set_ypack32", None)
         return False
 
 

@@ -190,7 +190,8 @@ class SpeechEncoderEngine:
                 "meta": torch.empty(4 * B, dtype=I32, device=dev),
                 # <= 64 rows: the out and FFN-down inputs also written packed by their producers (ops.XPack)
                 "attp": ops.XPack(self.d, dev, B * T) if B * T <= 64 and ops.XPACK else None,
-                "fp": ops.XPack(self.layers[0]["ff1"].N, dev, B * T) if B * T <= 64 and ops.XPACK else None}
+                "fp": ops.XPack(self.layers[0]["ff1"].N, dev, B * T) if B * T <= 64 and ops.XPACK else None,
+                "xp32": ops.XPack32(self.d, dev, B * T) if B * T <= 64 and ops.XPACK else None}
 
     def host_meta(self, caches, pe_indices):
         """Per-user ring / position metadata [starts | lens | rings | pos starts] and the next pe_index."""
@@ -232,25 +233,25 @@ class SpeechEncoderEngine:
         # pre-norms applied by the GEMMs on load (fo_gemm_ln) from the residual producers' row sums
         fuse_ln = B * T <= 64 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
         sA, sB = bufs["sA"], bufs["sB"]
-        attp, fp = (bufs.get("attp"), bufs.get("fp")) if fuse_ln else (None, None)
+        attp, fp, xp32 = (bufs.get("attp"), bufs.get("fp"), bufs.get("xp32")) if fuse_ln else (None, None, None)
         last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
             if fuse_ln and i > 0:
-                L["qkv"].ln(x, *L["ln1"], sA, out=qkv)
+                L["qkv"].ln(x, *L["ln1"], sA, out=qkv, xpack32=xp32)
             else:
                 ops.layernorm(x, *L["ln1"], out=h)
                 L["qkv"](h, out=qkv)
             ops.relpos_attention_fused(qkv, self.kr[i], self.vr[i], self.cap, st, ln, rg, self.ptab[i], ps,
                                        L["bu"], L["bv"], B, T, self.h, self.dk, scale, att, opack=attp)
             if fuse_ln:
-                L["out"].rowstats(att, x, sB, residual=True, xpack=attp)
-                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp)
+                L["out"].rowstats(att, x, sB, residual=True, xpack=attp, ypack32=xp32)
+                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp, xpack32=xp32)
             else:
                 L["out"](att, out=x, residual=True)
                 ops.layernorm(x, *L["ln2"], out=h)
                 L["ff1"](h, out=f, act="relu")
             if fuse_ln and i < last:
-                L["ff2"].rowstats(f, x, sA, residual=True, xpack=fp)
+                L["ff2"].rowstats(f, x, sA, residual=True, xpack=fp, ypack32=xp32)
             else:
                 L["ff2"](f, out=x, residual=True, xpack=fp)
         ops.layernorm(x, *self.after, out=x)

@@ -110,6 +110,11 @@ int fo_gemm_set_xpack(const void* hi, const void* lo);
  * (stats_out) -- or, without one, its output Y -- packed as fo_gemm_set_xpack reads it (hi, lo: [N/32][ceil(M/16)][64][8]
  * bf16).  Both or neither. */
 int fo_gemm_set_ypack(void* hi, void* lo);
+/* fp32 form of the same fragment order ([N/32][ceil(M/16)][64][8] floats, the exact values): the next fo_gemm* launch
+ * (<= 64 rows, plain epilogue) also writes its output Y there (ypack32); the next fo_gemm_ln launch reads its X from
+ * there instead of the row-major rows (xpack32; bit-identical).  NULL disarms. */
+int fo_gemm_set_ypack32(void* p);
+int fo_gemm_set_xpack32(const void* p);
 /* the calling thread's NEXT fo_attention (<= 16 tokens, not with the separate combine launch) or
  * fo_relpos_attention_fused (<= 32 rows) launch also writes its output packed as fo_gemm_set_xpack reads it (hi, lo:
  * [cols/32][ceil(rows/16)][64][8] bf16).  Both or neither. */

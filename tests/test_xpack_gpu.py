@@ -173,3 +173,28 @@ def test_two_row_block_packing_layernorm_producer_and_rowstats_consumer(dev, M):
     down.rowstats(f, b, st2, residual=True, xpack=fp)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M", [32, 27, 56])
+def test_fp32_fragment_copy_feeds_the_layernorm_gemm_bit_identically(dev, M):
+    """The encoder's residual stream in fp32 fragment order (ops.XPack32): written by the producer GEMM beside its
+    rows, read by the LayerNorm-on-load GEMM -- the same output bit for bit."""
+    g = torch.Generator(device="cpu").manual_seed(M + 5)
+    D, F = 256, 512
+    prod = ops.PackedLinear((torch.randn(D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(dev))
+    up = ops.PackedLinear((torch.randn(F, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(dev),
+                          torch.randn(F, generator=g).to(dev))
+    x = torch.randn(M, D, generator=g).to(dev)
+    st = ops.RowStats(M, dev, with_sums=True)
+    xr = torch.randn(M, D, generator=g).to(dev)
+    p32 = ops.XPack32(D, dev, M)
+    prod.rowstats(x, xr, st, residual=True, ypack32=p32)
+    lnw = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    lnb = (0.1 * torch.randn(D, generator=g)).to(dev)
+    a = up.ln(xr, lnw, lnb, st, act="relu")
+    b = up.ln(xr, lnw, lnb, st, act="relu", xpack32=p32)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    rb = (M + 15) // 16
+    back = p32.buf.view(D // 32, rb, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(rb * 16, D)[:M]
+    assert torch.equal(back, xr)
