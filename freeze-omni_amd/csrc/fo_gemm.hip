@@ -331,7 +331,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         for (int t = 0; t < NT; ++t) lnbv[u][t] = __builtin_nontemporal_load(bp[t] + (size_t)k * 64);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          const float4* q = a.xp32 ? reinterpret_cast<const float4*>(a.xp32 + (((size_t)k * a.prb + r) * 64 + lane) * 8)
+          const float4* q = a.xp32 ? reinterpret_cast<const float4*>(a.xp32 + (((size_t)k * a.prb + min((m0 >> 4) + r, a.prb - 1)) * 64 + lane) * 8)
                                    : reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
           lnxv[u][r][0] = q[0];
           lnxv[u][r][1] = q[1];
@@ -374,7 +374,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   // X fragment of row block r at k-step ks (LayerNorm applied on load when LN)
   auto ldx = [&](int r, int ks, bf16x8& hi, bf16x8& lo) {
     if constexpr (LN) {
-      const float* p = a.xp32 ? a.xp32 + (((size_t)ks * a.prb + r) * 64 + lane) * 8
+      const float* p = a.xp32 ? a.xp32 + (((size_t)ks * a.prb + min((m0 >> 4) + r, a.prb - 1)) * 64 + lane) * 8
                               : reinterpret_cast<const float*>(xr[r] + (size_t)ks * 32);
       const int k0 = ks * 32 + 8 * (lane >> 4);
       const float4 a0 = reinterpret_cast<const float4*>(p)[0], a1 = reinterpret_cast<const float4*>(p)[1];
@@ -392,8 +392,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
       }
     } else {
       if (XF32 && xpk) {
-        hi = a.xph[((size_t)ks * a.prb + r) * 64 + lane];
-        lo = a.xpl[((size_t)ks * a.prb + r) * 64 + lane];
+        hi = a.xph[((size_t)ks * a.prb + min((m0 >> 4) + r, a.prb - 1)) * 64 + lane];
+        lo = a.xpl[((size_t)ks * a.prb + min((m0 >> 4) + r, a.prb - 1)) * 64 + lane];
       } else {
         load_x<XT, XF32>(xr[r] + (size_t)ks * 32, hi, lo);
       }
@@ -522,8 +522,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
         for (int r = 0; r < RB; ++r) {
           if constexpr (XF32) {
             if (xpk) {
-              xf0[u][r][0] = __builtin_bit_cast(float4, a.xph[((size_t)k * a.prb + r) * 64 + lane]);
-              xf0[u][r][1] = __builtin_bit_cast(float4, a.xpl[((size_t)k * a.prb + r) * 64 + lane]);
+              xf0[u][r][0] = __builtin_bit_cast(float4, a.xph[((size_t)k * a.prb + min((m0 >> 4) + r, a.prb - 1)) * 64 + lane]);
+              xf0[u][r][1] = __builtin_bit_cast(float4, a.xpl[((size_t)k * a.prb + min((m0 >> 4) + r, a.prb - 1)) * 64 + lane]);
             } else {
               const float4* q = reinterpret_cast<const float4*>(xr[r] + (size_t)k * 32);
               xf0[u][r][0] = q[0];
