@@ -1033,7 +1033,13 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
   issue(w1, ub < ue ? 2 * ub + 1 : a.ntiles);
   // X slice (hi in registers, lo in LDS); rows >= M clamp to the last row (computed, never stored)
   bf16x8 xh[KPW];
-  {
+  if (a.xph) {   // X packed by its producer (GemmArgs::xph / xpl): the fragments as they are
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      xh[j] = a.xph[(size_t)(wave * KPW + j) * 64 + lane];
+      xlo[wave][j][lane] = a.xpl[(size_t)(wave * KPW + j) * 64 + lane];
+    }
+  } else {
     const int row = min(lane & 15, a.M - 1);
     const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4) +
                       (size_t)wave * KPW * 32;

@@ -118,8 +118,8 @@ class DecoderStack:
                           meta.block_table, self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale,
                           nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps,
                           opack=attp)
-            L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg), xpack=attp)
-            L.gu(xg, out=m, M=T, norm=(sB, self.eps))
+            L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg), xpack=attp, ypack=xgp)
+            L.gu(xg, out=m, M=T, norm=(sB, self.eps), xpack=xgp)
             if i == last and final_norm is None:
                 L.down(m, out=x, residual=True, M=T)
             elif i == last:

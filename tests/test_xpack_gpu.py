@@ -198,3 +198,21 @@ def test_fp32_fragment_copy_feeds_the_layernorm_gemm_bit_identically(dev, M):
     rb = (M + 15) // 16
     back = p32.buf.view(D // 32, rb, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(rb * 16, D)[:M]
     assert torch.equal(back, xr)
+
+
+@pytest.mark.parametrize("M", [16, 11])
+def test_xstationary_gate_up_reads_packed_x_bit_identically(dev, M):
+    """The Qwen2 gate/up X-stationary stream (k_gemm_xs) loading its X slice packed: the same SwiGLU output."""
+    g = torch.Generator(device="cpu").manual_seed(M + 99)
+    D, I = 3584, 18944
+    lin = ops.PackedLinear((torch.randn(I, D, generator=g) * 0.02).to(torch.bfloat16).to(dev),
+                           swiglu_up=(torch.randn(I, D, generator=g) * 0.02).to(torch.bfloat16).to(dev))
+    x = torch.randn(M, D, generator=g).to(dev)
+    xp = ops.XPack(D, dev, M)
+    h, lo, _ = _pack_rb(x)
+    xp.hi.copy_(h)
+    xp.lo.copy_(lo)
+    a = lin(x, M=M)
+    b = lin(x, M=M, xpack=xp)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
