@@ -906,6 +906,21 @@ def run_duplex(eng, args, seconds, sync, probe=False):
             "stages": stages}
 
 
+def dist_info(dist, world):
+    """The process group the run used (None: a single process without a launcher)."""
+    if dist is None:
+        return None
+    import torch
+    be = dist.get_backend()
+    v = None
+    if be == "nccl":
+        try:
+            v = ".".join(str(x) for x in torch.cuda.nccl.version())
+        except Exception:
+            v = None
+    return {"backend": be, "rccl_version": v, "world_size": world}
+
+
 def topology(world):
     """n_gpus = GPUs the job ran on: a FO_DIST_REHEARSAL run puts every rank on cuda:0, so it is one GPU (its ranks
     are replicas sharing that GPU, not a scaling point)."""
@@ -990,6 +1005,7 @@ def main_duplex(args, eng, dev, dist, world, rank, load_s):
             "dialog_ss": c["dialog_ss"], "load_s": round(load_s, 2),
             "roofline": duplex_roofline(pr, eng),
             "tick_stage_ms": duplex_stage_split(pr),
+            "dist": dist_info(dist, world),
             "cpu_baseline": None,
         }
         s = json.dumps(line)
@@ -1018,7 +1034,10 @@ def main():
     rehearsal = os.environ.get("FO_DIST_REHEARSAL") == "1"
     if rehearsal:
         local = 0
-    if world > 1:
+    # every torch.distributed.run rank joins the process group, at world 1 too: the launcher path, RCCL init, the
+    # weight broadcast and the checksum all_gather are one code path whatever N is
+    launched = "WORLD_SIZE" in os.environ and "RANK" in os.environ
+    if world > 1 or launched:
         import torch.distributed as dist
         if rehearsal:
             dist.init_process_group("gloo")
@@ -1156,6 +1175,7 @@ def main():
             "rtf_per_user_p50": round(float(np.percentile(rtf_user, 50)), 3) if rtf_user else None,
             "load_s": round(load_s, 2), "weight_broadcast_s": None if bcast_s is None else round(bcast_s, 3),
             "weight_broadcast_bytes": bcast_bytes, "weights_verified": weights_verified,
+            "dist": dist_info(dist, world),
             "roofline": {"bound": "hbm", "achieved": round(probe["gbps"], 1), "peak": peak, "unit": "GB/s",
                          "frac": round(probe["gbps"] / peak, 4),
                          "traffic": None if traffic is None else round(traffic),

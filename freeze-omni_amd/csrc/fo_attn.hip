@@ -92,7 +92,10 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
   for (int d = tid; d < HD; d += DEC_NT) q_s[d] = qr[d] * a.scale;
   float* orow = a.out + ((size_t)t0 * a.H + h) * HD;
   if (L > DEC_MAXK || (L + a.PS - 1) / a.PS > nb) {  // host contract broken: poison, never read wrong keys
-    if (tid < HD) orow[tid] = NAN;
+    for (int d = tid; d < HD; d += DEC_NT) {
+      orow[d] = NAN;   // (and the packed copy the next GEMM reads, when armed)
+      if (a.oph) xpack_store(a.oph, a.opl, t0, h * HD + d, NAN, a.prb);
+    }
     return;
   }
   __syncthreads();
@@ -416,8 +419,10 @@ inline int attn_waves() {
   return g_attn_nw;
 }
 
-thread_local uint16_t* g_oph = nullptr;   // fo_attention_set_opack: the next launch's packed output
+// fo_attention_set_opack: the next launch's packed output and its extent (columns, allocated row blocks)
+thread_local uint16_t* g_oph = nullptr;
 thread_local uint16_t* g_opl = nullptr;
+thread_local int g_op_cols = 0, g_op_rb = 0;
 
 inline int grid_for(long long n) {
   long long g = (n + 255) / 256;
@@ -428,10 +433,17 @@ inline int grid_for(long long n) {
 
 extern "C" {
 
-int fo_attention_set_opack(void* hi, void* lo) {
+int fo_attention_set_opack(void* hi, void* lo, int cols, int cap_rb) {
+  g_oph = g_opl = nullptr;
+  g_op_cols = g_op_rb = 0;
   FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_attention_set_opack: both halves or neither");
+  if (!hi) return 0;
+  FO_REQUIRE(cols > 0 && (cols & 31) == 0 && cap_rb >= 1 && cap_rb <= 4,
+             "fo_attention_set_opack: cols %d (a multiple of 32) and 1..4 row blocks (%d) required", cols, cap_rb);
   g_oph = reinterpret_cast<uint16_t*>(hi);
   g_opl = reinterpret_cast<uint16_t*>(lo);
+  g_op_cols = cols;
+  g_op_rb = cap_rb;
   return 0;
 }
 
@@ -466,15 +478,21 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
                  const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
                  float scale, int nsplit, float* part_ml, float* part_o, float* out, int* tickets,
                  int keys_per_split, hipStream_t s) {
+  uint16_t *oph = g_oph, *opl = g_opl;   // the armed packed output is consumed by this launch whatever happens
+  const int op_cols = g_op_cols, op_rb = g_op_rb;
+  g_oph = g_opl = nullptr;
+  g_op_cols = g_op_rb = 0;
   FO_REQUIRE(T > 0 && n_items > 0 && KVH > 0 && H % KVH == 0, "fo_attention: bad shape");
+  FO_REQUIRE(!oph || (op_cols == H * hd && op_rb * 16 >= T),
+             "fo_attention: packed output of %d columns x %d row blocks armed for %d x %d tokens", op_cols, op_rb,
+             H * hd, T);
   FO_REQUIRE(items || T % n_items == 0, "fo_attention: items NULL needs T / n_items tokens per item");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
   FO_REQUIRE(max_rows >= 1 && max_rows <= 16, "fo_attention: %d query rows per item (max 16)", max_rows);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
-             tickets, keys_per_split, items ? 1 : T / n_items, g_oph, g_opl, (T + 15) / 16};
-  g_oph = g_opl = nullptr;   // one launch
+             tickets, keys_per_split, items ? 1 : T / n_items, oph, opl, (T + 15) / 16};
   const bool dec = max_rows == 1 && (long long)maxb * PS <= DEC_MAXK;
   FO_REQUIRE(!a.oph || (T <= 64 && (dec || nsplit == 1 || tickets)),
              "fo_attention: packed output needs <= 64 tokens and no combine launch");
@@ -483,6 +501,8 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
     if (hd == 128) hipLaunchKernelGGL((k_attn_decode<128>), g1, dim3(DEC_NT), 0, s, a);
     else if (hd == 64) hipLaunchKernelGGL((k_attn_decode<64>), g1, dim3(DEC_NT), 0, s, a);
     else hipLaunchKernelGGL((k_attn_decode<32>), g1, dim3(DEC_NT), 0, s, a);
+    fo::count_launch(FO_L_ATTN_DECODE);
+    if (a.oph) fo::count_launch(FO_L_ATTN_OPACK);
     return fo::check_launch("fo_attention/decode");
   }
   dim3 grid(n_items, KVH, nsplit);
@@ -490,6 +510,8 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   else if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
   else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_attn_mfma<32>), grid, dim3(256), 0, s, a);
+  fo::count_launch(FO_L_ATTN_MFMA);
+  if (a.oph) fo::count_launch(FO_L_ATTN_OPACK);
   int rc = fo::check_launch("fo_attention/rows");
   if (rc || nsplit == 1 || tickets) return rc;
   hipLaunchKernelGGL(k_attn_combine, dim3(T, H), dim3(hd < 64 ? 64 : hd), 0, s, a, hd);
@@ -508,14 +530,20 @@ int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, i
                               const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
                               const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,
                               hipStream_t s) {
+  uint16_t *oph = g_oph, *opl = g_opl;   // consumed by this launch whatever happens
+  const int op_cols = g_op_cols, op_rb = g_op_rb;
+  g_oph = g_opl = nullptr;
+  g_op_cols = g_op_rb = 0;
+  FO_REQUIRE(!oph || (op_cols == h * dk && op_rb * 16 >= B * T),
+             "fo_relpos_attention_fused: packed output of %d columns x %d row blocks armed for %d x %d rows", op_cols,
+             op_rb, h * dk, B * T);
   FO_REQUIRE(T >= 1 && T <= cap && dk % 4 == 0 && (ldq % 4) == 0, "fo_relpos_attention_fused: T=%d dk=%d", T, dk);
   const size_t lds = (size_t)(3 * cap * (dk + 4) + 2 * T * dk + T * cap) * sizeof(float);
   FO_REQUIRE(lds <= 160 * 1024, "fo_relpos_attention_fused: ring of %d x %d exceeds LDS", cap, dk);
-  uint16_t *oph = g_oph, *opl = g_opl;
-  g_oph = g_opl = nullptr;   // one launch
-  FO_REQUIRE(!oph || B * T <= 64, "fo_relpos_attention_fused: packed output needs <= 64 rows");
   hipLaunchKernelGGL(k_relpos_fused, dim3(B, h), dim3(256), lds, s, qkv, ldq, kr, vr, cap, start, len, ring, ptab,
                      pstart, bu, bv, T, h, dk, scale, out, ldo, oph, opl, (B * T + 15) / 16);
+  fo::count_launch(FO_L_RELPOS);
+  if (oph) fo::count_launch(FO_L_ATTN_OPACK);
   return fo::check_launch("fo_relpos_attention_fused");
 }
 

@@ -178,7 +178,28 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   }
   const int pb0 = c0 / a.PS, npg = (c1 - 1) / a.PS - pb0 + 1;
   if (npg > MAXPG || (whole && (c1 - 1) / a.PS >= a.maxb)) {  // host contract broken: poison, never read wrong keys
-    for (int r = tid; r < R; r += NTH) a.out[((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD] = NAN;
+    // the item's rows become NaN wherever they are read: one split writes out (and the packed copy the next GEMM
+    // reads) directly; a split of several publishes a poisoned partial (m = +inf, l = 1, o = NaN: every merge weight
+    // turns NaN) and still arrives, so the in-launch merge runs and the tickets stay balanced for the next launch
+    if (a.nsplit == 1) {
+      for (int e = tid; e < R * HD; e += NTH) {
+        const int r = e / HD, d = e - r * HD;
+        const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+        a.out[th * HD + d] = NAN;
+        if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, NAN, a.prb);
+      }
+      return;
+    }
+    for (int e = tid; e < R * HD; e += NTH) {
+      const int r = e / HD, d = e - r * HD;
+      const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+      a.part_o[(th * a.nsplit + sp) * HD + d] = NAN;
+      if (d == 0) {
+        a.part_ml[(th * a.nsplit + sp) * 2] = INFINITY;
+        a.part_ml[(th * a.nsplit + sp) * 2 + 1] = 1.f;
+      }
+    }
+    if (a.cnt) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
     return;
   }
   const int pb = whole ? 0 : pb0;  // pg_s holds pages pb..

@@ -6,9 +6,17 @@
 #include "fo_common.h"
 #include <hip/hip_ext.h>
 
+#include <atomic>
+
+#include "fo_hip.h"
+
 static thread_local char g_err[1024] = {0};
+static std::atomic<long long> g_launches[FO_LAUNCH_KINDS];
 
 namespace fo {
+void count_launch(int kind) {
+  if (kind >= 0 && kind < FO_LAUNCH_KINDS) g_launches[kind].fetch_add(1, std::memory_order_relaxed);
+}
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -28,6 +36,15 @@ int check_launch(const char* what) {
 extern "C" {
 
 int fo_version(void) { return 1; }
+
+int fo_launch_counts(long long* out, int n) {
+  for (int i = 0; out && i < n && i < FO_LAUNCH_KINDS; ++i) out[i] = g_launches[i].load(std::memory_order_relaxed);
+  return FO_LAUNCH_KINDS;
+}
+int fo_launch_counts_reset(void) {
+  for (int i = 0; i < FO_LAUNCH_KINDS; ++i) g_launches[i].store(0, std::memory_order_relaxed);
+  return 0;
+}
 
 // Copies the last error message of this thread into buf (always NUL-terminated).
 int fo_last_error(char* buf, int len) {

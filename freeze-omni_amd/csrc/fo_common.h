@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fo_hip.h"
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef uint16_t bf16_t;  // raw bf16 storage
@@ -16,6 +18,10 @@ typedef uint16_t bf16_t;  // raw bf16 storage
 namespace fo {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// host-side launch counters per kernel family (include/fo_hip.h FoLaunchKind; fo_launch_counts): tests assert
+// which kernel family a shape was routed to.  Counted when the launch is issued (a captured graph counts once,
+// at capture).
+void count_launch(int kind);
 }  // namespace fo
 
 #define FO_REQUIRE(cond, ...)            \
@@ -39,10 +45,10 @@ int check_launch(const char* what);
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-// Packed fp32 activations for the <= 32-row GEMMs: element (m < 16 rbs, n) of an fp32 matrix as bf16 hi + lo (the
+// Packed fp32 activations for the <= 64-row GEMMs: element (m < 16 rbs, n) of an fp32 matrix as bf16 hi + lo (the
 // split a GEMM would do on load: hi = bf16(v), lo = bf16(v - hi)) at its MFMA A-fragment position: k-step n / 32,
-// lane 16 (n % 32 / 8) + m, element n % 8 of the lane's 8.  [K/32][64][8] bf16 per half.
-// With rbs row blocks of 16 (<= 16 rows: 1; <= 32: 2) the k-step holds rbs fragments: [K/32][rbs][64][8].
+// row block m / 16, lane 16 (n % 32 / 8) + m % 16, element n % 8 of the lane's 8.
+// With rbs = ceil(M / 16) row blocks (1..4) the k-step holds rbs fragments: [K/32][rbs][64][8] bf16 per half.
 __device__ __forceinline__ void xpack_store(uint16_t* hp, uint16_t* lp, int m, int n, float v, int rbs = 1) {
   const int c = n & 31;
   const size_t o = ((size_t)(((n >> 5) * rbs + (m >> 4)) * 64 + ((c >> 3) << 4) + (m & 15))) * 8 + (c & 7);

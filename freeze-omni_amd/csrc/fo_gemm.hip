@@ -955,12 +955,30 @@ void launch_mid(dim3 grid, const GemmArgs& a, hipStream_t s) {
 }
 
 thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
-thread_local const void* g_xph = nullptr;           // fo_gemm_set_xpack: the next launch's packed X
-thread_local const void* g_xpl = nullptr;
-thread_local void* g_ypkh = nullptr;                // fo_gemm_set_ypack: the next launch's packed yg output
-thread_local void* g_ypkl = nullptr;
-thread_local float* g_yp32 = nullptr;               // fo_gemm_set_ypack32 / _xpack32: fp32 fragment-order copies
-thread_local const float* g_xp32 = nullptr;
+// packed activations armed for the calling thread's next launch, with their extent (cols, allocated row blocks)
+struct PackArm {
+  const void* p0 = nullptr;
+  const void* p1 = nullptr;
+  int cols = 0, cap_rb = 0;
+};
+thread_local PackArm g_xpk;    // fo_gemm_set_xpack: the next launch's packed X (hi, lo)
+thread_local PackArm g_ypk;    // fo_gemm_set_ypack: the next launch's packed yg / Y output (hi, lo)
+thread_local PackArm g_yp32k;  // fo_gemm_set_ypack32 / _xpack32: fp32 fragment-order copies
+thread_local PackArm g_xp32k;
+inline int arm_pack(PackArm& g, const void* p0, const void* p1, bool two, int cols, int cap_rb, const char* what) {
+  g = PackArm{};
+  FO_REQUIRE(!two || (p0 == nullptr) == (p1 == nullptr), "%s: both halves or neither", what);
+  if (!p0) return 0;
+  FO_REQUIRE(cols > 0 && (cols & 31) == 0 && cap_rb >= 1 && cap_rb <= 4,
+             "%s: cols %d (a multiple of 32) and 1..4 row blocks (%d) required", what, cols, cap_rb);
+  g = PackArm{p0, p1, cols, cap_rb};
+  return 0;
+}
+// the launch's check of an armed pack against what it reads (cols = its K) or writes (cols = its N) at M rows
+#define FO_PACK_FITS(pk, want_cols, M, what)                                                                         \
+  FO_REQUIRE(!(pk).p0 || ((pk).cols == (want_cols) && (pk).cap_rb * 16 >= (M)),                                 \
+             "%s: packed buffer of %d columns x %d row blocks armed for a launch of %d columns x %d rows", what, \
+             (pk).cols, (pk).cap_rb, (want_cols), (M))
 
 // forced (waves, tiles per workgroup) of the M <= 16 kernels; 0 = automatic (sweeps only)
 thread_local int g_force_nw = 0, g_force_nt = 0;
@@ -1366,7 +1384,14 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
                      int* sgroups, const GemmArgs* rope, hipStream_t stream, const float* lnw = nullptr,
                      const float* lnb = nullptr, float lneps = 0.f, float* sout1 = nullptr,
                      const float* rstats1 = nullptr) {
+  // the packed buffers armed for this launch are consumed whatever happens below (one launch each)
+  const PackArm xpk = g_xpk, ypk = g_ypk, yp32k = g_yp32k, xp32k = g_xp32k;
+  g_xpk = g_ypk = g_yp32k = g_xp32k = PackArm{};
   FO_REQUIRE(M > 0 && N > 0 && K > 0, "fo_gemm: bad shape M=%d N=%d K=%d", M, N, K);
+  FO_PACK_FITS(xpk, K, M, "fo_gemm (packed X)");
+  FO_PACK_FITS(xp32k, K, M, "fo_gemm (fp32 packed X)");
+  FO_PACK_FITS(ypk, N, M, "fo_gemm (packed output)");
+  FO_PACK_FITS(yp32k, N, M, "fo_gemm (fp32 packed output)");
   FO_REQUIRE(!rstats || rgroups > 0, "fo_gemm: row statistics without a group count");
   FO_REQUIRE(!sout || (!swiglu && !out_bf16 && (!yg || gnext)), "fo_gemm: row statistics need fp32 non-SwiGLU output");
   FO_REQUIRE((K & 31) == 0, "fo_gemm: K=%d must be a multiple of 32", K);
@@ -1408,16 +1433,12 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.sout1 = sout1;
   a.rstats1 = rstats1;
   a.trc = g_trc;
-  a.xph = reinterpret_cast<const bf16x8*>(g_xph);
-  a.xpl = reinterpret_cast<const bf16x8*>(g_xpl);
-  a.ypkh = reinterpret_cast<bf16_t*>(g_ypkh);
-  a.ypkl = reinterpret_cast<bf16_t*>(g_ypkl);
-  a.yp32 = g_yp32;
-  a.xp32 = g_xp32;
-  g_xph = g_xpl = nullptr;   // one launch each
-  g_ypkh = g_ypkl = nullptr;
-  g_yp32 = nullptr;
-  g_xp32 = nullptr;
+  a.xph = reinterpret_cast<const bf16x8*>(xpk.p0);
+  a.xpl = reinterpret_cast<const bf16x8*>(xpk.p1);
+  a.ypkh = reinterpret_cast<bf16_t*>(const_cast<void*>(ypk.p0));
+  a.ypkl = reinterpret_cast<bf16_t*>(const_cast<void*>(ypk.p1));
+  a.yp32 = reinterpret_cast<float*>(const_cast<void*>(yp32k.p0));
+  a.xp32 = reinterpret_cast<const float*>(xp32k.p0);
   FO_REQUIRE(!a.xp32 || (lnw && M <= 64), "fo_gemm: the fp32 packed X is read by LayerNorm-on-load launches only");
   FO_REQUIRE(!a.yp32 || (M <= 64 && !swiglu && !rope), "fo_gemm: fp32 packed output needs <= 64 plain rows");
   a.prb = (M + 15) / 16;
@@ -1463,6 +1484,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (sgroups) *sgroups = units;
     if (sout) FO_REQUIRE(!swiglu && !rope, "fo_gemm: statistics with a paired epilogue");
     hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    fo::count_launch(FO_L_GEMM_XS);
+    if (a.xph) fo::count_launch(FO_L_GEMM_XP);
     return fo::check_launch("fo_gemm/xs");
   }
   // 17..64 rows on large weights (duplex ticks: 8 sessions x 4 framing-B tokens, the assistant prefix 8 x 5, prefixed
@@ -1496,6 +1519,10 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     int rc = fo::check_launch("fo_gemm/xsk");
     if (rc) return rc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, RBk * 16);
+    fo::count_launch(FO_L_GEMM_XSK);
+    fo::count_launch(FO_L_GEMM_REDUCE);
+    if (a.ypkh) fo::count_launch(FO_L_GEMM_YPACK);
+    if (a.yp32) fo::count_launch(FO_L_GEMM_YPACK32);
     return fo::check_launch("fo_gemm/xsk reduce");
   }
   // mid-size row counts on large weights (the Qwen2 prefills of a turn: assistant prefix, the first
@@ -1697,12 +1724,20 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       else launch_gemm<1, 4, 4, 4, false>(wstream, x_f32, grid, a, stream);
     }
   }
+  const bool pipe_k = RB == 1 && x_f32 && (launch_pipe || (g_launch_u != 4 && NT <= 2));
   g_launch_pipe = 0;
   g_launch_u = 4;
+  fo::count_launch(lnw ? FO_L_GEMM_LN : (mid ? FO_L_GEMM_MID : (pipe_k ? FO_L_GEMM_PIPE : FO_L_GEMM_OTHER)));
+  if (lnw && a.xp32) fo::count_launch(FO_L_GEMM_XP32);
+  if (a.xph && x_f32 && !lnw && !swiglu && !pipe_k) fo::count_launch(FO_L_GEMM_XP);
+  if (rope4) fo::count_launch(FO_L_GEMM_ROPE4);
+  if (a.ypkh) fo::count_launch(FO_L_GEMM_YPACK);
+  if (a.yp32) fo::count_launch(FO_L_GEMM_YPACK32);
   if (S > 1 && !merged) {
     int rc = fo::check_launch("fo_gemm/split");
     if (rc) return rc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, mt * RB * 16);
+    fo::count_launch(FO_L_GEMM_REDUCE);
   }
   return fo::check_launch("fo_gemm");
 }
@@ -1793,28 +1828,20 @@ int fo_gemm_set_trace(void* trace) {
   return 0;
 }
 
-int fo_gemm_set_xpack(const void* hi, const void* lo) {
-  FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_gemm_set_xpack: both halves or neither");
-  g_xph = hi;
-  g_xpl = lo;
-  return 0;
+int fo_gemm_set_xpack(const void* hi, const void* lo, int cols, int cap_rb) {
+  return arm_pack(g_xpk, hi, lo, true, cols, cap_rb, "fo_gemm_set_xpack");
 }
 
-int fo_gemm_set_ypack32(void* p) {
-  g_yp32 = reinterpret_cast<float*>(p);
-  return 0;
+int fo_gemm_set_ypack32(void* p, int cols, int cap_rb) {
+  return arm_pack(g_yp32k, p, nullptr, false, cols, cap_rb, "fo_gemm_set_ypack32");
 }
 
-int fo_gemm_set_xpack32(const void* p) {
-  g_xp32 = reinterpret_cast<const float*>(p);
-  return 0;
+int fo_gemm_set_xpack32(const void* p, int cols, int cap_rb) {
+  return arm_pack(g_xp32k, p, nullptr, false, cols, cap_rb, "fo_gemm_set_xpack32");
 }
 
-int fo_gemm_set_ypack(void* hi, void* lo) {
-  FO_REQUIRE((hi == nullptr) == (lo == nullptr), "fo_gemm_set_ypack: both halves or neither");
-  g_ypkh = hi;
-  g_ypkl = lo;
-  return 0;
+int fo_gemm_set_ypack(void* hi, void* lo, int cols, int cap_rb) {
+  return arm_pack(g_ypk, hi, lo, true, cols, cap_rb, "fo_gemm_set_ypack");
 }
 
 int fo_gemm_set_u(int u) {

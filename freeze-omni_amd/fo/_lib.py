@@ -62,11 +62,13 @@ _SIGS = {
     "fo_gemm_set_xs": (c_int, [c_int]),
     "fo_gemm_set_merge": (c_int, [c_int]),
     "fo_gemm_set_trace": (c_int, [c_vp]),
-    "fo_gemm_set_xpack": (c_int, [c_vp, c_vp]),
-    "fo_gemm_set_ypack": (c_int, [c_vp, c_vp]),
-    "fo_gemm_set_ypack32": (c_int, [c_vp]),
-    "fo_gemm_set_xpack32": (c_int, [c_vp]),
-    "fo_attention_set_opack": (c_int, [c_vp, c_vp]),
+    "fo_gemm_set_xpack": (c_int, [c_vp, c_vp, c_int, c_int]),
+    "fo_gemm_set_ypack": (c_int, [c_vp, c_vp, c_int, c_int]),
+    "fo_gemm_set_ypack32": (c_int, [c_vp, c_int, c_int]),
+    "fo_gemm_set_xpack32": (c_int, [c_vp, c_int, c_int]),
+    "fo_attention_set_opack": (c_int, [c_vp, c_vp, c_int, c_int]),
+    "fo_launch_counts": (c_int, [ctypes.POINTER(c_ll), c_int]),
+    "fo_launch_counts_reset": (c_int, []),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),

@@ -178,8 +178,9 @@ class PackedLinear:
         """x: fp32 or bf16 [M, >=Kp] (row stride x.stride(0)); returns out [M, N].
         norm: (RowStats, eps): x is the producer's yg (= residual * gamma) and rows are scaled by the
         RMSNorm rstd from the producer's statistics; stats_out: RowStats this GEMM fills (see RowStats).
-        xpack: XPack holding x (<= 16 rows) pre-split in fragment order (written by its producer), read instead of
-        splitting x; ypack: XPack this GEMM fills with stats_out's yg (<= 16 rows)."""
+        xpack: XPack holding x (<= 64 rows) pre-split in fragment order (written by its producer), read instead of
+        splitting x by the kernels that take packed X (include/fo_hip.h fo_gemm_set_xpack; the others read x);
+        ypack: XPack this GEMM fills with stats_out's yg -- or, without stats_out, its output (<= 64 rows)."""
         if norm is not None or stats_out is not None:
             return self._call_norm(x, out, act, residual, out_dtype, splitk, M, norm, stats_out, xpack, ypack)
         _check_dev(x)
@@ -290,7 +291,7 @@ class PackedLinear:
         return out
 
 
-# FO_XPACK=0 turns the packed <= 16-row activations off (A/B only)
+# FO_XPACK=0 turns the packed <= 64-row activations off (A/B only)
 XPACK = os.environ.get("FO_XPACK", "1") != "0"
 
 
@@ -305,7 +306,8 @@ class XPack:
         if K % 32 or not 1 <= rows <= 64:
             raise ValueError("XPack needs K % 32 == 0 and <= 64 rows")
         self.K, self.rows = K, rows
-        n = K * 16 * ((rows + 15) // 16)   # [K/32][row blocks][64][8]
+        self.rb = (rows + 15) // 16        # allocated row blocks (the extent the C-ABI setters pass along)
+        n = K * 16 * self.rb               # [K/32][row blocks][64][8]
         self.hi = torch.empty(n, dtype=BF16, device=device)
         self.lo = torch.empty(n, dtype=BF16, device=device)
 
@@ -319,36 +321,38 @@ class XPack32:
         if K % 32 or not 1 <= rows <= 64:
             raise ValueError("XPack32 needs K % 32 == 0 and <= 64 rows")
         self.K, self.rows = K, rows
-        self.buf = torch.empty(K * 16 * ((rows + 15) // 16), dtype=F32, device=device)
+        self.rb = (rows + 15) // 16
+        self.buf = torch.empty(K * 16 * self.rb, dtype=F32, device=device)
 
 
 class _packed:
     """Arms fo_gemm's packed-X input / packed-yg output for the one launch inside the block (thread-local in the
-    library, consumed by that launch); a launch that raises leaves nothing armed for the next one."""
+    library, consumed by that launch -- also when the launch refuses its arguments, e.g. a pack whose extent does not
+    fit); the disarm on an exception covers a failure between the setters and the launch."""
 
     def __init__(self, xpack, ypack, xpack32=None, ypack32=None):
         self.x, self.y, self.x32, self.y32 = xpack, ypack, xpack32, ypack32
 
     def __enter__(self):
         if self.x is not None:
-            _lib.call("fo_gemm_set_xpack", self.x.hi.data_ptr(), self.x.lo.data_ptr())
+            _lib.call("fo_gemm_set_xpack", self.x.hi.data_ptr(), self.x.lo.data_ptr(), self.x.K, self.x.rb)
         if self.y is not None:
-            _lib.call("fo_gemm_set_ypack", self.y.hi.data_ptr(), self.y.lo.data_ptr())
+            _lib.call("fo_gemm_set_ypack", self.y.hi.data_ptr(), self.y.lo.data_ptr(), self.y.K, self.y.rb)
         if self.x32 is not None:
-            _lib.call("fo_gemm_set_xpack32", self.x32.buf.data_ptr())
+            _lib.call("fo_gemm_set_xpack32", self.x32.buf.data_ptr(), self.x32.K, self.x32.rb)
         if self.y32 is not None:
-            _lib.call("fo_gemm_set_ypack32", self.y32.buf.data_ptr())
+            _lib.call("fo_gemm_set_ypack32", self.y32.buf.data_ptr(), self.y32.K, self.y32.rb)
 
     def __exit__(self, et, ev, tb):
         if et is not None:
             if self.x is not None:
-                _lib.call("fo_gemm_set_xpack", None, None)
+                _lib.call("fo_gemm_set_xpack", None, None, 0, 0)
             if self.y is not None:
-                _lib.call("fo_gemm_set_ypack", None, None)
+                _lib.call("fo_gemm_set_ypack", None, None, 0, 0)
             if self.x32 is not None:
-                _lib.call("fo_gemm_set_xpack32", None)
+                _lib.call("fo_gemm_set_xpack32", None, 0, 0)
             if self.y32 is not None:
-                _lib.call("fo_gemm_set_ypack32", None)
+                _lib.call("fo_gemm_set_ypack32", None, 0, 0)
         return False
 
 
@@ -385,6 +389,25 @@ def h2d(a, device, dtype=None):
     p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     p.copy_(t)
     return p.to(device, non_blocking=True)
+
+
+# ---------------------------------------------------------------- launch counters (include/fo_hip.h FoLaunchKind)
+LAUNCH_KINDS = ("gemm_xs", "gemm_xsk", "gemm_xp", "gemm_reduce", "gemm_ln", "gemm_xp32", "gemm_ypack", "gemm_ypack32",
+                "gemm_mid", "gemm_rope4", "gemm_pipe", "gemm_other", "attn_mfma", "attn_decode", "attn_opack", "relpos")
+
+
+def launch_counts():
+    """{kind: launches issued since the last reset} (host-side counters; a captured graph counts at capture)."""
+    import ctypes
+    lib = _lib.load()
+    n = lib.fo_launch_counts(None, 0)
+    buf = (ctypes.c_longlong * n)()
+    lib.fo_launch_counts(buf, n)
+    return {k: int(buf[i]) for i, k in enumerate(LAUNCH_KINDS)}
+
+
+def launch_counts_reset():
+    _lib.call("fo_launch_counts_reset")
 
 
 # ---------------------------------------------------------------- kernel wrappers
@@ -511,7 +534,7 @@ def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc,
     if tickets is not None and tickets.numel() < n_items * KVH:
         raise ValueError("attention tickets buffer smaller than n_items * KVH")
     if opack is not None:
-        _lib.call("fo_attention_set_opack", opack.hi.data_ptr(), opack.lo.data_ptr())
+        _lib.call("fo_attention_set_opack", opack.hi.data_ptr(), opack.lo.data_ptr(), opack.K, opack.rb)
     try:
         _lib.call("fo_attention", q.data_ptr(), T, ptr(items), n_items, max_rows, tok_nvis.data_ptr(),
                   block_table.data_ptr(), block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, KVH, hd,
@@ -519,7 +542,7 @@ def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc,
                   stream(q.device))
     except Exception:
         if opack is not None:   # the launch did not consume it: never leave it for the next one
-            _lib.call("fo_attention_set_opack", None, None)
+            _lib.call("fo_attention_set_opack", None, None, 0, 0)
         raise
     return out
 
@@ -532,12 +555,12 @@ def enc_kv_write(k, v, B, T, d, start, length, ring, cap, kr, vr):
 def relpos_attention_fused(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out,
                            opack=None):
     if opack is not None:
-        _lib.call("fo_attention_set_opack", opack.hi.data_ptr(), opack.lo.data_ptr())
+        _lib.call("fo_attention_set_opack", opack.hi.data_ptr(), opack.lo.data_ptr(), opack.K, opack.rb)
     try:
         _relpos_fused_call(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out)
     except Exception:
         if opack is not None:   # the launch did not consume it: never leave it for the next one
-            _lib.call("fo_attention_set_opack", None, None)
+            _lib.call("fo_attention_set_opack", None, None, 0, 0)
         raise
 
 

@@ -101,24 +101,55 @@ int fo_gemm_set_merge(int on);
  * (100 MHz) to trace[wg * 24 + slot]: 0 start, 1 + w the end of wave w's weight stream, 17 the K reduce done,
  * 18 the epilogue issued.  nullptr turns it off (the default).  Returns 0. */
 int fo_gemm_set_trace(void* trace);
-/* the calling thread's NEXT fo_gemm launch takes its <= 32 fp32 X rows also as bf16 hi / lo halves packed in MFMA
- * A-fragment order by their producer (hi, lo: [K/32][ceil(M/16)][64][8] bf16, lane l = row 16 b + (l & 15) of row
- * block b, columns 8 (l >> 4) .. + 8 of each 32-column k-step; the <= 2-row-block grid kernels read them instead of
- * splitting X, bit-identical).  Both or neither.  Returns 0. */
-int fo_gemm_set_xpack(const void* hi, const void* lo);
-/* the calling thread's NEXT fo_gemm launch (<= 32 rows, plain epilogue) also writes its next-norm input yg
- * (stats_out) -- or, without one, its output Y -- packed as fo_gemm_set_xpack reads it (hi, lo: [N/32][ceil(M/16)][64][8]
- * bf16).  Both or neither. */
-int fo_gemm_set_ypack(void* hi, void* lo);
-/* fp32 form of the same fragment order ([N/32][ceil(M/16)][64][8] floats, the exact values): the next fo_gemm* launch
- * (<= 64 rows, plain epilogue) also writes its output Y there (ypack32); the next fo_gemm_ln launch reads its X from
- * there instead of the row-major rows (xpack32; bit-identical).  NULL disarms. */
-int fo_gemm_set_ypack32(void* p);
-int fo_gemm_set_xpack32(const void* p);
-/* the calling thread's NEXT fo_attention (<= 16 tokens, not with the separate combine launch) or
- * fo_relpos_attention_fused (<= 32 rows) launch also writes its output packed as fo_gemm_set_xpack reads it (hi, lo:
- * [cols/32][ceil(rows/16)][64][8] bf16).  Both or neither. */
-int fo_attention_set_opack(void* hi, void* lo);
+/* Packed activations (fo/ops.py XPack / XPack32).  A packed buffer holds an fp32 activation of <= 64 rows in MFMA
+ * A-fragment order: k-step k (32 columns), row block b (16 rows), lane l = row 16 b + (l & 15), columns 32 k +
+ * 8 (l >> 4) .. + 8, i.e. [cols/32][rb][64][8] elements, where rb is the row-block count the launch uses
+ * (ceil(M/16)).  Each setter arms the calling thread's NEXT matching launch only and carries the buffer's extent:
+ * cols (its K, a multiple of 32) and cap_rb (the row blocks it was allocated for, 1..4).  The consuming launch
+ * returns -2 (and consumes the arming) when cols differs from the K it reads / the N it writes, or when
+ * cap_rb < ceil(M/16) -- a pack built for another layer or for fewer rows is refused, never read or written out of
+ * bounds.  NULL pointers disarm (cols / cap_rb ignored).
+ * fo_gemm_set_xpack: X given as bf16 hi / lo halves (the split a GEMM does on load, bit-identical); read by the
+ *   one-row-tile and 17..64-row grid kernels (k_gemm_xp) and the <= 16-row gate/up stream (k_gemm_xs); the
+ *   software-pipelined <= 8-row kernels and the 17..64-row split-K stream (k_gemm_xsk) read row-major X and ignore it.
+ * fo_gemm_set_ypack: the launch (plain epilogue) also writes its next-norm input yg (stats_out) -- or, without one,
+ *   its output Y -- into hi / lo as fo_gemm_set_xpack reads it.
+ * fo_gemm_set_ypack32 / fo_gemm_set_xpack32: the fp32 form of the same order (exact values): the next launch writes
+ *   its output Y there / the next fo_gemm_ln launch reads its X from there (LayerNorm-on-load consumers only). */
+int fo_gemm_set_xpack(const void* hi, const void* lo, int cols, int cap_rb);
+int fo_gemm_set_ypack(void* hi, void* lo, int cols, int cap_rb);
+int fo_gemm_set_ypack32(void* p, int cols, int cap_rb);
+int fo_gemm_set_xpack32(const void* p, int cols, int cap_rb);
+/* the calling thread's NEXT fo_attention (<= 64 tokens, not with the separate combine launch; cols = H * hd) or
+ * fo_relpos_attention_fused (<= 64 rows; cols = h * dk) launch also writes its output packed as fo_gemm_set_xpack
+ * reads it, with the same extent check.  A launch whose host contract is broken (keys beyond the block table)
+ * writes NaN to both the fp32 and the packed output. */
+int fo_attention_set_opack(void* hi, void* lo, int cols, int cap_rb);
+/* Launch counters per kernel family (tests assert which kernels a shape was routed to).  Counted on the host when
+ * a launch is issued; a launch captured into a graph counts once, at capture.  fo_launch_counts copies
+ * min(n, FO_LAUNCH_KINDS) counters into out (n <= 0: none) and returns FO_LAUNCH_KINDS; fo_launch_counts_reset
+ * zeroes them (process-wide). */
+enum FoLaunchKind {
+  FO_L_GEMM_XS = 0,     /* k_gemm_xs: <= 16-row X-stationary gate/up stream */
+  FO_L_GEMM_XSK = 1,    /* k_gemm_xsk: 17..64-row X-stationary split-K stream */
+  FO_L_GEMM_XP = 2,     /* any GEMM launch that read packed X (fo_gemm_set_xpack) */
+  FO_L_GEMM_REDUCE = 3, /* k_gemm_reduce */
+  FO_L_GEMM_LN = 4,     /* k_gemm_ln: LayerNorm on load */
+  FO_L_GEMM_XP32 = 5,   /* a k_gemm_ln launch that read fp32 packed X */
+  FO_L_GEMM_YPACK = 6,  /* a GEMM launch that wrote packed output (ypack) */
+  FO_L_GEMM_YPACK32 = 7,/* a GEMM launch that wrote fp32 packed output */
+  FO_L_GEMM_MID = 8,    /* the 17..64-row one-row-tile grid kernels */
+  FO_L_GEMM_ROPE4 = 9,  /* the 17..64-row RoPE q|k|v in 4-tile column groups (epilogue in the reduce) */
+  FO_L_GEMM_PIPE = 10,  /* k_gemm_wpipe */
+  FO_L_GEMM_OTHER = 11, /* every other GEMM launch */
+  FO_L_ATTN_MFMA = 12,  /* k_attn_mfma */
+  FO_L_ATTN_DECODE = 13,/* k_attn_decode */
+  FO_L_ATTN_OPACK = 14, /* an attention launch that wrote packed output */
+  FO_L_RELPOS = 15,     /* k_relpos_fused */
+  FO_LAUNCH_KINDS = 24
+};
+int fo_launch_counts(long long* out, int n);
+int fo_launch_counts_reset(void);
 /* Software-pipelined one-row-tile fp32-X weight-stream GEMMs (M <= 16, >= 32 MB of weights: the next
  * k-group's weights + X in flight during this group's MFMAs).  3 (default): the measured policy; 0: plain
  * loops; 1 / 2: every such GEMM pipelined with 4 / 2 k-steps per group (sweeps).  Unset, the

@@ -39,7 +39,7 @@ for name, N, K, M, res in [("qwen_o", 3584, 3584, 16, True), ("qwen_qkv_plain", 
 
         def run(i):
             if mode == "packed":
-                lib.fo_gemm_set_xpack(hi.data_ptr(), lo.data_ptr())
+                lib.fo_gemm_set_xpack(hi.data_ptr(), lo.data_ptr(), K, (M + 15) // 16)
             lins[i](x, out=ys[i], residual=res, M=M)
         us = graph_time(lambda: run(next(it) % 6), 48)
         ys[0].copy_(y0)

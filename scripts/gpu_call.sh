@@ -15,6 +15,7 @@
 #   profdup    rocprofv3 kernel trace + stats of a 20 s duplex run       -> <tag>_profdup/, <tag>_profdup_table.txt
 #   profstage  rocprofv3 kernel trace of scripts/llm_stage_time.py (LLM / encoder stage replays) -> <tag>_profstage_table.txt
 #   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
+#   ddp1       bench.py as one torch.distributed.run rank (world 1: RCCL init, broadcast, checksum) -> <tag>_ddp1.json
 #   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
 #   ab         ENV_A / ENV_B (e.g. 'FO_X=0') alternated twice on the quick bench -> <tag>_ab.txt
 #   sweep      SWEEP='A=1|B=2|' settings ('|'-separated, empty = default), two rounds on the quick bench -> <tag>_sweep.txt
@@ -64,6 +65,9 @@ for S in "$@"; do
             [ $rc -eq 0 ] && line ${O}_duplex.log ;;
     rehearsal) FO_DIST_REHEARSAL=1 timeout -k 10 600 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu-baseline \
              --no-single-user --out ${O}_rehearsal_n2.json > ${O}_rehearsal_n2.log 2>&1; rc=$? ;;
+    ddp1)  timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 \
+             --master-port 29517 bench.py --gpus 1 --steps 1 --warmup 1 --no-cpu-baseline --no-single-user \
+             --out ${O}_ddp1.json > ${O}_ddp1.log 2>&1; rc=$?; [ $rc -eq 0 ] && line ${O}_ddp1.log ;;
     n2guard) timeout -k 10 120 python -u bench.py --gpus 2 --steps 1 > ${O}_n2guard.log 2>&1; rc=$?
              if [ $rc -eq 2 ] && grep -q refusing ${O}_n2guard.log; then echo "n2guard ok: $(tail -1 ${O}_n2guard.log)"; rc=0
              else echo "n2guard: expected a refusal, got rc $rc"; tail -5 ${O}_n2guard.log; [ $rc -eq 0 ] && rc=1; fi ;;

@@ -730,6 +730,89 @@ def gold_real_qwen2(seed=7, n_layers=2, n_sess=8):
           f"fixture {os.path.getsize(os.path.join(HERE, 'real_qwen2_t2.npz')) / 1e6:.2f} MB")
 
 
+# rows per session of the 17..64-row steps after the 128-row prefill (batched over the 8 sessions): M = 32 (4 framing-B
+# tokens each: a duplex tick), 40 (the 5-token assistant prefix), 44 (ragged: ticks with and without a 5-token chat
+# prefix -> the attention item table), 48, 64 (four row blocks)
+MID_ROWS = [[4] * 8, [5] * 8, [4, 9, 4, 4, 6, 4, 9, 4], [6] * 8, [8] * 8]
+
+
+def mid_embeds(step, b, rows, D=3584):
+    """fp16-valued input embeds of session b at mid step `step` (regenerated by tests/test_real_qwen2_mid_gpu.py)."""
+    return (np.random.default_rng(4321 + 100 * step + b).standard_normal((rows, D)) * 0.5).astype(np.float16)
+
+
+def gold_real_qwen2_mid(seed=7, n_layers=2, n_sess=8):
+    """The 17..64-row Qwen2-7B steps at REAL geometry through the reference's own AudioLLM._llm_forward_core /
+    _prediction_head_forward (models/audioLLM.py:479-493), the shapes every duplex tick and assistant prefix run
+    (bin/dialog_state_pred.py:777-844, models/audioLLM.py:350-429): the same 2-layer counter-hash Qwen2 and the same
+    eight sessions as gold_real_qwen2 (its 9 + 2b-row prefill, real_qwen2_t2.npz emb0), then the MID_ROWS steps, each
+    session its own DynamicCache.  Stored (weights and the mid-step inputs regenerate): per step the hidden rows at
+    1024 fixed columns, every row's float64 sum / sum of squares over all 3584 columns, each session's full last row,
+    the state probs, and the lm_head logits of each session's last row reduced as in gold_real_qwen2."""
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    sys.argv = ["golden"]
+    from models.audioLLM import AudioLLM
+    cfg = C.get("real")
+    assert cfg["seed"] == seed
+    lc = dict(cfg["llm"], num_hidden_layers=n_layers)
+    m = Qwen2ForCausalLM(Qwen2Config(**lc, torch_dtype="float32"))
+    for k, v in m.state_dict().items():
+        v.copy_(torch.from_numpy(synth_param(seed, k, tuple(v.shape), cfg["overrides"])))
+    m.eval()
+    D, V = lc["hidden_size"], lc["vocab_size"]
+    head = torch.nn.Linear(D, 4)
+    init_module(head, seed, "predictor_head.", cfg["overrides"])
+    obj = types.SimpleNamespace(llm_decoder=m, predictor_head=head)
+    base = np.load(os.path.join(HERE, "real_qwen2_t2.npz"))
+    rows0 = base["rows0"].tolist()
+    emb0 = base["emb0"]
+    cols = np.sort(np.random.default_rng(77).choice(D, 1024, replace=False))
+    fixed_idx = base["fixed_idx"]
+    out = {"cols": cols.astype(np.int64), "n_steps": np.array(len(MID_ROWS))}
+    insum = 0.0
+    for s, rows in enumerate(MID_ROWS):
+        out[f"rows{s}"] = np.array(rows, np.int64)
+    acc = {k: [[] for _ in MID_ROWS] for k in ("hcols", "hsum", "hsq", "hlast", "probs", "argmax", "margin", "top_ids",
+                                               "top_vals", "lse", "fixed")}
+    off = np.cumsum([0] + rows0)
+    for b in range(n_sess):
+        e = torch.from_numpy(emb0[off[b]:off[b + 1]].astype(np.float32)).unsqueeze(0)
+        mask = torch.full([1, e.shape[1]], True)
+        h, pkv = AudioLLM._llm_forward_core(obj, {"inputs_embeds": e.half(), "attention_mask": mask, "past_key_values": None})
+        assert np.abs(h[0, -1].numpy() - base["hid0"][b]).max() < 1e-4   # the same prefill as real_qwen2_t2.npz
+        for s, rows in enumerate(MID_ROWS):
+            x = mid_embeds(s, b, rows[b], D)
+            insum += float(x.astype(np.float64).sum())
+            past = pkv.get_seq_length()
+            mask = torch.full([1, past + rows[b]], True)
+            h, pkv = AudioLLM._llm_forward_core(obj, {"inputs_embeds": torch.from_numpy(x.astype(np.float32)).unsqueeze(0).half(),
+                                                      "attention_mask": mask, "past_key_values": pkv})
+            hv = h[0].numpy().astype(np.float32)
+            acc["hcols"][s].append(hv[:, cols])
+            acc["hsum"][s].append(hv.astype(np.float64).sum(1))
+            acc["hsq"][s].append((hv.astype(np.float64) ** 2).sum(1))
+            acc["hlast"][s].append(hv[-1])
+            acc["probs"][s].append(AudioLLM._prediction_head_forward(obj, h).numpy())
+            lg = m.lm_head(h[:, -1:])[0, 0]
+            v, i = torch.topk(lg, 32)
+            acc["argmax"][s].append(int(i[0]))
+            acc["margin"][s].append(float(v[0] - v[1]))
+            acc["top_ids"][s].append(i.numpy().astype(np.int64))
+            acc["top_vals"][s].append(v.detach().numpy().astype(np.float32))
+            acc["lse"][s].append(float(torch.logsumexp(lg.double(), 0)))
+            acc["fixed"][s].append(lg.detach().numpy()[fixed_idx].astype(np.float32))
+        print(f"real qwen2 mid session {b}: kv {pkv.get_seq_length()} margins {[round(x[-1], 4) for x in acc['margin']]}",
+              flush=True)
+    for k, per in acc.items():
+        for s in range(len(MID_ROWS)):
+            v = per[s]
+            out[f"{k}{s}"] = np.concatenate(v) if k in ("hcols", "hsum", "hsq") else np.array(v)
+    out["input_sum"] = np.array(insum)
+    np.savez_compressed(os.path.join(HERE, "real_qwen2_mid_t2.npz"), **out)
+    print(f"real qwen2 mid: fixture {os.path.getsize(os.path.join(HERE, 'real_qwen2_mid_t2.npz')) / 1e6:.2f} MB, "
+          f"input sum {insum:.6f}")
+
+
 ADAPTER_VARIANTS = [  # CNNSubsampling(enc_out_dim, llm_embed_dim, kernel_size, activation_func, norm)
     {"enc_out_dim": 16, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "relu", "norm": "batch"},
     {"enc_out_dim": 32, "llm_embed_dim": 128, "kernel_size": 5, "activation_func": "gelu", "norm": "layer"},
@@ -978,6 +1061,7 @@ def main():
     gold_llm_text(cfg)
     gold_real_t2()
     gold_real_qwen2()
+    gold_real_qwen2_mid()
     gold_adapter_variants(cfg["seed"])
     gold_codec_gst(cfg)
     with open(os.path.join(HERE, "param_shapes_tiny.json"), "w") as f:
@@ -1011,5 +1095,8 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["real_qwen2"]:
         install_shims()
         gold_real_qwen2()
+    elif sys.argv[1:] == ["real_qwen2_mid"]:
+        install_shims()
+        gold_real_qwen2_mid()
     else:
         main()

@@ -174,3 +174,20 @@ def test_server_transport_on_device(dev, pipe):
         if abs(p1 - 0.5) > 1e-3:
             assert g == w
     assert sum(m["event"] == "dialog_ss" for m in c.events) == got.count("dialog_ss")
+
+
+def test_duplex_encoder_graph_and_two_streams_match_eager(pipe):
+    """The duplex tick's steady-state encoder + adapter stage replays a captured EncoderGraph, the second identity's
+    on its own stream ('enc2'); with graphs off the same tick runs the eager encoder / adapter launches.  Both must
+    give the same state probabilities bit for bit and the same KV lengths / pe indices (same kernels, same order,
+    each stream with its own scratch)."""
+    eng = pipe.model.engine
+    assert eng.use_graphs
+    with_graphs = _run(pipe, True)
+    eng.use_graphs = False
+    try:
+        eager = _run(pipe, True)
+    finally:
+        eng.use_graphs = True
+    assert with_graphs == eager
+    assert any(x[0] == "system" for s, _, _ in with_graphs for x in s)   # both parties took part

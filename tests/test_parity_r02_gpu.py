@@ -223,6 +223,65 @@ def test_real_geometry_encoder_adapter_match_reference(dev):
             close(emb, ref, rtol=2e-3, atol=2e-3 * float(np.abs(ref).max()))
 
 
+def test_real_geometry_batched_framing_b_encoder_matches_reference(dev):
+    """The duplex tick's encoder shape at real geometry: 8 copies of real_encoder_t2's framing-B session in ONE batch
+    (8 x 7 = 56 rows) for its 8 chunks across the RelPE wrap -- the LayerNorm-on-load q|k|v / FFN-up GEMMs at four row
+    blocks (k_gemm_ln<*, 4, 8, *>) reading the fp32 fragment-order residual stream (XPack32), the packed out / FFN-down
+    inputs, the subsampling output linear (19,456 x 1024) on the split-K X-stationary stream (k_gemm_xsk) -- every
+    session's rows against the reference's per-session output (launch counters assert those kernels ran).  Then the
+    same 8-session stage as the captured EncoderGraph the duplex tick replays, on 8 fresh sessions: bit-identical to
+    the eager batch (same kernels, same order)."""
+    from types import SimpleNamespace
+
+    from fo import ops
+    from fo.engine import EncoderGraph
+    from fo.speech import AdapterEngine, SpeechEncoderEngine
+    g = load("real_encoder_t2.npz")
+    src = _t2_source(dev, {**encoder_shapes(T2, "user"), **adapter_shapes(T2, "user")})
+    enc = SpeechEncoderEngine(src, T2, "user", dev, max_sessions=16)
+    ada = AdapterEngine(src, T2, "user", dev, max_sessions=16)
+    B = 8
+    feats = g["B_feats"]
+    ecs, acs, pes = [enc.new_cache() for _ in range(B)], [ada.new_cache() for _ in range(B)], [int(g["B_pe0"])] * B
+    eager = []
+    for i in range(feats.shape[0]):
+        f = torch.from_numpy(np.repeat(feats[i][None], B, 0)).to(dev).contiguous()
+        ops.launch_counts_reset()
+        out, T, pes = enc.infer(f, ecs, pes)
+        emb, To = ada(out, T, acs)
+        torch.cuda.synchronize()
+        c = ops.launch_counts()
+        assert T == 7 and To == 4 and out.shape[0] == B * T
+        assert pes == [int(g["B_pe"][i])] * B
+        nb = len(enc.layers)
+        assert c["gemm_ln"] == 2 * nb - 1 and c["gemm_xp32"] == 2 * nb - 1, c   # block 0's q|k|v takes the LN launch
+        assert c["gemm_xsk"] >= 1 and c["relpos"] == nb and c["attn_opack"] == nb, c
+        ref_e, ref_a = g["B_enc"][i], g["B_ada"][i]
+        for b in range(B):
+            close(out[b * T:(b + 1) * T], ref_e, rtol=2e-3, atol=2e-3 * float(np.abs(ref_e).max()))
+            close(emb[b * To:(b + 1) * To], ref_a, rtol=2e-3, atol=2e-3 * float(np.abs(ref_a).max()))
+        eager.append((out.clone(), emb.clone()))
+    # the captured stage (engine EncoderGraph) on fresh sessions: the same values bit for bit
+    eng = SimpleNamespace(device=dev, enc={"user": enc}, ada={"user": ada})
+    st = ops.engine_stream(dev)
+    with torch.cuda.stream(st):
+        eg = EncoderGraph(eng, "user", B, feats.shape[1], st)
+        try:
+            items = [{"enc_cache": enc.new_cache(), "ada_cache": ada.new_cache(), "pe_index": int(g["B_pe0"])}
+                     for _ in range(B)]
+            for i in range(feats.shape[0]):
+                for it in items:
+                    it["feats"] = torch.from_numpy(feats[i]).to(dev)
+                emb, To, new_pe = eg.run(items)
+                st.synchronize()
+                for it, p in zip(items, new_pe):
+                    it["pe_index"] = p
+                assert torch.equal(emb[:B * To], eager[i][1]), f"EncoderGraph chunk {i} differs from the eager batch"
+                assert torch.equal(eg.eb["x"][:B * 7], eager[i][0]), f"EncoderGraph encoder rows, chunk {i}"
+        finally:
+            eg.destroy()
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_real_geometry_tts_ids_match_reference(dev, graph):
     """The AR speech decoder at 896 / 14 heads / 4864, 4 layers + pre_nn + prefix layers: 48 greedy

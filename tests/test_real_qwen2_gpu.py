@@ -142,3 +142,78 @@ def test_post_decode_probs_at_full_vocabulary_match_reference(dev, gold):
         np.testing.assert_allclose(got, want, atol=1e-6, rtol=1e-4, err_msg=f"setting {(T, k, p)}")
         drawn = ids.cpu().numpy()
         assert all(want[b, drawn[b]] > 0 for b in range(B)), (si, drawn)
+
+
+# ------------------------------------------------------------------ 17..64-row steps (duplex ticks, assistant prefix)
+def _mid_embeds(step, b, rows, D=3584):
+    """tests/golden/make_golden.py mid_embeds: the fp16-valued inputs of the mid steps (regenerated, checksummed)."""
+    return (np.random.default_rng(4321 + 100 * step + b).standard_normal((rows, D)) * 0.5).astype(np.float16)
+
+
+def test_qwen2_real_geometry_17_to_64_row_steps_match_reference(dev, llm, gold):
+    """real_qwen2_mid_t2.npz (make_golden.py real_qwen2_mid: the reference's _llm_forward_core /
+    _prediction_head_forward on the same 2-layer counter-hash Qwen2, each session its own DynamicCache): after the
+    128-row prefill, steps of 4, 5, ragged 4..9, 6 and 8 rows per session -- M = 32, 40, 44, 48, 64 batched, the
+    shapes of every duplex tick and assistant prefix -- on the DEFAULT policy: the X-stationary split-K gate/up and
+    down (k_gemm_xsk + k_gemm_reduce) at 2, 3 and 4 row blocks, the mid-row RoPE q|k|v in 4-tile groups, the packed
+    q|k|v / o inputs (k_gemm_xp) written by the reduce, the statistics epilogue and the attention.  The launch
+    counters assert each family ran on every step, so a policy change cannot route around what this test pins.
+    Tolerances as the other real-geometry steps: hidden 2e-3 abs (1024 fixed columns of every row, each session's
+    whole last row, and each row's sum / sum of squares over all 3584 columns at 2e-3 x sqrt(3584) / relative
+    1e-4), state probs 5e-4, logits 1e-3 abs + 1e-3 rel; greedy ids equal where the reference's top-2 margin
+    exceeds 2e-3 (otherwise within its top 2)."""
+    from fo import _lib, ops
+    mid = np.load(os.path.join(G, "real_qwen2_mid_t2.npz"))
+    lib = _lib.load()
+    assert lib.fo_gemm_set_pipe(3) >= -1
+    B, D = 8, llm.D
+    cols = mid["cols"]
+    rows0 = gold["rows0"].tolist()
+    seqs = [llm.new_seq() for _ in range(B)]
+    insum = 0.0
+    try:
+        x = torch.from_numpy(gold["emb0"].astype(np.float32)).to(dev)
+        h, bm = llm.forward(x, [(q, r) for q, r in zip(seqs, rows0)])
+        _close(h[bm.last_rows_host], gold["hid0"], 2e-3, 0, "prefill last rows")
+        for s in range(int(mid["n_steps"])):
+            rows = mid[f"rows{s}"].tolist()
+            M = sum(rows)
+            xs = [_mid_embeds(s, b, rows[b]) for b in range(B)]
+            insum += sum(float(v.astype(np.float64).sum()) for v in xs)
+            x = torch.from_numpy(np.concatenate(xs).astype(np.float32)).to(dev)
+            ops.launch_counts_reset()
+            h, bm = llm.forward(x, [(q, r) for q, r in zip(seqs, rows)])
+            torch.cuda.synchronize()
+            c = ops.launch_counts()
+            nl = len(llm.stack.layers)
+            what = f"step {s} (M = {M})"
+            assert c["gemm_xsk"] == 2 * nl, (what, c)          # gate/up + down per layer on the split-K stream
+            assert c["gemm_rope4"] == nl, (what, c)            # q|k|v in 4-tile groups, epilogue in the reduce
+            assert c["gemm_xp"] >= 2 * nl - 1, (what, c)       # o of every layer + q|k|v of layers > 0 read packed X
+            assert c["attn_mfma"] == nl and c["attn_opack"] == nl, (what, c)
+            assert c["gemm_ypack"] >= 2 * nl - 1, (what, c)    # o / down producers pack the next input
+            hv = h[:M].float().cpu().numpy()
+            _close(hv[:, cols], mid[f"hcols{s}"], 2e-3, 0, f"{what} hidden at fixed columns")
+            _close(hv[bm.last_rows_host], mid[f"hlast{s}"], 2e-3, 0, f"{what} last rows")
+            h64 = hv.astype(np.float64)
+            np.testing.assert_allclose(h64.sum(1), mid[f"hsum{s}"], atol=2e-3 * 3584 ** 0.5, err_msg=f"{what} row sums")
+            np.testing.assert_allclose((h64 ** 2).sum(1), mid[f"hsq{s}"], rtol=1e-4, err_msg=f"{what} row sumsq")
+            p = llm.state_probs(h, bm.last_rows_host).cpu().numpy()
+            _close(p, mid[f"probs{s}"], 5e-4, 0, f"{what} state probs")
+            lg = llm.logits(h, bm.last_rows_host).float().cpu().numpy()
+            for b in range(B):
+                row = lg[b]
+                top = mid[f"top_ids{s}"][b]
+                if mid[f"margin{s}"][b] > 2e-3:
+                    assert int(row.argmax()) == int(mid[f"argmax{s}"][b]), (what, b)
+                else:
+                    assert int(row.argmax()) in top[:2].tolist(), (what, b)
+                _close(row[top], mid[f"top_vals{s}"][b], 1e-3, 1e-3, f"{what} top-32 b{b}")
+                _close(row[gold["fixed_idx"]], mid[f"fixed{s}"][b], 1e-3, 1e-3, f"{what} fixed-index b{b}")
+                lse = float(np.logaddexp.reduce(row.astype(np.float64)))
+                assert abs(lse - float(mid[f"lse{s}"][b])) < 1e-3, (what, b, lse)
+        assert abs(insum - float(mid["input_sum"])) < 1e-6 * max(1.0, abs(insum)), (insum, float(mid["input_sum"]))
+    finally:
+        for q in seqs:
+            q.free()
+    assert llm.pool.pages_in_use() == 0

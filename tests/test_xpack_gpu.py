@@ -112,31 +112,94 @@ def test_packed_x_gemm_is_bit_identical(dev, M, N, K, rope):
         assert torch.equal(u, v)
 
 
-@pytest.mark.parametrize("H,KVH,hd,tokens", [(28, 4, 128, 2), (14, 14, 64, 1)])
-def test_attention_writes_the_packed_split(dev, H, KVH, hd, tokens):
+def _check_packed_rb(xp, y, M):
+    """xp (an XPack) holds the bf16 hi / lo split of y's first M rows in the ceil(M/16)-row-block fragment order."""
+    K = y.shape[1]
+    hi, lo, rb = _pack_rb(y[:M])
+    view = lambda t: t[:K * 16 * rb].view(K // 32, rb, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(rb * 16, K)[:M]  # noqa
+    assert torch.equal(view(xp.hi).view(torch.int16), view(hi).view(torch.int16))
+    assert torch.equal(view(xp.lo).view(torch.int16), view(lo).view(torch.int16))
+
+
+CTX = [3, 40, 150, 300, 700, 1, 64, 65, 129, 9, 17, 33, 250, 5, 90, 400]
+
+
+@pytest.mark.parametrize("H,KVH,hd,tokens,nseq", [(28, 4, 128, 2, 8), (14, 14, 64, 1, 16),
+                                                  # 17..64 tokens (duplex ticks, prefills): 2..4 row blocks
+                                                  (28, 4, 128, 4, 8), (28, 4, 128, 3, 16), (28, 4, 128, 4, 16),
+                                                  (14, 14, 64, 1, 48)])
+def test_attention_writes_the_packed_split(dev, H, KVH, hd, tokens, nseq):
     """fo_attention's packed output (multi-row kernel with the in-launch split merge; the decode kernel) equals
-    the split of its fp32 output."""
-    g = torch.Generator().manual_seed(H + hd)
-    pool = KVPool(1, KVH, hd, 256, 16, dev)
+    the split of its fp32 output, at 1..4 row blocks (the token row index th / H against the packed layout)."""
+    g = torch.Generator().manual_seed(H + hd + tokens * nseq)
+    pool = KVPool(1, KVH, hd, 1024, 16, dev)
     pool.k.copy_(torch.randn(pool.k.shape, generator=g))
     pool.v.copy_(torch.randn(pool.v.shape, generator=g))
-    seqs = [KVSeq(pool) for _ in range(16 // tokens)]
-    for s, n in zip(seqs, [3, 40, 150, 300, 700, 1, 64, 65, 129, 9, 17, 33, 250, 5, 90, 400][:len(seqs)]):
-        BatchMeta([(s, n, 0, True)], dev)
+    seqs = [KVSeq(pool) for _ in range(nseq)]
+    for i, s in enumerate(seqs):
+        BatchMeta([(s, CTX[i % 16] + i // 16, 0, True)], dev)
     meta = BatchMeta([(s, tokens, s.length, True) for s in seqs], dev, gqa=H // KVH)
     T = meta.T
+    assert T == tokens * nseq
     q = torch.randn(T, H * hd, generator=g).to(dev)
     ns = ops.attn_nsplit(meta.max_keys, meta.n_items, KVH)
     part_ml = torch.empty(T * H * ns * 2, device=dev)
     part_o = torch.empty(T * H * ns * hd, device=dev)
     tickets = torch.zeros(meta.n_items * KVH, dtype=torch.int32, device=dev)
     out = torch.empty(T, H * hd, device=dev)
-    xp = ops.XPack(H * hd, dev)
+    xp = ops.XPack(H * hd, dev, T)
+    ops.launch_counts_reset()
     ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0],
                   pool.v[0], H, KVH, hd, 1 / math.sqrt(hd), ns, part_ml, part_o, out, tickets=tickets,
                   keys_per_split=128, opack=xp)
     torch.cuda.synchronize()
-    _check_packed(xp, out, T)
+    c = ops.launch_counts()
+    assert c["attn_opack"] == 1 and c["attn_decode" if tokens == 1 else "attn_mfma"] == 1, c
+    _check_packed_rb(xp, out, T)
+    assert int(tickets.abs().sum()) == 0   # the in-launch merge left its tickets zeroed
+
+
+@pytest.mark.parametrize("tokens,nseq", [(2, 8), (4, 8), (1, 16)])
+def test_attention_poison_reaches_the_packed_o_input(dev, tokens, nseq):
+    """A broken host contract (a token sees more keys than its block table maps) poisons the attention output: NaN in
+    the fp32 rows AND in the packed copy the o projection reads (k_gemm_xp), so the o projection's output rows are
+    NaN instead of being computed from a previous layer's stale fragments; the other items stay finite and the
+    merge tickets stay balanced."""
+    H, KVH, hd = 28, 4, 128
+    g = torch.Generator().manual_seed(7 + tokens)
+    pool = KVPool(1, KVH, hd, 1024, 16, dev)
+    pool.k.copy_(torch.randn(pool.k.shape, generator=g))
+    pool.v.copy_(torch.randn(pool.v.shape, generator=g))
+    seqs = [KVSeq(pool) for _ in range(nseq)]
+    for i, s in enumerate(seqs):
+        BatchMeta([(s, 200 + 37 * i, 0, True)], dev)
+    meta = BatchMeta([(s, tokens, s.length, True) for s in seqs], dev, gqa=H // KVH)
+    T = meta.T
+    bad = 1   # session 1's tokens claim 4096 more keys than its pages hold
+    rows = list(range(bad * tokens, (bad + 1) * tokens))
+    nv = meta.tok_nvis.clone()
+    nv[rows] += 4096
+    q = torch.randn(T, H * hd, generator=g).to(dev)
+    ns = ops.attn_nsplit(meta.max_keys, meta.n_items, KVH)
+    part_ml = torch.empty(T * H * ns * 2, device=dev)
+    part_o = torch.empty(T * H * ns * hd, device=dev)
+    tickets = torch.zeros(meta.n_items * KVH, dtype=torch.int32, device=dev)
+    att = torch.zeros(T, H * hd, device=dev)
+    xp = ops.XPack(H * hd, dev, T)
+    xp.hi.zero_()   # a stale, finite previous content
+    xp.lo.zero_()
+    ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, nv, meta.block_table, pool.PS, pool.k[0], pool.v[0],
+                  H, KVH, hd, 1 / math.sqrt(hd), ns, part_ml, part_o, att, tickets=tickets, keys_per_split=128,
+                  opack=xp)
+    wo = ops.PackedLinear((torch.randn(3584, H * hd, generator=g) * 0.02).to(torch.bfloat16).to(dev))
+    y = torch.zeros(T, 3584, device=dev)
+    wo(att, out=y, residual=True, M=T, xpack=xp if T > 8 else None)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(y).all(dim=1).cpu()
+    assert not fin[rows].any(), "poisoned rows must be NaN after the o projection"
+    others = [r for r in range(T) if r not in rows]
+    assert fin[others].all()
+    assert int(tickets.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("M", [32, 27, 20])
