@@ -69,6 +69,9 @@ _SIGS = {
     "fo_attention_set_opack": (c_int, [c_vp, c_vp, c_int, c_int]),
     "fo_launch_counts": (c_int, [ctypes.POINTER(c_ll), c_int]),
     "fo_launch_counts_reset": (c_int, []),
+    "fo_subsample_ws_floats": (c_ll, [c_int, c_int, c_int, c_int]),
+    "fo_subsample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_ll, c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),
     "fo_pack_weight": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     "fo_gemm_pick_split": (c_int, [c_int, c_int, c_int]),

@@ -393,7 +393,8 @@ def h2d(a, device, dtype=None):
 
 # ---------------------------------------------------------------- launch counters (include/fo_hip.h FoLaunchKind)
 LAUNCH_KINDS = ("gemm_xs", "gemm_xsk", "gemm_xp", "gemm_reduce", "gemm_ln", "gemm_xp32", "gemm_ypack", "gemm_ypack32",
-                "gemm_mid", "gemm_rope4", "gemm_pipe", "gemm_other", "attn_mfma", "attn_decode", "attn_opack", "relpos")
+                "gemm_mid", "gemm_rope4", "gemm_pipe", "gemm_other", "attn_mfma", "attn_decode", "attn_opack", "relpos",
+                "subsample")
 
 
 def launch_counts():
@@ -454,6 +455,19 @@ def im2col_3x3s2(x, B, C, H, W, strides, out, mean=None, istd=None):
     _lib.call("fo_im2col_3x3s2", x.data_ptr(), B, C, H, W, *strides, ptr(mean), ptr(istd), out.data_ptr(),
               out.stride(0), stream(x.device))
     return out
+
+
+def subsample(feats, B, R, F, mean, istd, w1, b1, C, y1, w2p, b2, z):
+    """Conv2dSubsampling4 (+ GlobalCMVN) up to its output Linear: feats [B, R, F] -> z [B * H2, C * W2]
+    (fo_subsample; split-K scratch at the tail of the stream's Runtime workspace)."""
+    n = int(_lib.load().fo_subsample_ws_floats(B, R, F, C))
+    rt = Runtime.get(feats.device)
+    if n > rt.ws.numel():
+        raise RuntimeError(f"subsample: {n} workspace floats > {rt.ws.numel()}")
+    _lib.call("fo_subsample", feats.data_ptr(), B, R, F, mean.data_ptr(), istd.data_ptr(), w1.data_ptr(), b1.data_ptr(),
+              C, y1.data_ptr(), w2p.data_ptr(), b2.data_ptr(), z.data_ptr(), rt.ws.data_ptr(), rt.ws.numel(),
+              stream(feats.device))
+    return z
 
 
 def tcf_permute(x, B, T, F, C, out):

@@ -129,10 +129,14 @@ class SpeechEncoderEngine:
         self.cap = self.buffersize + 8
         g = lambda n, dt=F32: src.get(p + n, dt)  # noqa: E731
         self.mean, self.istd = g("global_cmvn.mean"), g("global_cmvn.istd")
-        self.conv1 = PackedLinear(g("enc.0.core.conv.0.weight", torch.bfloat16).reshape(self.C, 9),
-                                  g("enc.0.core.conv.0.bias"))
-        self.conv2 = PackedLinear(g("enc.0.core.conv.2.weight", torch.bfloat16).reshape(self.C, self.C * 9),
-                                  g("enc.0.core.conv.2.bias"))
+        # Conv2dSubsampling4 (fo_subsample): conv1 as a 9-tap fp32 stencil (bf16-valued weights, as the GEMMs see them),
+        # conv2 as an implicit GEMM with K tap-major: its weight packed from [C][C][3][3] permuted to [C][3][3][C]
+        if self.C % 32:
+            raise ValueError(f"subsampling-output-dim {self.C}: the implicit conv2 needs a multiple of 32")
+        self.conv1_w = g("enc.0.core.conv.0.weight", torch.bfloat16).float().reshape(self.C, 9).contiguous()
+        self.conv1_b = g("enc.0.core.conv.0.bias")
+        self.conv2 = PackedLinear(g("enc.0.core.conv.2.weight", torch.bfloat16).permute(0, 2, 3, 1)
+                                  .reshape(self.C, 9 * self.C), g("enc.0.core.conv.2.bias"))
         self.out = PackedLinear(g("enc.0.core.out.0.weight", torch.bfloat16), g("enc.0.core.out.0.bias"))
         self.embed = PackedLinear(g("enc.1.embed.0.weight", torch.bfloat16), g("enc.1.embed.0.bias"))
         self.embed_ln = (g("enc.1.embed.1.weight"), g("enc.1.embed.1.bias"))
@@ -163,7 +167,7 @@ class SpeechEncoderEngine:
 
     @property
     def weight_bytes(self):
-        n = self.conv1.nbytes + self.conv2.nbytes + self.out.nbytes + self.embed.nbytes
+        n = self.conv1_w.numel() * 2 + self.conv2.nbytes + self.out.nbytes + self.embed.nbytes
         for L in self.layers:
             n += L["qkv"].nbytes + L["out"].nbytes + L["ff1"].nbytes + L["ff2"].nbytes
         return n
@@ -182,8 +186,7 @@ class SpeechEncoderEngine:
         H1, W1, H2, W2 = self.dims(R)
         T, C, dev = H2, self.C, self.device
         e = lambda *shape: torch.empty(*shape, dtype=F32, device=dev)  # noqa: E731
-        return {"x1": e(B * H1 * W1, 32), "y1": e(B * H1 * W1, C), "x2": e(B * H2 * W2, self.conv2.Kp),
-                "y2": e(B * H2 * W2, C), "z": e(B * T, C * self.F), "o": e(B * T, self.out.N),
+        return {"y1": e(B * H1 * W1, C), "z": e(B * T, C * self.F), "o": e(B * T, self.out.N),
                 "x": e(B * T, self.d), "h": e(B * T, self.d), "qkv": e(B * T, 3 * self.d),
                 "att": e(B * T, self.d), "f": e(B * T, self.layers[0]["ff1"].N),
                 "sA": ops.RowStats(B * T, dev, with_sums=True), "sB": ops.RowStats(B * T, dev, with_sums=True),
@@ -217,11 +220,8 @@ class SpeechEncoderEngine:
         """The device part of infer(): bufs from buffers(B, R) with bufs['meta'] already uploaded."""
         H1, W1, H2, W2 = self.dims(R)
         T, C = H2, self.C
-        ops.im2col_3x3s2(feats, B, 1, R, 80, (R * 80, 0, 80, 1), bufs["x1"], self.mean, self.istd)
-        self.conv1(bufs["x1"], out=bufs["y1"], act="relu")
-        ops.im2col_3x3s2(bufs["y1"], B, C, H1, W1, (H1 * W1 * C, 1, W1 * C, C), bufs["x2"])
-        self.conv2(bufs["x2"], out=bufs["y2"], act="relu")
-        ops.tcf_permute(bufs["y2"], B, T, self.F, C, bufs["z"])
+        ops.subsample(feats, B, R, 80, self.mean, self.istd, self.conv1_w, self.conv1_b, C, bufs["y1"],
+                      self.conv2.packed, self.conv2.bias, bufs["z"])
         self.out(bufs["z"], out=bufs["o"])
         x = self.embed(bufs["o"], out=bufs["x"])
         ops.layernorm(x, *self.embed_ln, out=x, relu=True)

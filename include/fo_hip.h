@@ -146,6 +146,7 @@ enum FoLaunchKind {
   FO_L_ATTN_DECODE = 13,/* k_attn_decode */
   FO_L_ATTN_OPACK = 14, /* an attention launch that wrote packed output */
   FO_L_RELPOS = 15,     /* k_relpos_fused */
+  FO_L_SUBSAMPLE = 16,  /* fo_subsample: the encoder front end (conv1 stencil + conv2 implicit GEMM + transpose) */
   FO_LAUNCH_KINDS = 24
 };
 int fo_launch_counts(long long* out, int n);
@@ -216,6 +217,16 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
                  const int* block_table, int maxb, int PS, const float* kc, const float* vc, int H, int KVH, int hd,
                  float scale, int nsplit, float* part_ml, float* part_o, float* out, int* tickets,
                  int keys_per_split, hipStream_t s);
+/* Conv2dSubsampling4.infer up to its output Linear (models/encoder/subsampling.py:67-73) with GlobalCMVN
+ * (models/encoder/cmvn.py:24-35): feats [B][R][F] fp32 -> z [B * H2][C * W2] (the Linear's input rows, the reference's
+ * x.transpose(1, 2).view(b, t, c * f)), H1 = (R - 3) / 2 + 1, W1 = (F - 3) / 2 + 1, H2 / W2 likewise from H1 / W1.
+ * w1 [C][9] fp32 (conv.0 weight), b1 [C]; y1: scratch [B * H1 * W1][C]; w2p: conv.2's weight [C][C][3][3] permuted to
+ * [C][3][3][C] (K tap-major) and packed by fo_pack_weight; b2 [C]; ws >= fo_subsample_ws_floats(B, R, F, C) floats
+ * (split-K partial slabs).  C % 32 == 0. */
+long long fo_subsample_ws_floats(int B, int R, int F, int C);
+int fo_subsample(const float* feats, int B, int R, int F, const float* mean, const float* istd, const float* w1,
+                 const float* b1, int C, float* y1, const void* w2p, const float* b2, float* z, float* ws,
+                 long long ws_floats, hipStream_t s);
 /* encoder MultiHeadedAttention.infer left-chunk buffer as a ring + rel-pos scores
  * (models/encoder/attention.py:407-459) */
 int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,
