@@ -70,15 +70,17 @@ __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
 // more than 1/16 full here, and no split / merge round trip is needed at <= 4096 keys.
 constexpr int DEC_MAXK = MAXPG * 16;
 constexpr int DEC_NW = 8, DEC_NT = DEC_NW * 64;  // 8 waves: a key per thread up to 512 keys
+// One (work item, head) of the decode attention; the normalised output row is left in o_s[HD] (LDS, visible to
+// every thread after the call) and, unless to_lds_only, stored to out (+ the packed copy when armed).  Returns
+// false when the host contract is broken (the row is then NaN, stored and in o_s).
 template <int HD>
-__global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
+__device__ bool attn_decode_row(const AttnArgs& a, const int it, const int h, float* o_s, bool to_lds_only) {
   static_assert(HD % 4 == 0 && HD <= 128, "decode attention: head_dim");
   __shared__ float s_s[DEC_MAXK];
   __shared__ float q_s[HD];
   __shared__ float acc_s[DEC_NW][HD];
   __shared__ float red_s[DEC_NW];
   __shared__ int pg_s[MAXPG];
-  const int it = blockIdx.x, h = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // items == NULL: the dense decode batch (item b = sequence b = token b), nothing to look up first
   const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it;
@@ -93,10 +95,13 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
   float* orow = a.out + ((size_t)t0 * a.H + h) * HD;
   if (L > DEC_MAXK || (L + a.PS - 1) / a.PS > nb) {  // host contract broken: poison, never read wrong keys
     for (int d = tid; d < HD; d += DEC_NT) {
+      o_s[d] = NAN;
+      if (to_lds_only) continue;
       orow[d] = NAN;   // (and the packed copy the next GEMM reads, when armed)
       if (a.oph) xpack_store(a.oph, a.opl, t0, h * HD + d, NAN, a.prb);
     }
-    return;
+    __syncthreads();
+    return false;
   }
   __syncthreads();
   const size_t page_sz = (size_t)a.KVH * a.PS * HD, head_off = (size_t)h * a.PS * HD;
@@ -174,9 +179,120 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
     float o = 0.f;
 #pragma unroll
     for (int w = 0; w < DEC_NW; ++w) o += acc_s[w][d];
+    o_s[d] = o / sum;
+    if (to_lds_only) continue;
     orow[d] = o / sum;
     if (a.oph) xpack_store(a.oph, a.opl, t0, h * HD + d, o / sum, a.prb);
   }
+  __syncthreads();
+  return true;
+}
+
+template <int HD>
+__global__ __launch_bounds__(DEC_NT) void k_attn_decode(AttnArgs a) {
+  __shared__ float o_s[HD];
+  attn_decode_row<HD>(a, blockIdx.x, blockIdx.y, o_s, false);
+}
+
+// The AR speech decoder's attention fused with its o projection, residual add and the next RMSNorm's statistics
+// (models/decoder/decoder.py:341-349 through LlamaAttention.o_proj + the residual of LlamaDecoderLayer): o is a
+// sum over heads, o[s] = sum_h att[s][h] . Wo[:, h*HD:(h+1)*HD]^T, so each (session, head) workgroup multiplies its
+// own attention row by its head's slice of the packed o weight (N x HD, loaded into registers at the start, while the
+// attention runs) and publishes an N-wide partial; the last head to arrive for a session (agent-scope release /
+// acquire ticket, as the split merge) sums the H partials in head order (deterministic), adds the residual and
+// writes x (in place), yg = x * gamma_next and the row's sum of squares (one statistics group) -- the next
+// gate/up GEMM's RMSNorm-on-load input.  Workgroups of one head are dealt to one XCD (its L2 serves the head's
+// slice to every session).  For o slices of <= 128 KiB per head (the 896-wide decoder; not Qwen2's 3584 x 128).
+struct AttnOArgs {
+  const bf16x8* wo;   // packed [N/16][K/32][64][8], K = H * HD
+  float* part;        // [S][H][N]
+  int* tickets;       // [S] zeroed, left zeroed
+  float* x;           // [S][ldx] residual stream, updated in place
+  const float* gnext; // [N]
+  float* yg;          // [S][ldx]
+  float* sout;        // [S]
+  int N, ldx, KS;     // KS = K / 32
+};
+constexpr int AO_TILES = 8;   // 16-column tiles per wave (8 waves: up to 128 * 8 = 1024 columns)
+template <int HD>
+__global__ __launch_bounds__(DEC_NT) void k_attn_decode_o(AttnArgs a, AttnOArgs o) {
+  constexpr int KPH = HD / 32;   // k-steps per head
+  __shared__ float o_s[HD];
+  __shared__ float red_s[DEC_NW];
+  __shared__ int last_s;
+  const int S = gridDim.x / (8 * ((a.H + 7) / 8));
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int h = xcd + 8 * (slot / S), it = slot % S;
+  if (h >= a.H) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ntiles = (o.N + 15) / 16;
+  // this head's o weight fragments: wave w owns tiles w*AO_TILES .. +AO_TILES, both of the head's k-steps
+  bf16x8 wf[AO_TILES][KPH];
+#pragma unroll
+  for (int t = 0; t < AO_TILES; ++t) {
+    const int tile = wave * AO_TILES + t;
+#pragma unroll
+    for (int k = 0; k < KPH; ++k)
+      if (tile < ntiles) wf[t][k] = __builtin_nontemporal_load(o.wo + ((size_t)tile * o.KS + h * KPH + k) * 64 + lane);
+  }
+  attn_decode_row<HD>(a, it, h, o_s, true);
+  // A fragments of the attention row (row 0 of a 16-row block; the other rows zero), fp32 split into hi + lo
+  bf16x8 ah[KPH], al[KPH];
+#pragma unroll
+  for (int k = 0; k < KPH; ++k) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (lane & 15) == 0 ? o_s[k * 32 + 8 * (lane >> 4) + e] : 0.f;
+      const __bf16 hv = (__bf16)v;
+      ah[k][e] = hv;
+      al[k][e] = (__bf16)(v - (float)hv);
+    }
+  }
+  const int s = a.items ? a.items[3 * it + 1] : it;   // this item's token (decode: one per sequence)
+  float* prow = o.part + ((size_t)s * a.H + h) * o.N;
+#pragma unroll
+  for (int t = 0; t < AO_TILES; ++t) {
+    const int tile = wave * AO_TILES + t;
+    if (tile >= ntiles) break;   // wave-uniform
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KPH; ++k) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[k], wf[t][k], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[k], wf[t][k], acc, 0, 0, 0);
+    }
+    const int n = tile * 16 + lane;
+    if (lane < 16 && n < o.N) prow[n] = acc[0];   // D row 0: lanes 0..15, element 0
+  }
+  // publish the partial and take the session's ticket (the split-merge protocol of attn_arrive_and_merge)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(o.tickets + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = old == a.H - 1;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(o.tickets + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const float* ps = o.part + (size_t)s * a.H * o.N;
+  float ssq = 0.f;
+  for (int n = tid; n < o.N; n += DEC_NT) {
+    float v = 0.f;
+    for (int hh = 0; hh < a.H; ++hh) v += ps[(size_t)hh * o.N + n];   // head order: deterministic
+    const size_t off = (size_t)s * o.ldx + n;
+    const float y = o.x[off] + v;
+    o.x[off] = y;
+    o.yg[off] = y * o.gnext[n];
+    ssq += y * y;
+  }
+  ssq = block_sum<DEC_NW>(ssq, red_s);
+  if (tid == 0) o.sout[s] = ssq;
 }
 
 // merge split partials: grid (T, H)
@@ -445,6 +561,27 @@ int fo_attention_set_opack(void* hi, void* lo, int cols, int cap_rb) {
   g_op_cols = cols;
   g_op_rb = cap_rb;
   return 0;
+}
+
+// Decode attention (one token per sequence, items NULL or one per token) fused with the o projection + residual
+// + next-norm statistics (k_attn_decode_o above).  Arguments as fo_attention's decode form, plus: wo packed o weight
+// (N x H*hd), part >= T * H * N floats, tickets T zeroed ints (left zeroed), x [T][ldx] residual (updated), gnext
+// [N], yg [T][ldx], sout [T] (one statistics group per row).
+int fo_attention_o(const float* q, int T, const int* items, const int* tok_nvis, const int* block_table, int maxb,
+                   int PS, const float* kc, const float* vc, int H, int hd, float scale, const void* wo, int N,
+                   float* part, int* tickets, float* x, int ldx, const float* gnext, float* yg, float* sout,
+                   hipStream_t s) {
+  FO_REQUIRE(T > 0 && H > 0 && hd == 64 && N > 0 && N <= 16 * AO_TILES * DEC_NW && ldx >= N,
+             "fo_attention_o: T=%d H=%d hd=%d N=%d (N <= %d)", T, H, hd, N, 16 * AO_TILES * DEC_NW);
+  FO_REQUIRE((long long)maxb * PS <= DEC_MAXK, "fo_attention_o: %d keys per sequence exceed %d", maxb * PS, DEC_MAXK);
+  FO_REQUIRE(wo && part && tickets && x && gnext && yg && sout, "fo_attention_o: null argument");
+  AttnArgs a{q, items, tok_nvis, block_table, kc, vc, nullptr, nullptr, nullptr, H, H, PS, maxb, 1, scale,
+             nullptr, 0, 1, nullptr, nullptr, 1};
+  AttnOArgs o{reinterpret_cast<const bf16x8*>(wo), part, tickets, x, gnext, yg, sout, N, ldx, H * hd / 32};
+  const int grid = 8 * T * ((H + 7) / 8);
+  hipLaunchKernelGGL((k_attn_decode_o<64>), dim3(grid), dim3(DEC_NT), 0, s, a, o);
+  fo::count_launch(FO_L_ATTN_O);
+  return fo::check_launch("fo_attention_o");
 }
 
 int fo_attn_nsplit(int max_keys, int n_items, int KVH) {

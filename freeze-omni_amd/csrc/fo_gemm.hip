@@ -955,6 +955,7 @@ void launch_mid(dim3 grid, const GemmArgs& a, hipStream_t s) {
 }
 
 thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
+int g_xs_var = 0;                                   // fo_gemm_set_xs_variant (probes)
 // packed activations armed for the calling thread's next launch, with their extent (cols, allocated row blocks)
 struct PackArm {
   const void* p0 = nullptr;
@@ -1024,11 +1025,19 @@ void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, h
 //  * per unit the NW partial tiles are reduced through LDS (two barriers), then the epilogue of the
 //    row-major output (the post-scaled RMSNorm and SwiGLU) as in gemm_body.
 constexpr int XS_NW = 8, XS_KPW = 14;
-template <int NW, int KPW>  // the SwiGLU pair (gate, up) of one 16-column output tile per unit
+// VAR (probes, fo_gemm_set_xs_variant): bit 0 = no cross-wave reduction (wave 0's partial is stored: WRONG
+// results, the barrier-free bound), bit 1 = default cache policy on the weight loads instead of nt, bit 2 = the
+// cross-wave reduction without workgroup barriers: per-unit partial slots double-buffered by unit parity, an LDS
+// arrival counter per slot; the wave that arrives last sums the NW partials in wave order (the same order, so the
+// same bits as the barrier form) and runs the unit's epilogue while the other waves stream on; a wave reuses a slot
+// only once the reduction two units back has been consumed (LDS generation word)
+template <int NW, int KPW, int VAR = 0>  // the SwiGLU pair (gate, up) of one 16-column output tile per unit
 __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
+  constexpr bool BF = (VAR & 4) != 0;
   __shared__ bf16x8 xlo[NW][KPW][64];
-  __shared__ float part[NW][2][16][17];
+  __shared__ float part[BF ? 2 : 1][NW][2][16][17];
   __shared__ float rstd_s[16];
+  __shared__ int arr_s[2], gen_s[2];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int KS = NW * KPW;
   const int ub = (int)((long)units * blockIdx.x / gridDim.x);
@@ -1045,7 +1054,8 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
   auto issue = [&](bf16x8 (&w)[KPW], int tile) {
 #pragma unroll
     for (int j = 0; j < KPW; ++j)
-      w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024, 2));
+      w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024,
+                                                                               (VAR & 2) ? 0 : 2));
   };
   issue(w0, ub < ue ? 2 * ub : a.ntiles);
   issue(w1, ub < ue ? 2 * ub + 1 : a.ntiles);
@@ -1085,6 +1095,13 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
       if (lane == 0) rstd_s[rr] = rsqrtf(v / (float)a.K + a.reps);
     }
   }
+  if constexpr (BF) {
+    if (threadIdx.x < 2) {
+      arr_s[threadIdx.x] = 0;
+      gen_s[threadIdx.x] = 0;
+    }
+    __syncthreads();   // rstd_s and the counters, once (the only workgroup barrier of this form)
+  }
   auto compute = [&](bf16x8 (&w)[KPW]) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1103,21 +1120,70 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
     issue(w0, nxt);
     const f32x4 c1 = compute(w1);
     issue(w1, nxt + (u + 1 < ue ? 1 : 0));
+    if constexpr ((VAR & 1) != 0) {   // probe: no cross-wave reduction (the barrier-free bound; wrong results)
+      if (wave == 0 && lane < 16)
+        for (int i = 0; i < 4; ++i)
+          if (4 * 0 + i < a.M) epilogue_store(a, true, i, u * 16 + lane, c0[i], c1[i]);
+      continue;
+    }
+    if constexpr (BF) {
+      const int k = u - ub, sl = k & 1;
+      // the slot's previous unit (k - 2) must have been reduced: its reducer bumps gen_s[sl] once done reading
+      if (k >= 2) {
+        while (__hip_atomic_load(&gen_s[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (k >> 1))
+          __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        part[sl][wave][0][4 * (lane >> 4) + i][lane & 15] = c0[i];
+        part[sl][wave][1][4 * (lane >> 4) + i][lane & 15] = c1[i];
+      }
+      // LDS only: a wave's ds operations execute in order, so its partial writes land before its counter add; the
+      // asm orders the compiler and waits for them (no vmcnt wait: the weight loads stay in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      int old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(&arr_s[sl], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old != NW - 1) continue;   // another wave reduces this unit
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&arr_s[sl], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // this wave: the unit's 16 x 16 outputs, 4 per lane (rows 4 (lane >> 4) .. + 3, column lane & 15)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = 4 * (lane >> 4) + i, c = lane & 15;
+        float x1 = 0.f, x2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          x1 += part[sl][w][0][rr][c];
+          x2 += part[sl][w][1][rr][c];
+        }
+        if (a.rstats) {
+          x1 *= rstd_s[rr];
+          x2 *= rstd_s[rr];
+        }
+        const int n = u * 16 + c;
+        if (rr < a.M && n < a.N) epilogue_store(a, true, rr, n, x1, x2);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the partial reads are done: the slot is free
+      if (lane == 0) __hip_atomic_fetch_add(&gen_s[sl], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      continue;
+    } else {
     __syncthreads();  // the previous unit's epilogue has read part[]
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      part[wave][0][4 * (lane >> 4) + i][lane & 15] = c0[i];
-      part[wave][1][4 * (lane >> 4) + i][lane & 15] = c1[i];
+      part[0][wave][0][4 * (lane >> 4) + i][lane & 15] = c0[i];
+      part[0][wave][1][4 * (lane >> 4) + i][lane & 15] = c1[i];
     }
     __syncthreads();
+    }
     const int e = threadIdx.x;
     if (e < 256) {
       const int rr = e >> 4, c = e & 15;
       float x1 = 0.f, x2 = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
-        x1 += part[w][0][rr][c];
-        x2 += part[w][1][rr][c];
+        x1 += part[0][w][0][rr][c];
+        x2 += part[0][w][1][rr][c];
       }
       if (a.rstats) {
         x1 *= rstd_s[rr];
@@ -1483,7 +1549,13 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.S = 1;
     if (sgroups) *sgroups = units;
     if (sout) FO_REQUIRE(!swiglu && !rope, "fo_gemm: statistics with a paired epilogue");
-    hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    switch (g_xs_var) {
+      case 1: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 1>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
+      case 2: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 2>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
+      case 3: hipLaunchKernelGGL((k_gemm_xs<16, 7>), dim3(G), dim3(16 * 64), 0, stream, a, units); break;
+      case 4: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 4>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
+      default: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
+    }
     fo::count_launch(FO_L_GEMM_XS);
     if (a.xph) fo::count_launch(FO_L_GEMM_XP);
     return fo::check_launch("fo_gemm/xs");
@@ -1820,6 +1892,14 @@ int fo_gemm_set_merge(int on) {
   FO_REQUIRE(on >= 0 && on <= 2, "fo_gemm_set_merge: 0, 1 or 2");
   const int prev = merge_mode();
   g_merge = on;
+  return prev;
+}
+
+int fo_gemm_set_xs_variant(int v) {
+  FO_REQUIRE(v >= 0 && v <= 4, "fo_gemm_set_xs_variant: 0 (shipped), 1 (no reduction: wrong results), 2 (default "
+             "cache policy), 3 (16 waves x 7 k-steps), 4 (barrier-free reduction)");
+  const int prev = g_xs_var;
+  g_xs_var = v;
   return prev;
 }
 

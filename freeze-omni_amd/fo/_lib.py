@@ -60,6 +60,7 @@ _SIGS = {
     "fo_gemm_tune": (c_int, [c_int, c_int]),
     "fo_gemm_set_u": (c_int, [c_int]),
     "fo_gemm_set_xs": (c_int, [c_int]),
+    "fo_gemm_set_xs_variant": (c_int, [c_int]),
     "fo_gemm_set_merge": (c_int, [c_int]),
     "fo_gemm_set_trace": (c_int, [c_vp]),
     "fo_gemm_set_xpack": (c_int, [c_vp, c_vp, c_int, c_int]),
@@ -70,6 +71,8 @@ _SIGS = {
     "fo_launch_counts": (c_int, [ctypes.POINTER(c_ll), c_int]),
     "fo_launch_counts_reset": (c_int, []),
     "fo_subsample_ws_floats": (c_ll, [c_int, c_int, c_int, c_int]),
+    "fo_attention_o": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_float, c_vp,
+                               c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "fo_subsample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_ll, c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),

@@ -394,7 +394,7 @@ def h2d(a, device, dtype=None):
 # ---------------------------------------------------------------- launch counters (include/fo_hip.h FoLaunchKind)
 LAUNCH_KINDS = ("gemm_xs", "gemm_xsk", "gemm_xp", "gemm_reduce", "gemm_ln", "gemm_xp32", "gemm_ypack", "gemm_ypack32",
                 "gemm_mid", "gemm_rope4", "gemm_pipe", "gemm_other", "attn_mfma", "attn_decode", "attn_opack", "relpos",
-                "subsample")
+                "subsample", "attn_o")
 
 
 def launch_counts():
@@ -559,6 +559,19 @@ def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc,
             _lib.call("fo_attention_set_opack", None, None, 0, 0)
         raise
     return out
+
+
+def attention_o(q, T, items, tok_nvis, block_table, PS, kc, vc, H, hd, scale, wo, part, tickets, x, gnext, yg, stats):
+    """Decode attention (one token per sequence, MHA) + the o projection (PackedLinear wo) + residual into x + the
+    next RMSNorm's statistics (stats: RowStats filled with one group; yg = x * gnext) -- fo_attention_o."""
+    if tickets.numel() < T or part.numel() < T * H * wo.N:
+        raise ValueError("attention_o: tickets / partial buffers too small")
+    _lib.call("fo_attention_o", q.data_ptr(), T, ptr(items), tok_nvis.data_ptr(), block_table.data_ptr(),
+              block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, hd, float(scale), wo.packed.data_ptr(), wo.N,
+              part.data_ptr(), tickets.data_ptr(), x.data_ptr(), x.stride(0), gnext.data_ptr(), yg.data_ptr(),
+              stats.buf.data_ptr(), stream(q.device))
+    stats.groups = 1
+    return x
 
 
 def enc_kv_write(k, v, B, T, d, start, length, ring, cap, kr, vr):

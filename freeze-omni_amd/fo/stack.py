@@ -19,6 +19,10 @@ from .ops import F32, PackedLinear
 # FO_ATTN_DENSE=0 passes the item table even for one-token-per-sequence batches (A/B against a
 # library older than fo_attention's items == NULL form)
 ATTN_DENSE = os.environ.get("FO_ATTN_DENSE", "1") == "1"
+# FO_ATTN_O=0: the decode attention and the o projection as two launches (A/B against k_attn_decode_o)
+ATTN_O = os.environ.get("FO_ATTN_O", "1") == "1"
+# FO_XPACK_SMALL=1: packed q|k|v / o inputs also at <= 8 rows for wide stacks (the Qwen2 text step; A/B)
+XPACK_SMALL = os.environ.get("FO_XPACK_SMALL", "0") == "1"
 
 
 class Layer:
@@ -52,6 +56,15 @@ class DecoderStack:
                                 swiglu_up=src.get(q + "mlp.up_proj.weight", torch.bfloat16))
             L.down = PackedLinear(src.get(q + "mlp.down_proj.weight", torch.bfloat16))
             self.layers.append(L)
+        # decode steps (one token per sequence) of an MHA stack with a small o projection -- the AR speech decoder, 14
+        # heads of 64, o 896 x 896 -- fuse the attention with the o projection (fo_attention_o: each (session, head)
+        # workgroup multiplies its attention row by its head's o slice; the last head sums the partials)
+        self.attn_o = ATTN_O and H == KVH and self.hd == 64 and D <= 1024 and n_layers > 0
+
+    def _packs(self, T):
+        """Whether a T-row forward writes / reads packed activations (9..64 rows; <= 8 rows too for wide stacks under
+        FO_XPACK_SMALL)."""
+        return 8 < T <= 64 or (XPACK_SMALL and T <= 8 and self.D >= 2048)
 
     @property
     def weight_bytes(self):
@@ -68,9 +81,12 @@ class DecoderStack:
               "sA": ops.RowStats(T, device), "sB": ops.RowStats(T, device),
               "xg": torch.empty(T, self.D, dtype=F32, device=device),
               "tickets": torch.zeros(max(T, 2) * KVH, dtype=torch.int32, device=device)}
-        if 8 < T <= 64 and ops.XPACK:   # packed activations for the q|k|v and o inputs (ops.XPack)
+        if self._packs(T) and ops.XPACK:   # packed activations for the q|k|v and o inputs (ops.XPack)
             ws["xgp"] = ops.XPack(self.D, device, T)
             ws["attp"] = ops.XPack(H * hd, device, T)
+        if self.attn_o:
+            ws["o_part"] = torch.empty(T * H * self.D, dtype=F32, device=device)
+            ws["o_tickets"] = torch.zeros(max(T, 1), dtype=torch.int32, device=device)
         if nsplit > 1:
             ws["part_ml"] = torch.empty(T * H * nsplit * 2, dtype=F32, device=device)
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
@@ -102,7 +118,12 @@ class DecoderStack:
         # steps) the X re-read is half as large and the extra stores cost more than the reads save (AR step 172.4 ->
         # 177.1 us, r04zf)
         xgp, attp = ws.get("xgp"), ws.get("attp")
-        if not 8 < T <= 64 or xgp is None or xgp.rows < T:
+        if not self._packs(T) or xgp is None or xgp.rows < T:
+            xgp = attp = None
+        # a decode batch takes the fused attention + o projection (the decode attention's form: one row per item)
+        fuse_o = (self.attn_o and "o_part" in ws and meta.n_items == T == meta.S and meta.max_rows == 1 and
+                  meta.block_table.shape[1] * self.pool.PS <= 4096)
+        if fuse_o:
             xgp = attp = None
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
@@ -114,11 +135,16 @@ class DecoderStack:
             if i == 0 and not pre_normed:
                 ops.rmsnorm(x, L.ln1, self.eps, out=h, round_fp16=self.first_fp16, M=T)
             L.qkv.qkv_rope(xin, T, *rope, norm=norm, xpack=xgp if i > 0 else None)
-            ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis,
-                          meta.block_table, self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale,
-                          nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps,
-                          opack=attp)
-            L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg), xpack=attp, ypack=xgp)
+            if fuse_o:
+                ops.attention_o(q, T, None if dense else meta.items, meta.tok_nvis, meta.block_table, self.pool.PS,
+                                self.pool.k[li], self.pool.v[li], H, hd, scale, L.o, ws["o_part"], ws["o_tickets"], x,
+                                L.ln2, xg, sB)
+            else:
+                ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis,
+                              meta.block_table, self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale,
+                              nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps,
+                              opack=attp)
+                L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg), xpack=attp, ypack=xgp)
             L.gu(xg, out=m, M=T, norm=(sB, self.eps), xpack=xgp)
             if i == last and final_norm is None:
                 L.down(m, out=x, residual=True, M=T)

@@ -89,6 +89,9 @@ int fo_gemm_set_u(int u);
  * o, gate/up, lm_head): 0 off, 1 on (default; FO_GEMM_XS=0 turns it off).  Process-global; returns the
  * previous setting. */
 int fo_gemm_set_xs(int on);
+/* probe hook: variant of the k_gemm_xs launch (0 shipped; 1 no cross-wave reduction -- WRONG results, a timing
+ * bound; 2 default-policy weight loads; 3 16 waves x 7 k-steps).  Process-global; returns the previous one. */
+int fo_gemm_set_xs_variant(int v);
 /* Split-K of the one-row-tile plain GEMMs (Qwen2 / TTS down, encoder FFN w2) merged inside the launch:
  * each split stores its partial tile write-through and takes the tile's ticket in `counters` (zeroed
  * ints, left zeroed); the last split sums every partial in split order (k_gemm_reduce's order, bit for
@@ -147,6 +150,7 @@ enum FoLaunchKind {
   FO_L_ATTN_OPACK = 14, /* an attention launch that wrote packed output */
   FO_L_RELPOS = 15,     /* k_relpos_fused */
   FO_L_SUBSAMPLE = 16,  /* fo_subsample: the encoder front end (conv1 stencil + conv2 implicit GEMM + transpose) */
+  FO_L_ATTN_O = 17,     /* k_attn_decode_o: decode attention + o projection + residual + next-norm statistics */
   FO_LAUNCH_KINDS = 24
 };
 int fo_launch_counts(long long* out, int n);
@@ -227,6 +231,17 @@ long long fo_subsample_ws_floats(int B, int R, int F, int C);
 int fo_subsample(const float* feats, int B, int R, int F, const float* mean, const float* istd, const float* w1,
                  const float* b1, int C, float* y1, const void* w2p, const float* b2, float* z, float* ws,
                  long long ws_floats, hipStream_t s);
+/* The AR speech decoder's decode attention (one token per sequence, MHA: KVH == H, hd 64; items NULL or one per
+ * token) fused with its o projection (LlamaAttention.o_proj, models/decoder/decoder.py:341-349), the layer's
+ * residual add and the next RMSNorm's statistics: x[t] += sum_h att[t][h] . Wo[:, h*hd:(h+1)*hd]^T (the H head
+ * partials summed in head order by the last head to finish, an agent-scope ticket), yg[t] = x[t] * gnext,
+ * sout[t] = sum x[t]^2 (one statistics group, read by the next fo_gemm_rms consumer with rgroups 1).
+ * wo: the o weight packed by fo_pack_weight (N <= 1024 outputs, K = H * hd); part >= T * H * N floats; tickets: T
+ * zeroed ints, left zeroed. */
+int fo_attention_o(const float* q, int T, const int* items, const int* tok_nvis, const int* block_table, int maxb,
+                   int PS, const float* kc, const float* vc, int H, int hd, float scale, const void* wo, int N,
+                   float* part, int* tickets, float* x, int ldx, const float* gnext, float* yg, float* sout,
+                   hipStream_t s);
 /* encoder MultiHeadedAttention.infer left-chunk buffer as a ring + rel-pos scores
  * (models/encoder/attention.py:407-459) */
 int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,

@@ -15,6 +15,7 @@
 #   profdup    rocprofv3 kernel trace + stats of a 20 s duplex run       -> <tag>_profdup/, <tag>_profdup_table.txt
 #   profstage  rocprofv3 kernel trace of scripts/llm_stage_time.py (LLM / encoder stage replays) -> <tag>_profstage_table.txt
 #   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
+#   vocpmc     vocoder: MFMA counter passes + FETCH_SIZE + kernel trace of one 8-user call -> <tag>_vocoder_mfma.json
 #   ddp1       bench.py as one torch.distributed.run rank (world 1: RCCL init, broadcast, checksum) -> <tag>_ddp1.json
 #   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
 #   ab         ENV_A / ENV_B (e.g. 'FO_X=0') alternated twice on the quick bench -> <tag>_ab.txt
@@ -65,6 +66,18 @@ for S in "$@"; do
             [ $rc -eq 0 ] && line ${O}_duplex.log ;;
     rehearsal) FO_DIST_REHEARSAL=1 timeout -k 10 600 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu-baseline \
              --no-single-user --out ${O}_rehearsal_n2.json > ${O}_rehearsal_n2.log 2>&1; rc=$? ;;
+    vocpmc) V="python3 $ROOTD/scripts/vocoder_time.py 8 3"
+           (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+             SQ_INSTS_VALU_MFMA_MOPS_BF16 --kernel-include-regex "k_conv|k_codec|k_silence" -d $ROOTD/${O}_voc_p1 -o p1 \
+             -f csv -- $V) > ${O}_voc_p1.log 2>&1 && \
+           (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex \
+             "k_conv|k_codec|k_silence" -d $ROOTD/${O}_voc_p2 -o p2 -f csv -- $V) > ${O}_voc_p2.log 2>&1 && \
+           (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_conv|k_codec|k_silence" \
+             -d $ROOTD/${O}_voc_p3 -o p3 -f csv -- $V) > ${O}_voc_p3.log 2>&1 && \
+           (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace -d $ROOTD/${O}_voc_t -o t -f csv -- $V) \
+             > ${O}_voc_t.log 2>&1 && timeout -k 10 120 python3 -u scripts/vocoder_time.py 8 20 > ${O}_voc_time.log 2>&1 && \
+           python3 scripts/pmc_json.py ${O}_vocoder_mfma.json ${O}_voc_p1 ${O}_voc_p2 ${O}_voc_t --pass3 ${O}_voc_p3 \
+             --note "$(tail -1 ${O}_voc_time.log)" > ${O}_voc_pmc.txt 2>&1; rc=$?; cat ${O}_voc_time.log; head -30 ${O}_voc_pmc.txt ;;
     ddp1)  timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 \
              --master-port 29517 bench.py --gpus 1 --steps 1 --warmup 1 --no-cpu-baseline --no-single-user \
              --out ${O}_ddp1.json > ${O}_ddp1.log 2>&1; rc=$?; [ $rc -eq 0 ] && line ${O}_ddp1.log ;;

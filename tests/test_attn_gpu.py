@@ -95,3 +95,43 @@ def test_single_row_decode_attention(dev, hd):
     ref = _reference(q, pool, seqs, host, H, KVH, hd, scale)
     torch.testing.assert_close(out.cpu().double(), ref, atol=1e-5, rtol=1e-5)
 
+
+
+@pytest.mark.parametrize("B,lens", [(8, [3, 40, 150, 300, 700, 1, 64, 129]), (3, [17, 2, 1000]), (16, None)])
+def test_decode_attention_fused_with_o_projection(dev, B, lens):
+    """fo_attention_o (the AR speech decoder's attention + o projection + residual + next-norm statistics in one
+    launch, the head partials summed in head order by the last head) against a float64 torch reference of
+    softmax(q K^T) V -> x + att Wo^T, yg = x * gamma, sum of squares: H = 14 heads of 64, o 896 x 896."""
+    H, hd, D = 14, 64, 896
+    g = torch.Generator().manual_seed(B * 7 + (lens[0] if lens else 0))
+    lens = lens or [int(x) for x in torch.randint(1, 900, (B,), generator=g)]
+    pool = KVPool(1, H, hd, 1024, 16, dev)
+    pool.k.copy_(torch.randn(pool.k.shape, generator=g))
+    pool.v.copy_(torch.randn(pool.v.shape, generator=g))
+    seqs = [KVSeq(pool) for _ in range(B)]
+    for s, n in zip(seqs, lens):
+        BatchMeta([(s, n - 1, 0, False)], dev) if n > 1 else None
+    meta = BatchMeta([(s, 1, s.length, False) for s in seqs], dev)
+    q = torch.randn(B, H * hd, generator=g)
+    wo = (torch.randn(D, H * hd, generator=g) / (H * hd) ** 0.5).to(torch.bfloat16)
+    gamma = 1 + 0.1 * torch.randn(D, generator=g)
+    x0 = torch.randn(B, D, generator=g)
+    lin = ops.PackedLinear(wo.to(dev))
+    x = x0.clone().to(dev)
+    yg = torch.empty(B, D, device=dev)
+    st = ops.RowStats(B, dev)
+    part = torch.empty(B * H * D, device=dev)
+    tickets = torch.zeros(B, dtype=torch.int32, device=dev)
+    ops.launch_counts_reset()
+    ops.attention_o(q.to(dev), B, None, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0], pool.v[0], H, hd,
+                    hd ** -0.5, lin, part, tickets, x, gamma.to(dev), yg, st)
+    torch.cuda.synchronize()
+    assert ops.launch_counts()["attn_o"] == 1 and st.groups == 1
+    att = _reference(q, pool, seqs, [(b, seqs[b].length) for b in range(B)], H, H, hd, hd ** -0.5)
+    ref = x0.double() + att @ wo.double().T
+    tol = 2e-5 * float(ref.abs().max())
+    assert (x.cpu().double() - ref).abs().max() < tol
+    assert (yg.cpu().double() - ref * gamma.double()).abs().max() < tol * 2
+    ss = (ref ** 2).sum(1)
+    assert torch.allclose(st.buf[:B].cpu().double(), ss, rtol=1e-5)
+    assert int(tickets.abs().sum()) == 0
