@@ -955,7 +955,14 @@ void launch_mid(dim3 grid, const GemmArgs& a, hipStream_t s) {
 }
 
 thread_local unsigned long long* g_trc = nullptr;  // fo_gemm_set_trace (probes)
-int g_xs_var = 0;                                   // fo_gemm_set_xs_variant (probes)
+int g_xs_var = -1;   // fo_gemm_set_xs_variant (probes); -1: FO_XS_VARIANT (0-4) decides at first use, default 0
+inline int xs_variant() {
+  if (g_xs_var < 0) {
+    const char* e = getenv("FO_XS_VARIANT");
+    g_xs_var = (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 0;
+  }
+  return g_xs_var;
+}
 // packed activations armed for the calling thread's next launch, with their extent (cols, allocated row blocks)
 struct PackArm {
   const void* p0 = nullptr;
@@ -1549,7 +1556,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.S = 1;
     if (sgroups) *sgroups = units;
     if (sout) FO_REQUIRE(!swiglu && !rope, "fo_gemm: statistics with a paired epilogue");
-    switch (g_xs_var) {
+    switch (xs_variant()) {
       case 1: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 1>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
       case 2: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 2>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
       case 3: hipLaunchKernelGGL((k_gemm_xs<16, 7>), dim3(G), dim3(16 * 64), 0, stream, a, units); break;
@@ -1898,7 +1905,7 @@ int fo_gemm_set_merge(int on) {
 int fo_gemm_set_xs_variant(int v) {
   FO_REQUIRE(v >= 0 && v <= 4, "fo_gemm_set_xs_variant: 0 (shipped), 1 (no reduction: wrong results), 2 (default "
              "cache policy), 3 (16 waves x 7 k-steps), 4 (barrier-free reduction)");
-  const int prev = g_xs_var;
+  const int prev = xs_variant();
   g_xs_var = v;
   return prev;
 }

@@ -1,7 +1,8 @@
 """Where does the X-stationary gate/up stream (k_gemm_xs, M = 16, K = 3584, the dominant kernel) lose against the
 lm_head's 6.4 TB/s?  Graph-replayed over weight copies beyond the Infinity Cache (as xs_balance_probe.py), the
 shipped kernel against probe variants (fo_gemm_set_xs_variant): 1 = no cross-wave LDS reduction (wrong results: the
-bound of removing the two barriers per unit), 2 = default-policy (not nt) weight loads, 3 = 16 waves x 7 k-steps.
+bound of removing the two barriers per unit), 2 = default-policy (not nt) weight loads, 3 = 16 waves x 7 k-steps, 4 = the
+cross-wave reduction without workgroup barriers (the last-arriving wave reduces; bit-identical to the shipped kernel).
 Also the Qwen2 lm_head (1.09 GB) for the achievable streaming rate.  python scripts/xs_variant_probe.py (GPU)."""
 import os
 import sys
