@@ -283,8 +283,16 @@ __global__ __launch_bounds__(DEC_NT) void k_attn_decode_o(AttnArgs a, AttnOArgs 
   const float* ps = o.part + (size_t)s * a.H * o.N;
   float ssq = 0.f;
   for (int n = tid; n < o.N; n += DEC_NT) {
+    // the H partials come from other XCDs' workgroups (a memory-side round trip each): all loads of a group of 16
+    // heads are issued together, then summed in head order (deterministic)
     float v = 0.f;
-    for (int hh = 0; hh < a.H; ++hh) v += ps[(size_t)hh * o.N + n];   // head order: deterministic
+    for (int h0 = 0; h0 < a.H; h0 += 16) {
+      float pv[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) pv[j] = h0 + j < a.H ? ps[(size_t)(h0 + j) * o.N + n] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v += pv[j];
+    }
     const size_t off = (size_t)s * o.ldx + n;
     const float y = o.x[off] + v;
     o.x[off] = y;

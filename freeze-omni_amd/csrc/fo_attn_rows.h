@@ -79,34 +79,80 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
     __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  // per row: split weights exp(m_q - M) (0 for empty splits) and 1 / l into LDS (w_s: [16][KT + 4],
-  // the kernel's P tile, ns <= KT), then every (row, d) sums its ns partials with independent loads
+  // per row: split weights exp(m_q - M) (0 for empty splits) and 1 / l into LDS (w_s: [16][KT + 4], the kernel's P
+  // tile, ns <= KT).  The partials were written by other XCDs' workgroups, so every read is a memory-side round trip:
+  // the loads are issued in groups of MQ splits (x EU outputs per thread below) before any of them is used, and the
+  // sums still run in split order (the same result bit for bit as a serial loop).
+  constexpr int MQ = 8, EU = 4;
   for (int r = tid; r < R; r += blockDim.x) {
     const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-    const float* ml = a.part_ml + th * a.nsplit * 2;
+    const float2* ml = reinterpret_cast<const float2*>(a.part_ml + th * a.nsplit * 2);
     float M = -INFINITY;
-    for (int q = 0; q < ns; ++q)
-      if (ml[2 * q + 1] > 0.f) M = fmaxf(M, ml[2 * q]);
+    for (int q0 = 0; q0 < ns; q0 += MQ) {
+      float2 v[MQ];
+#pragma unroll
+      for (int j = 0; j < MQ; ++j) v[j] = q0 + j < ns ? ml[q0 + j] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < MQ; ++j)
+        if (v[j].y > 0.f) M = fmaxf(M, v[j].x);
+    }
     float l = 0.f;
-    for (int q = 0; q < ns; ++q) {
-      const float ls = ml[2 * q + 1];
-      const float w = ls > 0.f ? expf(ml[2 * q] - M) : 0.f;
-      if (ls > 0.f) l += ls * w;
-      w_s[r * (KT + 4) + q] = w;
+    for (int q0 = 0; q0 < ns; q0 += MQ) {   // (second pass: cache hits)
+      float2 v[MQ];
+#pragma unroll
+      for (int j = 0; j < MQ; ++j) v[j] = q0 + j < ns ? ml[q0 + j] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < MQ; ++j) {
+        if (q0 + j >= ns) break;
+        const float w = v[j].y > 0.f ? expf(v[j].x - M) : 0.f;
+        if (v[j].y > 0.f) l += v[j].y * w;
+        w_s[r * (KT + 4) + q0 + j] = w;
+      }
     }
     w_s[r * (KT + 4) + KT] = 1.f / l;
   }
   __syncthreads();
-  for (int e = tid; e < R * HD; e += blockDim.x) {
-    const int r = e / HD, d = e - (e / HD) * HD;
-    const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-    const float* po = a.part_o + th * a.nsplit * HD + d;
-    const float* w = w_s + r * (KT + 4);
-    float o = 0.f;
-    for (int q = 0; q < ns; ++q)
-      if (w[q] != 0.f) o += po[(size_t)q * HD] * w[q];
-    a.out[th * HD + d] = o * w[KT];
-    if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, o * w[KT], a.prb);
+  const int RH = R * HD;
+  for (int e0 = tid; e0 < RH; e0 += EU * blockDim.x) {
+    const float* po[EU];
+    const float* w[EU];
+    size_t tho[EU];
+    float o[EU];
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      const int e = min(e0 + u * (int)blockDim.x, RH - 1);
+      const int r = e / HD, d = e - (e / HD) * HD;
+      const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
+      po[u] = a.part_o + th * a.nsplit * HD + d;
+      w[u] = w_s + r * (KT + 4);
+      tho[u] = th * HD + d;
+      o[u] = 0.f;
+    }
+    for (int q0 = 0; q0 < ns; q0 += MQ) {
+      float pv[EU][MQ];
+#pragma unroll
+      for (int u = 0; u < EU; ++u)
+#pragma unroll
+        for (int j = 0; j < MQ; ++j) {
+          const int q = q0 + j;
+          pv[u][j] = q < ns && w[u][q] != 0.f ? po[u][(size_t)q * HD] : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < EU; ++u)
+#pragma unroll
+        for (int j = 0; j < MQ; ++j) {
+          const int q = q0 + j;
+          if (q < ns && w[u][q] != 0.f) o[u] += pv[u][j] * w[u][q];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      if (e0 + u * (int)blockDim.x >= RH) break;
+      const float y = o[u] * w[u][KT];
+      a.out[tho[u]] = y;
+      if (a.oph) xpack_store(a.oph, a.opl, (int)(tho[u] / HD / a.H), (int)((tho[u] / HD) % a.H) * HD + (int)(tho[u] % HD),
+                             y, a.prb);
+    }
   }
 }
 

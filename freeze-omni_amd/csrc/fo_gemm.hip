@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
 // RoPE + paged-KV append, residual, row statistics).  k-steps past K (the last split of a long-K layer) load
 // nothing and multiply zero X.
 template <int NW, int KPW, int RB, int UA>   // UA units (2 UA tile buffers) of weights in flight per wave
-__global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
+__global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int G) {
   // the per-unit cross-wave reduction holds both tiles when the LDS allows, else one tile at a time
   constexpr int PT = (NW * RB * KPW * 1024 + NW * 2 * RB * 16 * 17 * 4 <= 160 * 1024) ? 2 : 1;
   __shared__ bf16x8 xlo[NW][RB][KPW][64];
@@ -1222,9 +1222,16 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units) {
   constexpr int ROWS = RB * 16;
   constexpr int NB = 2 * UA;
   const int KS = a.K >> 5;
-  const int sp = blockIdx.y;
-  const int ub = (int)((long)units * blockIdx.x / gridDim.x);
-  const int ue = (int)((long)units * (blockIdx.x + 1) / gridDim.x);
+  // XCD-aware placement: the S x G (split, column group) workgroups are dealt to the 8 XCDs (workgroup id % 8) in
+  // contiguous runs of the split-major order, so a split's column groups share one XCD (at most two): its X slice
+  // comes from HBM once and from that XCD's L2 after, instead of once per XCD (r04zs FETCH: the 40-row down read
+  // X ~8x, 160.2 MB per launch against 138.8 MB)
+  const int total = a.S * G, per_x = (total + 7) >> 3;
+  const int w = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+  if (w >= total) return;   // (the grid is 8 per_x: the padding workgroups leave before any barrier)
+  const int sp = w / G, gx = w - sp * G;
+  const int ub = (int)((long)units * gx / G);
+  const int ue = (int)((long)units * (gx + 1) / G);
   const int ks0 = sp * KW + wave * KPW;                 // this wave's first k-step
   const int nj = max(0, min(KPW, KS - ks0));            // its k-steps inside K (wave-uniform)
   const unsigned long long wbase = (unsigned long long)a.Wp;
@@ -1591,10 +1598,10 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.S = S;
     a.counters = nullptr;
     if (sgroups) *sgroups = (N + 255) / 256;
-    dim3 grid(G, S);
-    if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2, 2>), grid, dim3(512), 0, stream, a, units);
-    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<8, 4, 3, 3>), grid, dim3(512), 0, stream, a, units);
-    else hipLaunchKernelGGL((k_gemm_xsk<8, 3, 4, 4>), grid, dim3(512), 0, stream, a, units);
+    const dim3 grid(8 * ((S * G + 7) / 8));
+    if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2, 2>), grid, dim3(512), 0, stream, a, units, G);
+    else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<8, 4, 3, 3>), grid, dim3(512), 0, stream, a, units, G);
+    else hipLaunchKernelGGL((k_gemm_xsk<8, 3, 4, 4>), grid, dim3(512), 0, stream, a, units, G);
     int rc = fo::check_launch("fo_gemm/xsk");
     if (rc) return rc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, RBk * 16);

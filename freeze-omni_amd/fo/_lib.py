@@ -73,6 +73,10 @@ _SIGS = {
     "fo_subsample_ws_floats": (c_ll, [c_int, c_int, c_int, c_int]),
     "fo_attention_o": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_float, c_vp,
                                c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "fo_enc_attn_block": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_vp, c_vp, c_vp,
+                                  c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "fo_enc_attn_out": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fo_subsample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_ll, c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),

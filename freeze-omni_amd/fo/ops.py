@@ -394,7 +394,7 @@ def h2d(a, device, dtype=None):
 # ---------------------------------------------------------------- launch counters (include/fo_hip.h FoLaunchKind)
 LAUNCH_KINDS = ("gemm_xs", "gemm_xsk", "gemm_xp", "gemm_reduce", "gemm_ln", "gemm_xp32", "gemm_ypack", "gemm_ypack32",
                 "gemm_mid", "gemm_rope4", "gemm_pipe", "gemm_other", "attn_mfma", "attn_decode", "attn_opack", "relpos",
-                "subsample", "attn_o")
+                "subsample", "attn_o", "enc_block")
 
 
 def launch_counts():
@@ -570,6 +570,37 @@ def attention_o(q, T, items, tok_nvis, block_table, PS, kc, vc, H, hd, scale, wo
               block_table.shape[1], PS, kc.data_ptr(), vc.data_ptr(), H, hd, float(scale), wo.packed.data_ptr(), wo.N,
               part.data_ptr(), tickets.data_ptr(), x.data_ptr(), x.stride(0), gnext.data_ptr(), yg.data_ptr(),
               stats.buf.data_ptr(), stream(q.device))
+    stats.groups = 1
+    return x
+
+
+def enc_attn_block(x, B, T, h, ln1, qkv, kr, vr, cap, meta, ptab, bu, bv, out, scale, part, tickets, stats,
+                   eps=1e-5):
+    """The attention half of a speech-encoder block in one launch (fo_enc_attn_block): x [B*T, d] += linear_out(
+    relpos attention(q|k|v(LayerNorm1(x)))) in place; stats (RowStats with_sums) gets the updated rows' sums in one
+    group for the FFN's LayerNorm-on-load GEMM.  qkv / out: PackedLinear; meta: int32 [4B]."""
+    d = x.shape[1]
+    if part.numel() < B * h * T * d or tickets.numel() < B or stats.buf1 is None:
+        raise ValueError("enc_attn_block: partial / ticket / statistics buffers too small")
+    _lib.call("fo_enc_attn_block", x.data_ptr(), B, T, d, h, ln1[0].data_ptr(), ln1[1].data_ptr(), float(eps),
+              qkv.packed.data_ptr(), qkv.bias.data_ptr(), kr.data_ptr(), vr.data_ptr(), cap, meta.data_ptr(),
+              ptab.data_ptr(), bu.data_ptr(), bv.data_ptr(), out.packed.data_ptr(), out.bias.data_ptr(), float(scale),
+              part.data_ptr(), tickets.data_ptr(), stats.buf1.data_ptr(), stats.buf.data_ptr(), stream(x.device))
+    stats.groups = 1
+    return x
+
+
+def enc_attn_out(qkv, x, B, T, h, kr, vr, cap, meta, ptab, bu, bv, out, scale, part, tickets, stats):
+    """fo_enc_attn_out: the rel-pos attention of the chunk's q|k|v rows (qkv [B*T, >= 3d], bias applied) + linear_out
+    (PackedLinear out) + the residual into x (in place); stats (RowStats with_sums) gets the updated rows' sums in one
+    group."""
+    d = x.shape[1]
+    if part.numel() < B * h * T * d or tickets.numel() < B or stats.buf1 is None:
+        raise ValueError("enc_attn_out: partial / ticket / statistics buffers too small")
+    _lib.call("fo_enc_attn_out", qkv.data_ptr(), qkv.stride(0), x.data_ptr(), B, T, d, h, kr.data_ptr(), vr.data_ptr(),
+              cap, meta.data_ptr(), ptab.data_ptr(), bu.data_ptr(), bv.data_ptr(), out.packed.data_ptr(),
+              out.bias.data_ptr(), float(scale), part.data_ptr(), tickets.data_ptr(), stats.buf1.data_ptr(),
+              stats.buf.data_ptr(), stream(x.device))
     stats.groups = 1
     return x
 
@@ -772,23 +803,30 @@ class SampleCheck:
     def free(self):
         self.buf.free()
 
+    def __del__(self):   # the pinned word goes with its owner (a thread's default check dies with the thread)
+        try:
+            self.free()
+        except Exception:
+            pass
 
-_CHECKS = {}
-_CHECKS_LOCK = threading.Lock()
+
+_CHECKS = threading.local()
 
 
 def sample_check(device):
-    """The default SampleCheck of a device FOR THE CALLING THREAD (used when a sampler call passes none).  Keyed by
-    (device, thread): the eager text step, AudioLLM._post_decode, LLM2TTSCodecAR.infer and speak's eager loop may run
-    on several host threads (speech workers, server sessions), and a NaN row drawn by one thread must raise in that
-    thread's check, not in another's (check() clears the word on read)."""
+    """The default SampleCheck of a device FOR THE CALLING THREAD (used when a sampler call passes none).  Held in
+    thread-local storage: the eager text step, AudioLLM._post_decode, LLM2TTSCodecAR.infer and speak's eager loop may
+    run on several host threads (speech workers, server sessions), and a NaN row drawn by one thread must raise in that
+    thread's check, not in another's (check() clears the word on read); a thread's checks are released when it ends,
+    so a later thread (even one reusing its id) starts from a fresh, cleared word."""
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
-    key = (idx, threading.get_ident())
-    with _CHECKS_LOCK:
-        if key not in _CHECKS:
-            _CHECKS[key] = SampleCheck()
-        return _CHECKS[key]
+    per = getattr(_CHECKS, "by_device", None)
+    if per is None:
+        per = _CHECKS.by_device = {}
+    if idx not in per:
+        per[idx] = SampleCheck()
+    return per[idx]
 
 
 def sample(logits, V, out_ids, top_k=None, temperature=None, top_p=None, seed=0, step=None, out_max=None, B=None,

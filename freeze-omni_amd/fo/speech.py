@@ -22,6 +22,11 @@ import torch
 from . import ops, tables
 from .ops import F32, I32, PackedLinear
 
+# the encoder block's attention half: FO_ENC_BLOCK=0 three launches (LayerNorm-on-load q|k|v GEMM, rel-pos attention,
+# out GEMM + reduce); 1 one launch (fo_enc_attn_block: LayerNorm1 + q|k|v + attention + out + residual); 2 (default)
+# the q|k|v GEMM, then attention + out + residual in one launch (fo_enc_attn_out)
+ENC_BLOCK = int(os.environ.get("FO_ENC_BLOCK", "2") or 0)
+
 FRAMINGS = {
     # name: (chunk_frames, carried_frames, win, shift, nfft, scale)
     "A": (16, 3, 400, 160, 512, 32768.0),   # bin/inference.py:44-52, x32768 (:74)
@@ -164,6 +169,9 @@ class SpeechEncoderEngine:
         self.kr = torch.zeros(self.nb, max_sessions, self.cap, self.d, dtype=F32, device=self.device)
         self.vr = torch.zeros_like(self.kr)
         self.slots = SlotPool(max_sessions)
+        # the attention half of each block as one launch (fo_enc_attn_block) where the geometry fits it
+        self.fused_block = (ENC_BLOCK if self.dk == 64 and self.d % 256 == 0 and self.d <= 1024
+                            and self.cap + 8 <= 96 else 0)
 
     @property
     def weight_bytes(self):
@@ -194,7 +202,9 @@ class SpeechEncoderEngine:
                 # <= 64 rows: the out and FFN-down inputs also written packed by their producers (ops.XPack)
                 "attp": ops.XPack(self.d, dev, B * T) if B * T <= 64 and ops.XPACK else None,
                 "fp": ops.XPack(self.layers[0]["ff1"].N, dev, B * T) if B * T <= 64 and ops.XPACK else None,
-                "xp32": ops.XPack32(self.d, dev, B * T) if B * T <= 64 and ops.XPACK else None}
+                "xp32": ops.XPack32(self.d, dev, B * T) if B * T <= 64 and ops.XPACK else None,
+                "part": e(B * self.h * T * self.d) if self.fused_block and T <= 8 else None,
+                "tickets": torch.zeros(B, dtype=I32, device=dev)}
 
     def host_meta(self, caches, pe_indices):
         """Per-user ring / position metadata [starts | lens | rings | pos starts] and the next pe_index."""
@@ -235,6 +245,35 @@ class SpeechEncoderEngine:
         sA, sB = bufs["sA"], bufs["sB"]
         attp, fp, xp32 = (bufs.get("attp"), bufs.get("fp"), bufs.get("xp32")) if fuse_ln else (None, None, None)
         last = len(self.layers) - 1
+        if fuse_ln and bufs.get("part") is not None and self.fused_block == 1:
+            # a launch for the attention half (LayerNorm1 .. residual, + the row sums ff1's norm reads), then
+            # feed_forward as two GEMMs
+            for i, L in enumerate(self.layers):
+                ops.enc_attn_block(x, B, T, self.h, L["ln1"], L["qkv"], self.kr[i], self.vr[i], self.cap, meta,
+                                   self.ptab[i], L["bu"], L["bv"], L["out"], scale, bufs["part"], bufs["tickets"], sB)
+                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp)
+                L["ff2"](f, out=x, residual=True, xpack=fp)
+            ops.layernorm(x, *self.after, out=x)
+            return x, T
+        if fuse_ln and bufs.get("part") is not None and self.fused_block == 2:
+            # q|k|v by the LayerNorm-on-load GEMM, then attention + linear_out + residual (+ the row sums ff1's norm
+            # reads) in one launch, then feed_forward as two GEMMs (w_2 also writes the next block's statistics and
+            # its fp32 packed residual)
+            for i, L in enumerate(self.layers):
+                if i > 0:
+                    L["qkv"].ln(x, *L["ln1"], sA, out=qkv, xpack32=xp32)
+                else:
+                    ops.layernorm(x, *L["ln1"], out=h)
+                    L["qkv"](h, out=qkv)
+                ops.enc_attn_out(qkv, x, B, T, self.h, self.kr[i], self.vr[i], self.cap, meta, self.ptab[i], L["bu"],
+                                 L["bv"], L["out"], scale, bufs["part"], bufs["tickets"], sB)
+                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp)
+                if i < last:
+                    L["ff2"].rowstats(f, x, sA, residual=True, xpack=fp, ypack32=xp32)
+                else:
+                    L["ff2"](f, out=x, residual=True, xpack=fp)
+            ops.layernorm(x, *self.after, out=x)
+            return x, T
         for i, L in enumerate(self.layers):
             if fuse_ln and i > 0:
                 L["qkv"].ln(x, *L["ln1"], sA, out=qkv, xpack32=xp32)

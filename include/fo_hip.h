@@ -151,6 +151,7 @@ enum FoLaunchKind {
   FO_L_RELPOS = 15,     /* k_relpos_fused */
   FO_L_SUBSAMPLE = 16,  /* fo_subsample: the encoder front end (conv1 stencil + conv2 implicit GEMM + transpose) */
   FO_L_ATTN_O = 17,     /* k_attn_decode_o: decode attention + o projection + residual + next-norm statistics */
+  FO_L_ENC_BLOCK = 18,  /* k_enc_attn_block: the attention half of a speech-encoder block */
   FO_LAUNCH_KINDS = 24
 };
 int fo_launch_counts(long long* out, int n);
@@ -242,6 +243,24 @@ int fo_attention_o(const float* q, int T, const int* items, const int* tok_nvis,
                    int PS, const float* kc, const float* vc, int H, int hd, float scale, const void* wo, int N,
                    float* part, int* tickets, float* x, int ldx, const float* gnext, float* yg, float* sout,
                    hipStream_t s);
+/* The attention half of a speech-encoder block in one launch (models/encoder/transformer.py:103-118 with
+ * MultiHeadedAttention.infer, models/encoder/attention.py:407-459): x += linear_out(relpos_attention(linear_q|k|v(
+ * LayerNorm1(x)), ring)) for B sessions x T rows, in place, plus the updated rows' sums / sums of squares (ssum, ssq:
+ * [B * T], one statistics group for the next LayerNorm-on-load GEMM).  A workgroup per (session, head); head
+ * partials of linear_out in part (>= B * h * T * d floats) summed in head order by the session's last head
+ * (tickets: B zeroed ints, left zeroed).  wqkv: linear_q|k|v [3d][d] packed by fo_pack_weight, bqkv [3d]; wout:
+ * linear_out [d][d] packed, bout [d]; kr / vr, cap, meta [start B | len B | ring B | pos start B], ptab, bu, bv as
+ * fo_relpos_attention_fused.  Head size 64, T <= 8, d = 64 h a multiple of 256 and <= 1024, cap + T <= 96. */
+int fo_enc_attn_block(float* x, int B, int T, int d, int h, const float* lnw, const float* lnb, float ln_eps,
+                      const void* wqkv, const float* bqkv, float* kr, float* vr, int cap, const int* meta,
+                      const float* ptab, const float* bu, const float* bv, const void* wout, const float* bout,
+                      float scale, float* part, int* tickets, float* ssum, float* ssq, hipStream_t s);
+/* fo_enc_attn_block's second half alone: q|k|v given ([B * T] rows of ldq >= 3d floats, + bias: the LayerNorm-on-load
+ * GEMM's output), the rel-pos attention, linear_out, the residual and the row statistics in one launch. */
+int fo_enc_attn_out(const float* qkv, int ldq, float* x, int B, int T, int d, int h, float* kr, float* vr, int cap,
+                    const int* meta, const float* ptab, const float* bu, const float* bv, const void* wout,
+                    const float* bout, float scale, float* part, int* tickets, float* ssum, float* ssq,
+                    hipStream_t s);
 /* encoder MultiHeadedAttention.infer left-chunk buffer as a ring + rel-pos scores
  * (models/encoder/attention.py:407-459) */
 int fo_enc_kv_write(const float* k, const float* v, int ldkv, int B, int T, int d, const int* start, const int* len,

@@ -8,6 +8,7 @@
 #   quick      bench without the CPU baseline / config-2 leg, 3 turns    -> <tag>_quick.json
 #   prof       rocprofv3 --kernel-trace --stats of the bench (2 turns)   -> <tag>_prof/
 #   fetch      FETCH_SIZE pass on the dominant kernel                    -> <tag>_pmc/
+#   fetchdup   FETCH_SIZE pass on the duplex line's split-K / encoder kernels  -> <tag>_fetchdup.txt
 #   tts        rocprofv3 kernel stats of the AR decode step alone        -> <tag>_prof_tts/
 #   text       rocprofv3 kernel stats of the text step alone             -> <tag>_prof_text/
 #   steptrace  per-node timeline of the AR decode step (kernel trace)   -> <tag>_step_timeline.txt
@@ -49,6 +50,10 @@ for S in "$@"; do
     fetch) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gemm_xs -d $ROOTD/${O}_pmc \
              -o fetch -f csv -- python3 $ROOTD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-single-user) \
              > ${O}_pmc.log 2>&1; rc=$? ;;
+    fetchdup) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_gemm_xsk|k_subsample|k_enc" \
+             -d $ROOTD/${O}_pmcdup -o fetch -f csv -- python3 $ROOTD/bench.py --scenario duplex --duplex-sec 6 --steps 1 \
+             --warmup 1) > ${O}_pmcdup.log 2>&1 && python3 scripts/fetch_table.py ${O}_pmcdup > ${O}_fetchdup.txt 2>&1; rc=$?
+             cat ${O}_fetchdup.txt | head -30 ;;
     tts)   (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_tts -o tts -f csv -- \
              python3 $ROOTD/scripts/tts_step_time.py 8 multi) > ${O}_prof_tts.log 2>&1; rc=$? ;;
     steptrace) (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace -d $ROOTD/${O}_steptrace -o tts -f csv -- \

@@ -223,14 +223,18 @@ def test_real_geometry_encoder_adapter_match_reference(dev):
             close(emb, ref, rtol=2e-3, atol=2e-3 * float(np.abs(ref).max()))
 
 
-def test_real_geometry_batched_framing_b_encoder_matches_reference(dev):
+@pytest.mark.parametrize("fused", [2, 1, 0])
+def test_real_geometry_batched_framing_b_encoder_matches_reference(dev, fused):
     """The duplex tick's encoder shape at real geometry: 8 copies of real_encoder_t2's framing-B session in ONE batch
-    (8 x 7 = 56 rows) for its 8 chunks across the RelPE wrap -- the LayerNorm-on-load q|k|v / FFN-up GEMMs at four row
-    blocks (k_gemm_ln<*, 4, 8, *>) reading the fp32 fragment-order residual stream (XPack32), the packed out / FFN-down
-    inputs, the subsampling output linear (19,456 x 1024) on the split-K X-stationary stream (k_gemm_xsk) -- every
-    session's rows against the reference's per-session output (launch counters assert those kernels ran).  Then the
-    same 8-session stage as the captured EncoderGraph the duplex tick replays, on 8 fresh sessions: bit-identical to
-    the eager batch (same kernels, same order)."""
+    (8 x 7 = 56 rows) for its 8 chunks across the RelPE wrap.  fused 2 (default): the LayerNorm-on-load q|k|v GEMM
+    reading the fp32 fragment-order residual stream (XPack32), then attention + linear_out + residual in one
+    fo_enc_attn_out launch, the LayerNorm-on-load FFN-up GEMM at four row blocks (k_gemm_ln<*, 4, 8, *>) reading its
+    row sums; fused 1: the whole attention half as one fo_enc_attn_block launch; 0: the LayerNorm-on-load q|k|v /
+    FFN-up GEMMs on XPack32, the rel-pos attention writing the packed out input.  Both: the packed FFN-down input, the
+    subsampling output linear (19,456 x 1024) on the split-K X-stationary stream (k_gemm_xsk) -- every session's rows
+    against the reference's per-session output (launch counters assert which kernels ran).  Then the same 8-session
+    stage as the captured EncoderGraph the duplex tick replays, on 8 fresh sessions: bit-identical to the eager batch
+    (same kernels, same order)."""
     from types import SimpleNamespace
 
     from fo import ops
@@ -239,6 +243,8 @@ def test_real_geometry_batched_framing_b_encoder_matches_reference(dev):
     g = load("real_encoder_t2.npz")
     src = _t2_source(dev, {**encoder_shapes(T2, "user"), **adapter_shapes(T2, "user")})
     enc = SpeechEncoderEngine(src, T2, "user", dev, max_sessions=16)
+    assert enc.fused_block, "real geometry (d 1024, 16 heads of 64) takes fo_enc_attn_block"
+    enc.fused_block = fused
     ada = AdapterEngine(src, T2, "user", dev, max_sessions=16)
     B = 8
     feats = g["B_feats"]
@@ -254,8 +260,15 @@ def test_real_geometry_batched_framing_b_encoder_matches_reference(dev):
         assert T == 7 and To == 4 and out.shape[0] == B * T
         assert pes == [int(g["B_pe"][i])] * B
         nb = len(enc.layers)
-        assert c["gemm_ln"] == 2 * nb - 1 and c["gemm_xp32"] == 2 * nb - 1, c   # block 0's q|k|v takes the LN launch
-        assert c["gemm_xsk"] >= 1 and c["relpos"] == nb and c["attn_opack"] == nb, c
+        if fused == 2:
+            assert c["enc_block"] == nb and c["gemm_ln"] == 2 * nb - 1 and c["relpos"] == 0, c
+            assert c["gemm_xp32"] == nb - 1, c
+        elif fused == 1:
+            assert c["enc_block"] == nb and c["gemm_ln"] == nb and c["relpos"] == 0 and c["gemm_xp32"] == 0, c
+        else:   # block 0's q|k|v takes the LayerNorm launch
+            assert c["gemm_ln"] == 2 * nb - 1 and c["gemm_xp32"] == 2 * nb - 1, c
+            assert c["relpos"] == nb and c["attn_opack"] == nb and c["enc_block"] == 0, c
+        assert c["gemm_xsk"] >= 1, c
         ref_e, ref_a = g["B_enc"][i], g["B_ada"][i]
         for b in range(B):
             close(out[b * T:(b + 1) * T], ref_e, rtol=2e-3, atol=2e-3 * float(np.abs(ref_e).max()))

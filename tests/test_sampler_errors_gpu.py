@@ -69,3 +69,41 @@ def test_speech_decode_raises_on_nan_logits(dev):
     finally:
         b[3] = keep
     assert eng.tts.pool.pages_in_use() == 0
+
+
+def test_default_check_is_per_thread_and_dies_with_it(dev):
+    """ops.sample_check (the check a sampler call uses when it passes none) is thread-local: a NaN row drawn on one
+    thread raises in that thread's check only, and a thread that ends takes its check (and pinned word) with it --
+    a later thread starts from a fresh, cleared word."""
+    import gc
+    import threading
+    import weakref
+
+    from fo import ops
+    V = 1028
+    lg = torch.randn(1, V, device=dev)
+    lg[0, 3] = float("nan")
+    out = torch.empty(1, dtype=torch.int32, device=dev)
+    seen = {}
+
+    def worker():
+        chk = ops.sample_check(dev)
+        assert ops.sample_check(dev) is chk
+        seen["ref"] = weakref.ref(chk)
+        seen["id"] = id(chk)
+        ops.sample(lg, V, out, torch.ones(1, dtype=torch.int32, device=dev))
+        torch.cuda.synchronize()
+        seen["flagged"] = int(chk.buf.np[0, 0]) != 0   # left unread: it must not leak into another thread
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join()
+    gc.collect()
+    assert seen["flagged"]
+    assert seen["ref"]() is None, "a finished thread's default check is released"
+    mine = ops.sample_check(dev)
+    mine.check()   # this thread never drew the NaN row: no error
+    t2 = threading.Thread(target=lambda: seen.update(fresh=ops.sample_check(dev).buf.np[0, 0] == 0))
+    t2.start()
+    t2.join()
+    assert seen["fresh"]
