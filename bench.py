@@ -783,7 +783,7 @@ def recorded_kernel_avg_us(kernel_regex):
 
 def gemm_probe(engine, M, reps=2):
     """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the X-stationary
-    k_gemm_xs<8,14> launch of every layer) with HIP events on the launching stream.
+    k_gemm_xs<16,7> launch of every layer) with HIP events on the launching stream.
     The launches walk all layers' gate/up weights in order, as a chunk step does, so no launch finds
     its weights in the Infinity Cache from the previous one (273 MB per layer > 256 MB MALL)."""
     import torch
@@ -1180,7 +1180,7 @@ def main():
                          "frac": round(probe["gbps"] / peak, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
-                         "kernel": "k_gemm_xs<8,14> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all "
+                         "kernel": "k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all "
                                    "28 layers in turn)",
                          "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2),
                          "frac_source": "live: HIP events around every layer's gate/up launch on the engine stream "

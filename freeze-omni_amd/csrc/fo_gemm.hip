@@ -1031,7 +1031,9 @@ void launch_nw(int nw, bool wstream, bool x_f32, dim3 grid, const GemmArgs& a, h
 //    buffered -- the next unit's loads are issued right after the MFMAs that free a buffer;
 //  * per unit the NW partial tiles are reduced through LDS (two barriers), then the epilogue of the
 //    row-major output (the post-scaled RMSNorm and SwiGLU) as in gemm_body.
-constexpr int XS_NW = 8, XS_KPW = 14;
+// 16 waves x 7 k-steps (round 5, scripts/xs_variant_probe.py: 47.0-47.3 us per 271.6 MB launch against 48.6-49.5 us
+// for round 4's 8 x 14, graph-replayed over cold weight copies); FO_XS_VARIANT=3 runs the 8 x 14 shape
+constexpr int XS_NW = 16, XS_KPW = 7;
 // VAR (probes, fo_gemm_set_xs_variant): bit 0 = no cross-wave reduction (wave 0's partial is stored: WRONG
 // results, the barrier-free bound), bit 1 = default cache policy on the weight loads instead of nt, bit 2 = the
 // cross-wave reduction without workgroup barriers: per-unit partial slots double-buffered by unit parity, an LDS
@@ -1200,6 +1202,164 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
       if (rr < a.M && n < a.N) epilogue_store(a, true, rr, n, x1, x2);
     }
   }
+}
+
+// ---- probe (verdict r04 item 4: where a persistent layer would win or lose): the o -> gate/up seam of a Qwen2 layer
+// at <= 16 rows as ONE launch.  Workgroups [0, n_o) are the o projection (one tile pair each, 8 waves x 14 k-steps
+// over K = 3584, + residual, writing Y, yg = Y * gamma_next and the row's sum of squares per pair), then publish
+// (release fence + relaxed add on `ready`); workgroups [n_o, n_o + G) are k_gemm_xs's gate/up stream: they issue
+// their first two tiles' weights, then wave 0 polls `ready` (acquire; a bounded poll: past ~0.1 s the launch
+// proceeds and flags *ready_timeout, so a broken producer cannot hang the GPU), then the X slice (yg) and the rstd
+// from the o workgroups' partials, and the unit loop.  The dispatcher places workgroups in id order, so every o
+// workgroup is resident before any gate/up workgroup waits, and none of them waits on anything: the poll always ends.
+// Per-workgroup wall clocks (trc[4 w + 0..3]: start, weights of the first units issued / o reduced, ready seen /
+// o stored, end).  Same math as the two launches (o reduced in a different K order: ~1 ulp differences).
+__global__ __launch_bounds__(512) void k_seam_o_gu(GemmArgs ao, GemmArgs ag, int n_o, int units, int G, int* ready,
+                                                   int* ready_timeout, unsigned long long* trc) {
+  constexpr int NW = 8, KPW = 14, KS = NW * KPW;
+  __shared__ bf16x8 xlo[NW][KPW][64];
+  __shared__ float part[NW][2][16][17];
+  __shared__ float rstd_s[16];
+  __shared__ float rs_s[16][2];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wg = blockIdx.x;
+  unsigned long long* tr = trc ? trc + (size_t)wg * 4 : nullptr;
+  if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
+  const bool is_o = wg < n_o;
+  const GemmArgs& a = is_o ? ao : ag;
+  const unsigned long long wbase = (unsigned long long)a.Wp;
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(wbase >> 32)) << 32) |
+                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)wbase)),
+      (short)0, __builtin_amdgcn_readfirstlane(a.ntiles * KS * 1024), 0x00020000);
+  const int voff = (wave * KPW * 64 + lane) * 16;
+  bf16x8 w0[KPW], w1[KPW];
+  auto issue = [&](bf16x8 (&w)[KPW], int tile) {
+#pragma unroll
+    for (int j = 0; j < KPW; ++j)
+      w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, (tile * KS + j) * 1024, 2));
+  };
+  const int gj = wg - n_o;
+  const int ub = is_o ? wg : (int)((long)units * gj / G);
+  const int ue = is_o ? wg + 1 : (int)((long)units * (gj + 1) / G);
+  issue(w0, ub < ue ? 2 * ub : a.ntiles);
+  issue(w1, ub < ue ? 2 * ub + 1 : a.ntiles);
+  if (!is_o) {   // wait for every o workgroup's stores (bounded)
+    if (threadIdx.x == 0) {
+      long spins = 0;
+      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n_o) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1l << 22)) {
+          *ready_timeout = 1;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (tr) tr[2] = wall_clock64();
+    }
+    __syncthreads();
+  }
+  // X slice of this wave's k-steps (o: the attention output; gate/up: yg), hi in VGPRs, lo in LDS
+  bf16x8 xh[KPW];
+  {
+    const int row = min(lane & 15, a.M - 1);
+    const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4) + (size_t)wave * KPW * 32;
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      const float4 p0 = reinterpret_cast<const float4*>(xp + j * 32)[0];
+      const float4 p1 = reinterpret_cast<const float4*>(xp + j * 32)[1];
+      const float f[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+      bf16x8 lo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const __bf16 h = (__bf16)f[i];
+        xh[j][i] = h;
+        lo[i] = (__bf16)(f[i] - (float)h);
+      }
+      xlo[wave][j][lane] = lo;
+    }
+  }
+  if (!is_o) {   // rstd of each row from the o workgroups' partial sums of squares
+    for (int rr = wave; rr < 16; rr += NW) {
+      const int m = min(rr, a.M - 1);
+      float v = 0.f;
+      for (int j = lane; j < a.rgroups; j += 64) v += a.rstats[(size_t)m * a.rgroups + j];
+      v = wave_sum(v);
+      if (lane == 0) rstd_s[rr] = rsqrtf(v / (float)a.K + a.reps);
+    }
+  }
+  auto compute = [&](bf16x8 (&w)[KPW]) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[j], w[j], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xlo[wave][j][lane], w[j], acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  for (int u = ub; u < ue; ++u) {
+    const int nxt = u + 1 < ue ? 2 * (u + 1) : a.ntiles;
+    const f32x4 c0 = compute(w0);
+    issue(w0, nxt);
+    const f32x4 c1 = compute(w1);
+    issue(w1, nxt + (u + 1 < ue ? 1 : 0));
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      part[wave][0][4 * (lane >> 4) + i][lane & 15] = c0[i];
+      part[wave][1][4 * (lane >> 4) + i][lane & 15] = c1[i];
+    }
+    __syncthreads();
+    if (is_o && tr && threadIdx.x == 0) tr[1] = wall_clock64();
+    const int e = threadIdx.x;
+    if (e < 512) {
+      const int t = e >> 8, rr = (e >> 4) & 15, c = e & 15;   // o: both tiles of the pair; gate/up: the SwiGLU pair
+      float x1 = 0.f, x2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        x1 += part[w][is_o ? t : 0][rr][c];
+        x2 += part[w][1][rr][c];
+      }
+      if (is_o) {
+        const int n = (2 * u + t) * 16 + c;
+        float y = 0.f;
+        if (rr < a.M && n < a.N) {
+          const size_t o = (size_t)rr * a.ldy + n;
+          y = x1 + (a.bias ? a.bias[n] : 0.f) + reinterpret_cast<float*>(a.Y)[o];
+          reinterpret_cast<float*>(a.Y)[o] = y;
+          a.yg[o] = y * a.gnext[n];
+        }
+        // the row's sum of squares over this pair's 32 columns: 16 lanes of each tile's row, then the two tiles
+        float q = y * y;
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) q += __shfl_xor(q, off, 16);
+        if (c == 0) rs_s[rr][t] = q;
+      } else if (e < 256) {
+        if (a.rstats) {
+          x1 *= rstd_s[rr];
+          x2 *= rstd_s[rr];
+        }
+        const int n = u * 16 + c;
+        if (rr < a.M && n < a.N) epilogue_store(a, true, rr, n, x1, x2);
+      }
+    }
+    if (is_o) {
+      __syncthreads();
+      if (threadIdx.x < 16 && (int)threadIdx.x < a.M)
+        a.sout[(size_t)threadIdx.x * n_o + wg] = rs_s[threadIdx.x][0] + rs_s[threadIdx.x][1];
+    }
+  }
+  if (is_o) {   // publish
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (tr) tr[2] = wall_clock64();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (tr && threadIdx.x == 0) tr[3] = wall_clock64();
 }
 
 // X-stationary weight stream for 17..64 fp32 rows (RB = 2..4 row blocks): k_gemm_xs's design with the K range
@@ -1566,8 +1726,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     switch (xs_variant()) {
       case 1: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 1>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
       case 2: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 2>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
-      case 3: hipLaunchKernelGGL((k_gemm_xs<16, 7>), dim3(G), dim3(16 * 64), 0, stream, a, units); break;
-      case 4: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW, 4>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units); break;
+      case 3: hipLaunchKernelGGL((k_gemm_xs<8, 14>), dim3(G), dim3(8 * 64), 0, stream, a, units); break;
+      case 4: hipLaunchKernelGGL((k_gemm_xs<8, 14, 4>), dim3(G), dim3(8 * 64), 0, stream, a, units); break;
       default: hipLaunchKernelGGL((k_gemm_xs<XS_NW, XS_KPW>), dim3(G), dim3(XS_NW * 64), 0, stream, a, units);
     }
     fo::count_launch(FO_L_GEMM_XS);
@@ -1911,10 +2071,37 @@ int fo_gemm_set_merge(int on) {
 
 int fo_gemm_set_xs_variant(int v) {
   FO_REQUIRE(v >= 0 && v <= 4, "fo_gemm_set_xs_variant: 0 (shipped), 1 (no reduction: wrong results), 2 (default "
-             "cache policy), 3 (16 waves x 7 k-steps), 4 (barrier-free reduction)");
+             "cache policy), 3 (round 4's 8 waves x 14 k-steps), 4 (8 x 14, barrier-free reduction)");
   const int prev = xs_variant();
   g_xs_var = v;
   return prev;
+}
+
+int fo_probe_seam(const float* xo, int M, const void* wo, const float* bo, float* x, const float* gnext, float* yg,
+                  float* sout, const void* wgu, int n_gu_out, float* h, float eps, int* ready, int* ready_timeout,
+                  void* trace, int mode, hipStream_t s) {
+  // mode 0: the seam launch (o + gate/up); 1: its o workgroups alone; 2: its gate/up workgroups alone (ready must
+  // already hold n_o)
+  constexpr int K = 3584, NO = 3584;
+  FO_REQUIRE(M >= 1 && M <= 16 && n_gu_out % 16 == 0 && mode >= 0 && mode <= 2 && ready && ready_timeout,
+             "fo_probe_seam: M=%d (1..16), gate/up outputs %d (a multiple of 16), mode %d", M, n_gu_out, mode);
+  GemmArgs ao{};
+  ao.X = xo; ao.Wp = reinterpret_cast<const bf16_t*>(wo); ao.bias = bo; ao.Y = x; ao.ldx = K; ao.ldy = NO;
+  ao.M = M; ao.K = K; ao.N = NO; ao.ntiles = NO / 16; ao.S = 1; ao.residual = 1; ao.gnext = gnext; ao.yg = yg;
+  ao.sout = sout;
+  GemmArgs ag{};
+  ag.X = yg; ag.Wp = reinterpret_cast<const bf16_t*>(wgu); ag.Y = h; ag.ldx = NO; ag.ldy = n_gu_out; ag.M = M;
+  ag.K = K; ag.N = n_gu_out; ag.ntiles = 2 * n_gu_out / 16; ag.S = 1; ag.rstats = sout; ag.rgroups = NO / 32;
+  ag.reps = eps;
+  const int n_o = NO / 32, units = n_gu_out / 16;
+  const int per = (units + num_cus() - 1) / num_cus(), G = (units + per - 1) / per;
+  unsigned long long* trc = reinterpret_cast<unsigned long long*>(trace);
+  if (mode == 0) hipLaunchKernelGGL(k_seam_o_gu, dim3(n_o + G), dim3(512), 0, s, ao, ag, n_o, units, G, ready,
+                                    ready_timeout, trc);
+  else if (mode == 1) hipLaunchKernelGGL(k_seam_o_gu, dim3(n_o), dim3(512), 0, s, ao, ag, n_o, units, G, ready,
+                                         ready_timeout, trc);
+  else hipLaunchKernelGGL(k_seam_o_gu, dim3(G), dim3(512), 0, s, ao, ag, 0, units, G, ready, ready_timeout, trc);
+  return fo::check_launch("fo_probe_seam");
 }
 
 int fo_gemm_set_trace(void* trace) {

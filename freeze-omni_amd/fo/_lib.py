@@ -77,6 +77,8 @@ _SIGS = {
                                   c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fo_enc_attn_out": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
                                 c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "fo_probe_seam": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_float, c_vp,
+                              c_vp, c_vp, c_int, c_vp]),
     "fo_subsample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_ll, c_vp]),
     "fo_pack_weight_elems": (c_ll, [c_int, c_int]),

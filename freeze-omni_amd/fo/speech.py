@@ -23,9 +23,9 @@ from . import ops, tables
 from .ops import F32, I32, PackedLinear
 
 # the encoder block's attention half: FO_ENC_BLOCK=0 three launches (LayerNorm-on-load q|k|v GEMM, rel-pos attention,
-# out GEMM + reduce); 1 one launch (fo_enc_attn_block: LayerNorm1 + q|k|v + attention + out + residual); 2 (default)
+# out GEMM + reduce; the default); 1 one launch (fo_enc_attn_block: LayerNorm1 + q|k|v + attention + out + residual); 2
 # the q|k|v GEMM, then attention + out + residual in one launch (fo_enc_attn_out)
-ENC_BLOCK = int(os.environ.get("FO_ENC_BLOCK", "2") or 0)
+ENC_BLOCK = int(os.environ.get("FO_ENC_BLOCK", "0") or 0)
 
 FRAMINGS = {
     # name: (chunk_frames, carried_frames, win, shift, nfft, scale)
@@ -170,8 +170,8 @@ class SpeechEncoderEngine:
         self.vr = torch.zeros_like(self.kr)
         self.slots = SlotPool(max_sessions)
         # the attention half of each block as one launch (fo_enc_attn_block) where the geometry fits it
-        self.fused_block = (ENC_BLOCK if self.dk == 64 and self.d % 256 == 0 and self.d <= 1024
-                            and self.cap + 8 <= 96 else 0)
+        self.block_fusable = self.dk == 64 and self.d % 256 == 0 and self.d <= 1024 and self.cap + 8 <= 96
+        self.fused_block = ENC_BLOCK if self.block_fusable else 0
 
     @property
     def weight_bytes(self):

@@ -90,8 +90,17 @@ int fo_gemm_set_u(int u);
  * previous setting. */
 int fo_gemm_set_xs(int on);
 /* probe hook: variant of the k_gemm_xs launch (0 shipped; 1 no cross-wave reduction -- WRONG results, a timing
- * bound; 2 default-policy weight loads; 3 16 waves x 7 k-steps).  Process-global; returns the previous one. */
+ * bound; 2 default-policy weight loads; 3 round 4's 8 waves x 14 k-steps; 4 8 x 14 with the barrier-free
+ * reduction).  Process-global; returns the previous one. */
 int fo_gemm_set_xs_variant(int v);
+/* probe (scripts/seam_probe.py): the Qwen2 o -> gate/up seam at <= 16 rows as one launch (k_seam_o_gu); xo [M][3584]
+ * attention output, wo / wgu packed o and SwiGLU-paired gate/up weights, x the residual stream (updated), yg / sout the
+ * next norm's input and partial sums of squares ([M][112]), h the SwiGLU output [M][n_gu_out]; ready: a zeroed int
+ * (left at 112), ready_timeout set when the bounded poll gave up; trace: 4 wall clocks per workgroup or NULL; mode 0
+ * the seam, 1 its o workgroups alone, 2 its gate/up workgroups alone. */
+int fo_probe_seam(const float* xo, int M, const void* wo, const float* bo, float* x, const float* gnext, float* yg,
+                  float* sout, const void* wgu, int n_gu_out, float* h, float eps, int* ready, int* ready_timeout,
+                  void* trace, int mode, hipStream_t s);
 /* Split-K of the one-row-tile plain GEMMs (Qwen2 / TTS down, encoder FFN w2) merged inside the launch:
  * each split stores its partial tile write-through and takes the tile's ticket in `counters` (zeroed
  * ints, left zeroed); the last split sums every partial in split order (k_gemm_reduce's order, bit for

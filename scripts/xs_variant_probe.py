@@ -1,8 +1,9 @@
 """Where does the X-stationary gate/up stream (k_gemm_xs, M = 16, K = 3584, the dominant kernel) lose against the
 lm_head's 6.4 TB/s?  Graph-replayed over weight copies beyond the Infinity Cache (as xs_balance_probe.py), the
 shipped kernel against probe variants (fo_gemm_set_xs_variant): 1 = no cross-wave LDS reduction (wrong results: the
-bound of removing the two barriers per unit), 2 = default-policy (not nt) weight loads, 3 = 16 waves x 7 k-steps, 4 = the
-cross-wave reduction without workgroup barriers (the last-arriving wave reduces; bit-identical to the shipped kernel).
+bound of removing the two barriers per unit), 2 = default-policy (not nt) weight loads, 3 = round 4's 8 waves x 14
+k-steps (shipped until r05; the shipped shape is 16 x 7 since), 4 = 8 x 14 with the cross-wave reduction without
+workgroup barriers (the last-arriving wave reduces; bit-identical to 8 x 14).
 Also the Qwen2 lm_head (1.09 GB) for the achievable streaming rate.  python scripts/xs_variant_probe.py (GPU)."""
 import os
 import sys
@@ -25,10 +26,10 @@ outs = [torch.empty(M, I, device=dev) for _ in range(copies)]
 nbytes = 2 * I * D * 2
 ref = lins[0](x, M=M).clone()
 for rnd in range(2):
-    for var, name in ((0, "shipped <8,14>"), (1, "no reduction (bound)"), (2, "default-policy loads"),
-                      (3, "16 waves x 7"), (4, "barrier-free reduction")):
+    for var, name in ((0, "shipped <16,7>"), (1, "no reduction (bound)"), (2, "default-policy loads"),
+                      (3, "8 waves x 14 (r04)"), (4, "8 x 14 barrier-free")):
         lib.fo_gemm_set_xs_variant(var)
-        if var not in (1, 3):   # (3 sums 16 wave partials: another rounding order)
+        if var in (0, 2):   # (3 / 4 sum 8 wave partials: another rounding order; 1 is wrong by design)
             y = lins[0](x, M=M)
             torch.cuda.synchronize()
             assert torch.equal(y, ref), f"variant {var} differs from the shipped kernel"

@@ -226,11 +226,11 @@ def test_real_geometry_encoder_adapter_match_reference(dev):
 @pytest.mark.parametrize("fused", [2, 1, 0])
 def test_real_geometry_batched_framing_b_encoder_matches_reference(dev, fused):
     """The duplex tick's encoder shape at real geometry: 8 copies of real_encoder_t2's framing-B session in ONE batch
-    (8 x 7 = 56 rows) for its 8 chunks across the RelPE wrap.  fused 2 (default): the LayerNorm-on-load q|k|v GEMM
+    (8 x 7 = 56 rows) for its 8 chunks across the RelPE wrap.  fused 2: the LayerNorm-on-load q|k|v GEMM
     reading the fp32 fragment-order residual stream (XPack32), then attention + linear_out + residual in one
     fo_enc_attn_out launch, the LayerNorm-on-load FFN-up GEMM at four row blocks (k_gemm_ln<*, 4, 8, *>) reading its
     row sums; fused 1: the whole attention half as one fo_enc_attn_block launch; 0: the LayerNorm-on-load q|k|v /
-    FFN-up GEMMs on XPack32, the rel-pos attention writing the packed out input.  Both: the packed FFN-down input, the
+    FFN-up GEMMs on XPack32, the rel-pos attention writing the packed out input (the default).  All three: the packed FFN-down input, the
     subsampling output linear (19,456 x 1024) on the split-K X-stationary stream (k_gemm_xsk) -- every session's rows
     against the reference's per-session output (launch counters assert which kernels ran).  Then the same 8-session
     stage as the captured EncoderGraph the duplex tick replays, on 8 fresh sessions: bit-identical to the eager batch
@@ -243,7 +243,7 @@ def test_real_geometry_batched_framing_b_encoder_matches_reference(dev, fused):
     g = load("real_encoder_t2.npz")
     src = _t2_source(dev, {**encoder_shapes(T2, "user"), **adapter_shapes(T2, "user")})
     enc = SpeechEncoderEngine(src, T2, "user", dev, max_sessions=16)
-    assert enc.fused_block, "real geometry (d 1024, 16 heads of 64) takes fo_enc_attn_block"
+    assert enc.block_fusable, "real geometry (d 1024, 16 heads of 64) fits fo_enc_attn_block / fo_enc_attn_out"
     enc.fused_block = fused
     ada = AdapterEngine(src, T2, "user", dev, max_sessions=16)
     B = 8
