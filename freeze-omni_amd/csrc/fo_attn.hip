@@ -58,9 +58,9 @@ __global__ __launch_bounds__(256) void k_rope_kv_write(const float* qkv, int ldq
 
 #include "fo_attn_rows.h"
 
-template <int HD, int NW = 4>
+template <int HD, int NW = 4, int RT = 1>
 __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
-  attn_rows_body<HD, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  attn_rows_body<HD, NW, RT>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Single-row decode attention (the AR speech decoder's step, models/decoder/decoder.py:341-349: one
@@ -542,6 +542,8 @@ inline int attn_waves() {
   }
   return g_attn_nw;
 }
+// query rows one attention work item may carry (fo_attn_max_rows): 32 on the 8-wave head-dim-128 kernel
+inline int attn_max_rows(int hd) { return hd == 128 && attn_waves() == 8 ? 32 : 16; }
 
 // fo_attention_set_opack: the next launch's packed output and its extent (columns, allocated row blocks)
 thread_local uint16_t* g_oph = nullptr;
@@ -592,6 +594,8 @@ int fo_attention_o(const float* q, int T, const int* items, const int* tok_nvis,
   return fo::check_launch("fo_attention_o");
 }
 
+int fo_attn_max_rows(int hd) { return attn_max_rows(hd); }
+
 int fo_attn_nsplit(int max_keys, int n_items, int KVH) {
   // enough work groups to cover the chip (~2 per CU) while every split keeps >= one 64-key tile
   const int by_keys = (max_keys + KT - 1) / KT;
@@ -633,7 +637,11 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
              H * hd, T);
   FO_REQUIRE(items || T % n_items == 0, "fo_attention: items NULL needs T / n_items tokens per item");
   FO_REQUIRE(hd == 32 || hd == 64 || hd == 128, "fo_attention: head_dim %d unsupported", hd);
-  FO_REQUIRE(max_rows >= 1 && max_rows <= 16, "fo_attention: %d query rows per item (max 16)", max_rows);
+  // up to 32 query rows per item on the 8-wave head-dim-128 kernel (two row tiles share every K / V load: a duplex
+  // tick's 4 tokens x 7 query heads per kv head read the session's keys once, not twice), 16 elsewhere
+  const int rows_max = attn_max_rows(hd);
+  FO_REQUIRE(max_rows >= 1 && max_rows <= rows_max, "fo_attention: %d query rows per item (max %d)", max_rows,
+             rows_max);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
@@ -651,7 +659,8 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
     return fo::check_launch("fo_attention/decode");
   }
   dim3 grid(n_items, KVH, nsplit);
-  if (hd == 128 && attn_waves() == 8) hipLaunchKernelGGL((k_attn_mfma<128, 8>), grid, dim3(512), 0, s, a);
+  if (hd == 128 && attn_waves() == 8 && max_rows > 16) hipLaunchKernelGGL((k_attn_mfma<128, 8, 2>), grid, dim3(512), 0, s, a);
+  else if (hd == 128 && attn_waves() == 8) hipLaunchKernelGGL((k_attn_mfma<128, 8>), grid, dim3(512), 0, s, a);
   else if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
   else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_attn_mfma<32>), grid, dim3(256), 0, s, a);

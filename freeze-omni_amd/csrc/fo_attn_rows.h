@@ -164,7 +164,7 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
 // while the current tile computes.  Every fp32 operand is split into bf16 hi + lo and each product
 // uses three MFMAs (hi*hi + hi*lo + lo*hi), so scores and outputs keep ~fp32 accuracy.  Online
 // softmax per row with the running max exchanged across the 4 waves through LDS.
-template <int HD, int NW>
+template <int HD, int NW, int RT = 1>   // RT: 16-row query tiles per item (2: up to 32 rows share the K / V loads)
 __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, const int kvh, const int sp) {
   constexpr int KT = 16 * NW;           // keys per tile: one 16-key column block per wave
   constexpr int NTH = NW * 64;
@@ -174,29 +174,33 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   constexpr int VP = HD + 2;             // V row pitch: the 4 key groups of a B fragment hit distinct banks
   constexpr int VL = KT * HD / 4 / NTH;  // float4 of V per thread per tile
   __shared__ float v_s[KT][VP];
-  __shared__ float p_s[16][KT + 4];
-  __shared__ float mx_s[NW][16];
-  __shared__ float l_s[NW][16];
-  __shared__ int nvis_s[16];
+  __shared__ float p_s[16 * RT][KT + 4];
+  __shared__ float mx_s[NW][16 * RT];
+  __shared__ float l_s[NW][16 * RT];
+  __shared__ int nvis_s[16 * RT];
+  // RT > 1: the Q fragments live in LDS (every wave uses the same ones; in registers they would spill)
+  constexpr bool QL = RT > 1;
+  __shared__ bf16x8 qf_s[QL ? RT : 1][QL ? DC : 1][2][64];
   __shared__ int pg_s[MAXPG];
 
   // items NULL: a uniform batch (tnu tokens per sequence, in sequence order) -- no item-table round trip
   const int seq = a.items ? a.items[3 * it] : it, t0 = a.items ? a.items[3 * it + 1] : it * a.tnu;
   const int tn = a.items ? a.items[3 * it + 2] : a.tnu;
   const int G = a.H / a.KVH;
-  const int R = tn * G;  // <= 16
+  const int R = tn * G;  // <= 16 RT
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = lane >> 4, col = lane & 15;
   const int* bt = a.block_table + (size_t)seq * a.maxb;
   // this lane's q row slices, requested before anything that waits (they depend only on t0)
-  float4 qraw[2 * DC];
-  {
-    const int r = col < R ? col : R - 1;
+  float4 qraw[RT][2 * DC];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int r = min(16 * rt + col, R - 1);
     const float* qr = a.q + ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * HD + 8 * grp;
 #pragma unroll
     for (int c = 0; c < DC; ++c) {
-      qraw[2 * c] = *reinterpret_cast<const float4*>(qr + 32 * c);
-      qraw[2 * c + 1] = *reinterpret_cast<const float4*>(qr + 32 * c + 4);
+      qraw[rt][2 * c] = *reinterpret_cast<const float4*>(qr + 32 * c);
+      qraw[rt][2 * c + 1] = *reinterpret_cast<const float4*>(qr + 32 * c + 4);
     }
   }
   // a block-table row that fits is staged whole, requested together with the key counts (no wait for
@@ -251,20 +255,30 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   const int pb = whole ? 0 : pb0;  // pg_s holds pages pb..
   if (!whole)
     for (int i = tid; i < npg; i += NTH) pg_s[i] = bt[pb + i];
-  if (tid < 16) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
+  if (tid < 16 * RT) nvis_s[tid] = tid < R ? a.tok_nvis[t0 + tid / G] : 0;
 
   // Q as A fragments: row = col (lane & 15), d = 32 c + 8 grp; rows >= R are zero
-  bf16x8 qh[DC], ql[DC];
-  {
+  bf16x8 qh[QL ? 1 : RT][DC], ql[QL ? 1 : RT][DC];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
     for (int c = 0; c < DC; ++c) {
       float f[8];
-      const float4 x0 = qraw[2 * c];
-      const float4 x1 = qraw[2 * c + 1];
-      const float sc = col < R ? a.scale : 0.f;
+      const float4 x0 = qraw[rt][2 * c];
+      const float4 x1 = qraw[rt][2 * c + 1];
+      const float sc = 16 * rt + col < R ? a.scale : 0.f;
       f[0] = x0.x * sc; f[1] = x0.y * sc; f[2] = x0.z * sc; f[3] = x0.w * sc;
       f[4] = x1.x * sc; f[5] = x1.y * sc; f[6] = x1.z * sc; f[7] = x1.w * sc;
-      split8(f, qh[c], ql[c]);
+      if constexpr (QL) {
+        bf16x8 h, l;
+        split8(f, h, l);
+        if (wave == 0) {
+          qf_s[rt][c][0][lane] = h;
+          qf_s[rt][c][1][lane] = l;
+        }
+      } else {
+        split8(f, qh[rt][c], ql[rt][c]);
+      }
     }
   }
   __syncthreads();  // pg_s, nvis_s
@@ -290,12 +304,15 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
     }                                                                                                     \
   }
 
-  float m_run[4], l_lane[4];
-  f32x4 acc[NTW];
+  float m_run[RT][4], l_lane[RT][4];
+  f32x4 acc[RT][NTW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { m_run[i] = -INFINITY; l_lane[i] = 0.f; }
+  for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
-  for (int n = 0; n < NTW; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) { m_run[rt][i] = -INFINITY; l_lane[rt][i] = 0.f; }
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc[rt][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   // tile t's loads are issued while tile t - 1 computes and two tiles are in flight from the start, so a
   // 256-key split waits for one round of memory, not two
@@ -317,56 +334,71 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
       split8(f, kh[c], kl[c]);
     }
     if (k0 + 2 * KT < c1) FO_ATTN_LOAD(kreg, vreg, k0 + 2 * KT)
-    // S[r = 4 grp + i][key = k0 + 16 wave + col]
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    // S[r = 16 rt + 4 grp + i][key = k0 + 16 wave + col]
+    f32x4 s[RT];
 #pragma unroll
-    for (int c = 0; c < DC; ++c) {
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[c], kh[c], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qh[c], kl[c], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ql[c], kh[c], s, 0, 0, 0);
+    for (int rt = 0; rt < RT; ++rt) {
+      s[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < DC; ++c) {
+        const bf16x8 qhv = QL ? qf_s[QL ? rt : 0][QL ? c : 0][0][lane] : qh[QL ? 0 : rt][c];
+        const bf16x8 qlv = QL ? qf_s[QL ? rt : 0][QL ? c : 0][1][lane] : ql[QL ? 0 : rt][c];
+        s[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qhv, kh[c], s[rt], 0, 0, 0);
+        s[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qhv, kl[c], s[rt], 0, 0, 0);
+        s[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qlv, kh[c], s[rt], 0, 0, 0);
+      }
     }
     const int key = k0 + 16 * wave + col;
-    bool valid[4];
-    float mw[4];
+    bool valid[RT][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      valid[i] = key < c1 && key < nvis_s[4 * grp + i];
-      mw[i] = row16_max(valid[i] ? s[i] : -INFINITY);
-    }
-    if (col == 0) {
+    for (int rt = 0; rt < RT; ++rt) {
+      float mw[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) mx_s[wave][4 * grp + i] = mw[i];
+      for (int i = 0; i < 4; ++i) {
+        valid[rt][i] = key < c1 && key < nvis_s[16 * rt + 4 * grp + i];
+        mw[i] = row16_max(valid[rt][i] ? s[rt][i] : -INFINITY);
+      }
+      if (col == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx_s[wave][16 * rt + 4 * grp + i] = mw[i];
+      }
     }
     __syncthreads();
-    float alpha[4];
+    float alpha[RT][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * grp + i;
-      float tm = mx_s[0][r];
+    for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
-      for (int w = 1; w < NW; ++w) tm = fmaxf(tm, mx_s[w][r]);
-      const float mn = fmaxf(m_run[i], tm);
-      alpha[i] = (m_run[i] == mn) ? 1.f : expf(m_run[i] - mn);
-      m_run[i] = mn;
-      const float p = valid[i] ? expf(s[i] - mn) : 0.f;
-      l_lane[i] = l_lane[i] * alpha[i] + p;
-      p_s[r][16 * wave + col] = p;
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * rt + 4 * grp + i;
+        float tm = mx_s[0][r];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) tm = fmaxf(tm, mx_s[w][r]);
+        const float mn = fmaxf(m_run[rt][i], tm);
+        alpha[rt][i] = (m_run[rt][i] == mn) ? 1.f : expf(m_run[rt][i] - mn);
+        m_run[rt][i] = mn;
+        const float p = valid[rt][i] ? expf(s[rt][i] - mn) : 0.f;
+        l_lane[rt][i] = l_lane[rt][i] * alpha[rt][i] + p;
+        p_s[r][16 * wave + col] = p;
+      }
     }
     __syncthreads();  // p_s and v_s complete
-    // O[r][d] += P[r][:] V[:][d] for this wave's d tiles
+    // O[r][d] += P[r][:] V[:][d] for this wave's d tiles (one V fragment split serves every row tile)
 #pragma unroll
-    for (int n = 0; n < NTW; ++n) {
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[n][i] *= alpha[i];
-    }
+      for (int n = 0; n < NTW; ++n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[rt][n][i] *= alpha[rt][i];
+      }
 #pragma unroll
     for (int kc = 0; kc < KT / 32; ++kc) {
-      bf16x8 ph, pl;
-      {
-        const float4 x0 = *reinterpret_cast<const float4*>(&p_s[col][32 * kc + 8 * grp]);
-        const float4 x1 = *reinterpret_cast<const float4*>(&p_s[col][32 * kc + 8 * grp + 4]);
+      bf16x8 ph[RT], pl[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const float4 x0 = *reinterpret_cast<const float4*>(&p_s[16 * rt + col][32 * kc + 8 * grp]);
+        const float4 x1 = *reinterpret_cast<const float4*>(&p_s[16 * rt + col][32 * kc + 8 * grp + 4]);
         const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        split8(f, ph, pl);
+        split8(f, ph[rt], pl[rt]);
       }
 #pragma unroll
       for (int n = 0; n < NTW; ++n) {
@@ -377,9 +409,12 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
           for (int e = 0; e < 8; ++e) f[e] = v_s[32 * kc + 8 * grp + e][16 * dt + col];
           bf16x8 vh, vl;
           split8(f, vh, vl);
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vh, acc[n], 0, 0, 0);
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph, vl, acc[n], 0, 0, 0);
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vh, acc[n], 0, 0, 0);
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[rt], vh, acc[rt][n], 0, 0, 0);
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[rt], vl, acc[rt][n], 0, 0, 0);
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl[rt], vh, acc[rt][n], 0, 0, 0);
+          }
         }
       }
     }
@@ -389,18 +424,23 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
     if (k0 + KT < c1) tile(kB, vB, k0 + KT);
   }
 #undef FO_ATTN_LOAD
-  // row sums: 16 lanes of the row group, then the 4 waves
-  float lw[4];
+  // row sums: 16 lanes of the row group, then the waves
 #pragma unroll
-  for (int i = 0; i < 4; ++i) lw[i] = row16_sum(l_lane[i]);
-  if (col == 0) {
+  for (int rt = 0; rt < RT; ++rt) {
+    float lw[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) l_s[wave][4 * grp + i] = lw[i];
+    for (int i = 0; i < 4; ++i) lw[i] = row16_sum(l_lane[rt][i]);
+    if (col == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) l_s[wave][16 * rt + 4 * grp + i] = lw[i];
+    }
   }
   __syncthreads();
 #pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int r = 4 * grp + i;
+    const int r = 16 * rt + 4 * grp + i;
     if (r >= R) continue;
     float l = l_s[0][r];
 #pragma unroll
@@ -412,14 +452,14 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
       if (dt >= NTILE) continue;
       const int d = 16 * dt + col;
       if (ns == 1) {
-        a.out[th * HD + d] = acc[n][i] / l;
-        if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, acc[n][i] / l, a.prb);
+        a.out[th * HD + d] = acc[rt][n][i] / l;
+        if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, acc[rt][n][i] / l, a.prb);
       } else {
-        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[n][i];
+        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[rt][n][i];
       }
     }
     if (ns > 1 && wave == 0 && col == 0) {
-      a.part_ml[(th * a.nsplit + sp) * 2] = m_run[i];
+      a.part_ml[(th * a.nsplit + sp) * 2] = m_run[rt][i];
       a.part_ml[(th * a.nsplit + sp) * 2 + 1] = l;
     }
   }

@@ -1512,6 +1512,11 @@ inline bool xs_mode() {
   }
   return g_xs == 1;
 }
+// weights of at least this many MiB take the 17..64-row split-K stream (fo_gemm_set_xsk_min_mb: probes)
+int g_xsk_min_mb = [] {
+  const char* e = getenv("FO_XSK_MIN_MB");
+  return e ? atoi(e) : 128;
+}();
 int g_xsk = -1;  // X-stationary split-K kernel for eligible 17..64-row GEMMs: -1 = FO_GEMM_XSK (default on)
 inline bool xsk_mode() {
   if (g_xsk < 0) {
@@ -1740,7 +1745,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   // output linear, 19,456 x 1024 = 40 MB: 48.8 us per chunk on the split-K grid kernel, r04i); on the 26-33 MB
   // q|k|v / o the one-row-tile kernels below are faster (r04d probe: o 14.8 vs 18.5 us, q|k|v 19.2 vs 24.4 us at 32 rows)
   const long long wbytes0 = (long long)a.ntiles * 16 * K * 2;
-  const bool big_w0 = wbytes0 >= (128ll << 20) || (K >= 8192 && wbytes0 >= (32ll << 20));
+  const bool big_w0 = wbytes0 >= ((long long)g_xsk_min_mb << 20) || (K >= 8192 && wbytes0 >= (32ll << 20));
   if (x_f32 && M > 16 && M <= 64 && !lnw && (a.ntiles % 2) == 0 && splitk <= 1 && xsk_mode() && !g_force_nt &&
       !g_force_nw && big_w0 && ldx % 4 == 0 && !sout1 && (K >> 5) >= 56) {
     const int RBk = (M + 15) / 16;
@@ -2055,6 +2060,13 @@ int fo_gemm_set_pipe(int on) {
 
 // X-stationary kernel switch for the eligible M <= 16 GEMMs (k_gemm_xs): 0 off, 1 on.  Process-global
 // (sweeps, A/B); returns the previous setting.  Unset, FO_GEMM_XS (default on) decides.
+int fo_gemm_set_xsk_min_mb(int mb) {
+  FO_REQUIRE(mb >= 0, "fo_gemm_set_xsk_min_mb: %d", mb);
+  const int prev = g_xsk_min_mb;
+  g_xsk_min_mb = mb;
+  return prev;
+}
+
 int fo_gemm_set_xs(int on) {
   FO_REQUIRE(on == 0 || on == 1, "fo_gemm_set_xs: 0 or 1");
   const int prev = xs_mode() ? 1 : 0;

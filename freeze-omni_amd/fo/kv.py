@@ -174,10 +174,11 @@ class BatchMeta:
 
     entries: list of (KVSeq, n_new, rope_pos_start, causal).  Reserves KV for the new tokens and
     advances each sequence's length.  gqa = query heads per kv head of the stack that consumes it:
-    attention work items hold up to 16 // gqa tokens of one sequence (fo_attention: 16 query rows).
+    attention work items hold up to rows // gqa tokens of one sequence (rows: query rows per item, at most
+    ops.attn_max_rows(head_dim) -- 32 on the Qwen2 kernel, 16 otherwise; the stacks use ops.attn_item_rows).
     """
 
-    def __init__(self, entries, device, gqa=1):
+    def __init__(self, entries, device, gqa=1, rows=16):
         T = sum(n for _, n, _, _ in entries)
         tok_seq = np.empty(T, np.int32)
         tok_pos = np.empty(T, np.int32)
@@ -212,7 +213,7 @@ class BatchMeta:
         bt = np.zeros((len(entries), maxb), np.int32)
         for s, (seq, _, _, _) in enumerate(entries):
             bt[s, :len(seq.pages)] = seq.pages
-        tpi = max(1, 16 // gqa)
+        tpi = max(1, rows // gqa)
         items = []
         t = 0
         for s, (seq, n, _, _) in enumerate(entries):

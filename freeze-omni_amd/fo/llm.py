@@ -51,7 +51,8 @@ class LLMEngine:
     def forward(self, x, entries):
         """x: fp32 [T, D] input embeds (already rounded to fp16 values, models/audioLLM.py:338,410);
         entries: list of (KVSeq, n_tokens).  Returns (final-normed hidden [T, D], BatchMeta)."""
-        meta = BatchMeta([(s, n, s.length, True) for s, n in entries], self.device, gqa=self.H // self.KVH)
+        meta = BatchMeta([(s, n, s.length, True) for s, n in entries], self.device, gqa=self.H // self.KVH,
+                         rows=ops.attn_item_rows(self.hd))
         self.stack.forward(x, meta)
         ops.rmsnorm(x, self.norm, self.eps, out=x)
         return x, meta

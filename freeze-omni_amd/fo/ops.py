@@ -522,6 +522,23 @@ def scale_(x, s):
     return x
 
 
+# FO_ATTN_ROWS=32: the Qwen2 prefills cut into work items of up to 32 query rows (4 tokens x 7 heads sharing one K / V
+# read, k_attn_mfma<128, 8, 2>) instead of 16 -- measured on the duplex line (r05j, two rounds of 30 s): p50 decision
+# 7.96 / 7.85 ms against 7.91 / 7.71 with 16-row items (half the work items, each with twice the MFMA and softmax work
+# per key, one workgroup per CU at 103 KB of LDS), so 16 stays the policy (A/B only)
+ATTN_ROWS32 = os.environ.get("FO_ATTN_ROWS") == "32"
+
+
+def attn_max_rows(hd):
+    """Query rows (tokens x query heads per kv head) one fo_attention work item may carry (the kernels' limit)."""
+    return _lib.load().fo_attn_max_rows(int(hd))
+
+
+def attn_item_rows(hd):
+    """Query rows per work item the stacks cut their batches into (the policy, <= attn_max_rows)."""
+    return attn_max_rows(hd) if ATTN_ROWS32 else 16
+
+
 def attn_nsplit(max_keys, n_items, KVH):
     return _lib.load().fo_attn_nsplit(int(max_keys), int(n_items), int(KVH))
 

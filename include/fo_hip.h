@@ -93,6 +93,9 @@ int fo_gemm_set_xs(int on);
  * bound; 2 default-policy weight loads; 3 round 4's 8 waves x 14 k-steps; 4 8 x 14 with the barrier-free
  * reduction).  Process-global; returns the previous one. */
 int fo_gemm_set_xs_variant(int v);
+/* probe hook: the weight size (MiB) from which 17..64-row fp32 GEMMs take k_gemm_xsk (default 128; long-K >= 32 MiB
+ * layers always).  Process-global; returns the previous value. */
+int fo_gemm_set_xsk_min_mb(int mb);
 /* probe (scripts/seam_probe.py): the Qwen2 o -> gate/up seam at <= 16 rows as one launch (k_seam_o_gu); xo [M][3584]
  * attention output, wo / wgu packed o and SwiGLU-paired gate/up weights, x the residual stream (updated), yg / sout the
  * next norm's input and partial sums of squares ([M][112]), h the SwiGLU output [M][n_gu_out]; ready: a zeroed int
@@ -215,6 +218,9 @@ int fo_record_ids(const int* ids, int B, int* dst, int ld, const int* row, hipSt
 
 /* ---------------------------------------------------------------- attention (fo_attn.hip) */
 /* number of key splits for fo_attention: ~2 work groups per CU, >= 64 keys per split, <= 32 */
+/* query rows (tokens x query heads per kv head) one work item of fo_attention may carry for head size hd: 32 on the
+ * 8-wave head-dim-128 kernel (two 16-row tiles sharing the K / V loads), else 16. */
+int fo_attn_max_rows(int hd);
 int fo_attn_nsplit(int max_keys, int n_items, int KVH);
 /* RoPE (rotate_half, host cos/sin tables) + paged KV append: transformers apply_rotary_pos_emb +
  * DynamicCache.update (models/audioLLM.py:416-419, models/decoder/decoder.py:146,305) */

@@ -20,6 +20,7 @@
 #   ddp1       bench.py as one torch.distributed.run rank (world 1: RCCL init, broadcast, checksum) -> <tag>_ddp1.json
 #   n2guard    bench.py --gpus 2 on this 1-GPU box must refuse without touching the GPU
 #   ab         ENV_A / ENV_B (e.g. 'FO_X=0') alternated twice on the quick bench -> <tag>_ab.txt
+#   abdup      DUP_SET='A=1|B=2|' settings, two rounds on a 30 s duplex line -> <tag>_abdup.txt
 #   sweep      SWEEP='A=1|B=2|' settings ('|'-separated, empty = default), two rounds on the quick bench -> <tag>_sweep.txt
 #   py:<script args>   any scripts/ probe, e.g. 'py:llm_stage_time.py' (200 s limit)
 set -o pipefail
@@ -95,6 +96,13 @@ for S in "$@"; do
                > ${O}_ab_$AB$i.log 2>&1 || { rc=$?; tail -20 ${O}_ab_$AB$i.log; break 2; }
              echo "$AB$i [${!E}] $(line ${O}_ab_$AB$i.log)" >> ${O}_ab.txt; rc=0
            done; done; cat ${O}_ab.txt ;;
+    abdup) : > ${O}_abdup.txt   # the same alternation on the duplex line (SWEEP-style settings in DUP_SET='A|B|C')
+           IFS='|' read -ra SET <<< "$DUP_SET"; rc=0
+           for i in 1 2; do for k in "${!SET[@]}"; do
+             timeout -k 10 300 env ${SET[$k]} python -u bench.py --scenario duplex --duplex-sec 30 \
+               > ${O}_abdup_$k$i.log 2>&1 || { rc=$?; tail -20 ${O}_abdup_$k$i.log; break 2; }
+             echo "$i [${SET[$k]:-default}] $(line ${O}_abdup_$k$i.log)" >> ${O}_abdup.txt
+           done; done; cat ${O}_abdup.txt ;;
     sweep) : > ${O}_sweep.txt   # SWEEP='A=1|B=2 C=3|' : each setting (empty = default) on the quick bench, two rounds
            IFS='|' read -ra SET <<< "$SWEEP"; rc=0
            for i in 1 2; do for k in "${!SET[@]}"; do
