@@ -1512,6 +1512,11 @@ inline bool xs_mode() {
   }
   return g_xs == 1;
 }
+// 65..128-row GEMMs on the split-K weight streams as two row halves (FO_GEMM_ROW_SPLIT=0: the 64-row tile kernels)
+const bool g_row_split = [] {
+  const char* e = getenv("FO_GEMM_ROW_SPLIT");
+  return !(e && e[0] == '0');
+}();
 // weights of at least this many MiB take the 17..64-row split-K stream (fo_gemm_set_xsk_min_mb: probes)
 int g_xsk_min_mb = [] {
   const char* e = getenv("FO_XSK_MIN_MB");
@@ -1644,6 +1649,39 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   FO_REQUIRE(ldy >= N, "fo_gemm: ldy=%d < N=%d", ldy, N);
   FO_REQUIRE(!(swiglu && (bias || scale)), "fo_gemm: swiglu with bias/affine unsupported");
   FO_REQUIRE(!scale == !shift, "fo_gemm: scale and shift go together");
+  // 65..128 rows on the large weight streams (a duplex tick whose sessions start a turn: the 5-token chat prefix on
+  // top of the 4 chunk rows; 8 x 9 = 72 rows): two X-stationary split-K launches on the two row halves (33..64 rows
+  // each) instead of 64-row tiles, which stream the whole weight once per row tile at ~1.4-2.5 TB/s (r05i duplex
+  // table: gate/up 193.8 us, down 110.4 us per layer at 72 rows).  Both halves take k_gemm_xsk, so their row
+  // statistics have the same group count ((N + 255) / 256) and the halves' rows tile the [M][groups] layout.
+  {
+    const long long wb = (long long)(swiglu ? 2 : 1) * ((N + 15) / 16) * 16 * K * 2;
+    const bool big = wb >= ((long long)g_xsk_min_mb << 20) || (K >= 8192 && wb >= (32ll << 20));
+    // (and the plain >= 8 MB projections -- the Qwen2 o: 57.0 us on 64-row tiles at 72 rows -- whose halves take
+    // the one-row-tile split-K kernels + k_gemm_reduce, the same statistics groups)
+    const bool mid_w = !swiglu && wb >= (8ll << 20);
+    if (M > 64 && M <= 128 && x_f32 && !lnw && !rope && !sout1 && !rstats1 && splitk <= 1 && (big || mid_w) &&
+        xsk_mode() && !g_force_nt && !g_force_nw && !xpk.p0 && !ypk.p0 && !yp32k.p0 && !xp32k.p0 && (K >> 5) >= 56 &&
+        (ldx % 4) == 0 && ((swiglu ? 2 : 1) * ((N + 15) / 16)) % 2 == 0 && g_row_split) {
+      const int M0 = (M + 1) / 2, grp = (N + 255) / 256;
+      int sg = 0;
+      for (int h = 0; h < 2; ++h) {
+        const int r0 = h ? M0 : 0, Mh = h ? M - M0 : M0;
+        const size_t yb = (size_t)r0 * ldy * (out_bf16 ? 2 : 4);
+        int sgh = 0;
+        const int rc = gemm_impl(static_cast<const char*>(X) + (size_t)r0 * ldx * 4, x_f32, ldx, Mh, K, Wp, N, swiglu,
+                                 bias, scale, shift, static_cast<char*>(Y) + yb, ldy, out_bf16, act, residual, ws,
+                                 ws_floats, counters, splitk, rstats ? rstats + (size_t)r0 * rgroups : nullptr, rgroups,
+                                 reps, sout ? sout + (size_t)r0 * grp : nullptr, gnext,
+                                 yg ? yg + (size_t)r0 * ldy : nullptr, &sgh, nullptr, stream);
+        if (rc) return rc;
+        FO_REQUIRE(!sout || sgh == grp, "fo_gemm: row halves wrote %d statistics groups, expected %d", sgh, grp);
+        sg = sgh;
+      }
+      if (sgroups) *sgroups = sg;
+      return 0;
+    }
+  }
   GemmArgs a;
   a.X = X;
   a.scale = scale;

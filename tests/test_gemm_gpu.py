@@ -119,6 +119,42 @@ def test_gemm_mid_rows(dev, M, N, K, sw):
         assert torch.equal(out2.cpu().double(), y)
 
 
+@pytest.mark.parametrize("M", [65, 72, 128])
+@pytest.mark.parametrize("producer", ["down", "o"])
+def test_gemm_row_halves_on_qwen2_streams(dev, M, producer):
+    """65..128 rows on the Qwen2 down (136 MB) or o (26 MB) projection (residual + the next RMSNorm's statistics) and
+    the gate/up (272 MB, SwiGLU + the RMSNorm consumer): each as two launches on the row halves (a duplex tick with
+    chat prefixes; k_gemm_xsk for down and gate/up, the one-row-tile split-K kernels for o), whose statistics groups
+    tile one [M][groups] layout; vs an fp64 residual -> RMSNorm -> SwiGLU reference."""
+    from fo import ops
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M)
+    D, I = 3584, 18944 if producer == "down" else 3584
+    wd = (torch.randn(D, I, generator=g) / I ** 0.5).to(torch.bfloat16)
+    wg = (torch.randn(18944, D, generator=g) / D ** 0.5).to(torch.bfloat16)
+    wu = (torch.randn(18944, D, generator=g) / D ** 0.5).to(torch.bfloat16)
+    gamma = torch.rand(D, generator=g) + 0.5
+    hin = torch.randn(M, I, generator=g)
+    res = torch.randn(M, D, generator=g)
+    down, gu = PackedLinear(wd.to(dev)), PackedLinear(wg.to(dev), swiglu_up=wu.to(dev))
+    st = ops.RowStats(M, dev)
+    x = res.clone().to(dev)
+    yg = torch.empty(M, D, device=dev)
+    ops.launch_counts_reset()
+    down(hin.to(dev), out=x, residual=True, stats_out=st.set(gamma.to(dev), yg))
+    out = gu(yg, norm=(st, 1e-6))
+    torch.cuda.synchronize()
+    c = ops.launch_counts()
+    assert c["gemm_xsk"] == (4 if producer == "down" else 2), c   # two row halves per GEMM
+    assert c["gemm_reduce"] == 4, c
+    y = res.double() + hin.double() @ wd.double().t()
+    torch.testing.assert_close(x.cpu().double(), y, rtol=1e-5, atol=1e-4)
+    h = y * torch.rsqrt((y * y).mean(-1, keepdim=True) + 1e-6) * gamma.double()
+    ref = torch.nn.functional.silu(h @ wg.double().t()) * (h @ wu.double().t())
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err < 2e-4 * ref.abs().max().item(), err
+
+
 @pytest.mark.parametrize("M", [8, 16, 40, 56])
 @pytest.mark.parametrize("sw", [False, True])
 def test_gemm_rmsnorm_across_gemms(dev, M, sw):
