@@ -542,6 +542,8 @@ inline int attn_waves() {
   }
   return g_attn_nw;
 }
+thread_local unsigned long long* g_attn_trc = nullptr;   // fo_attention_set_trace (probes)
+
 // query rows one attention work item may carry (fo_attn_max_rows): 32 on the 8-wave head-dim-128 kernel
 inline int attn_max_rows(int hd) { return hd == 128 && attn_waves() == 8 ? 32 : 16; }
 
@@ -596,6 +598,11 @@ int fo_attention_o(const float* q, int T, const int* items, const int* tok_nvis,
 
 int fo_attn_max_rows(int hd) { return attn_max_rows(hd); }
 
+int fo_attention_set_trace(void* trace) {
+  g_attn_trc = reinterpret_cast<unsigned long long*>(trace);
+  return 0;
+}
+
 int fo_attn_nsplit(int max_keys, int n_items, int KVH) {
   // enough work groups to cover the chip (~2 per CU) while every split keeps >= one 64-key tile
   const int by_keys = (max_keys + KT - 1) / KT;
@@ -645,7 +652,7 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
-             tickets, keys_per_split, items ? 1 : T / n_items, oph, opl, (T + 15) / 16};
+             tickets, keys_per_split, items ? 1 : T / n_items, oph, opl, (T + 15) / 16, g_attn_trc};
   const bool dec = max_rows == 1 && (long long)maxb * PS <= DEC_MAXK;
   FO_REQUIRE(!a.oph || (T <= 64 && (dec || nsplit == 1 || tickets)),
              "fo_attention: packed output needs <= 64 tokens and no combine launch");

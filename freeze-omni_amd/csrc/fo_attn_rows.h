@@ -25,6 +25,7 @@ struct AttnArgs {
   uint16_t* oph;
   uint16_t* opl;
   int prb;         // its row blocks: ceil(T / 16)
+  unsigned long long* trc;   // probes (fo_attention_set_trace): per workgroup {start, staged, tiles done, stored, end}
 };
 
 constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
@@ -191,6 +192,9 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = lane >> 4, col = lane & 15;
   const int* bt = a.block_table + (size_t)seq * a.maxb;
+  unsigned long long* const tr =
+      a.trc ? a.trc + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+  if (tr && tid == 0) tr[0] = wall_clock64();
   // this lane's q row slices, requested before anything that waits (they depend only on t0)
   float4 qraw[RT][2 * DC];
 #pragma unroll
@@ -282,6 +286,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
     }
   }
   __syncthreads();  // pg_s, nvis_s
+  if (tr && tid == 0) tr[1] = wall_clock64();
 
   const size_t head_off = (size_t)kvh * a.PS * HD;
   const size_t page_sz = (size_t)a.KVH * a.PS * HD;
@@ -424,6 +429,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
     if (k0 + KT < c1) tile(kB, vB, k0 + KT);
   }
 #undef FO_ATTN_LOAD
+  if (tr && tid == 0) tr[2] = wall_clock64();
   // row sums: 16 lanes of the row group, then the waves
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
@@ -463,6 +469,11 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
       a.part_ml[(th * a.nsplit + sp) * 2 + 1] = l;
     }
   }
+  if (tr && tid == 0) tr[3] = wall_clock64();
   if (a.cnt && ns > 1) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
+  if (tr && tid == 0) {
+    tr[4] = wall_clock64();
+    tr[5] = 1 + (unsigned long long)ns;   // (nonzero: this workgroup ran the tile loop)
+  }
 }
 

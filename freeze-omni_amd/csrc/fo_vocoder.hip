@@ -49,6 +49,7 @@ constexpr int CONV_MAXG = 5;
 struct ConvMulti {
   ConvArgs a[CONV_MAXG];
   int B, G, sum;
+  unsigned long long* trc;   // probes (fo_conv_set_trace): per workgroup {start, stage cycles, compute cycles, end}
 };
 
 constexpr int CONV_KMAX = 11;
@@ -79,6 +80,10 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
   for (int m = 0; m < MTW; ++m)
 #pragma unroll
     for (int n = 0; n < NTW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  unsigned long long* const tr =
+      mc.trc ? mc.trc + 4 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+  unsigned long long t_stage = 0, t_comp = 0;
+  if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
 
   const int tl = wave * 16 * NTW + (lane & 15);  // this lane's time row (tile n adds 16 n)
   const int kq = 8 * (lane >> 4);                 // this lane's 8-wide K slice inside a step
@@ -154,8 +159,14 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
     };
     const int nchunks = a.Cin / CK;
     for (int c = 0; c < nchunks; ++c) {
+      const unsigned long long c0 = tr ? clock64() : 0;
       stage(c);
+      const unsigned long long c1 = tr ? clock64() : 0;
       for (int s = 0; s < a.nks_c; ++s) comp(s);
+      if (tr) {
+        t_stage += c1 - c0;
+        t_comp += clock64() - c1;
+      }
     }
   }
   // C layout: row (output channel) = 4*(lane>>4) + i, column (time) = lane & 15.  Every epilogue
@@ -202,6 +213,10 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
       }
     }
   }
+  if (tr && threadIdx.x == 0) {
+    tr[1] = t_stage;
+    tr[2] = t_comp;
+  }
   float4 gg[MTW];
 #pragma unroll
   for (int m = 0; m < MTW; ++m) {
@@ -221,6 +236,7 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
       *reinterpret_cast<float4*>(a.out + off[n] + m * 16) = v;
     }
   }
+  if (tr && threadIdx.x == 0) tr[3] = wall_clock64();
 }
 
 // One ResBlock1 step with both of its convolutions in one workgroup (models/decoder/ticodec/models.py:90-110):
@@ -608,7 +624,10 @@ static int conv_check(const ConvArgs& a) {
 }
 
 // One launch of mc.G convolutions (all Cin -> Cout); Tq_max: the longest output range among them.
+thread_local unsigned long long* g_conv_trc = nullptr;   // fo_conv_set_trace (probes)
+
 static int conv_launch(ConvMulti& mc, int Tq_max, hipStream_t s) {
+  mc.trc = g_conv_trc;
   const int B = mc.B, Cin = mc.a[0].Cin, Cout = mc.a[0].Cout;
   const int CK = pick_ck(Cin);
   const int zg = mc.sum ? 1 : mc.G;
@@ -725,6 +744,11 @@ int fo_conv_pair_multi(const FoPairDesc* d, int G, int B, int C, int T, int sum,
     hipLaunchKernelGGL((k_conv_pair<4, 2, 32>), dim3((T + 127) / 128, 1, B * zg), dim3(256), 0, s, pm);
   }
   return fo::check_launch("fo_conv_pair_multi");
+}
+
+int fo_conv_set_trace(void* trace) {
+  g_conv_trc = reinterpret_cast<unsigned long long*>(trace);
+  return 0;
 }
 
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s) {

@@ -70,7 +70,7 @@ int fo_gemm_qkv_rope(const void* X, int x_f32, int ldx, int M, int K, const void
                      float* kc, float* vc, int H, int KVH, int hd, int PS, hipStream_t stream);
 /* Linear layer with the preceding LayerNorm applied to X as it is loaded (a speech-encoder block's
  * pre-norm + projection: norm1 -> linear_q/k/v and norm2 -> feed_forward.w_1,
- * models/encoder/transformer.py:103-130): Y = act(LN(X; lnw, lnb, eps) W^T + bias), X fp32, M <= 32.
+ * models/encoder/transformer.py:103-130): Y = act(LN(X; lnw, lnb, eps) W^T + bias), X fp32, M <= 64.
  * Row mean / variance come from the producer GEMM's partial sums (fo_gemm_rowstats): rsum / rsumsq
  * [M][rgroups]. */
 int fo_gemm_ln(const float* X, int ldx, int M, int K, const void* Wp, int N, const float* bias, const float* lnw,
@@ -221,6 +221,9 @@ int fo_record_ids(const int* ids, int B, int* dst, int ld, const int* row, hipSt
 /* query rows (tokens x query heads per kv head) one work item of fo_attention may carry for head size hd: 32 on the
  * 8-wave head-dim-128 kernel (two 16-row tiles sharing the K / V loads), else 16. */
 int fo_attn_max_rows(int hd);
+/* probe hook: per-workgroup wall clocks of the following multi-row fo_attention launches on this thread (8 slots a
+ * workgroup in linear block order: start, staged, tile loop done, partials stored, end, 1 + splits); NULL stops. */
+int fo_attention_set_trace(void* trace);
 int fo_attn_nsplit(int max_keys, int n_items, int KVH);
 /* RoPE (rotate_half, host cos/sin tables) + paged KV append: transformers apply_rotary_pos_emb +
  * DynamicCache.update (models/audioLLM.py:416-419, models/decoder/decoder.py:146,305) */
@@ -355,6 +358,9 @@ typedef struct FoPairDesc {
 int fo_conv_pair_multi(const FoPairDesc* descs, int G, int B, int C, int T, int sum, float slope, float oscale,
                        const float* gadd, hipStream_t s);
 /* Quantizer.embed (models/decoder/ticodec/models.py:661-700), channel-last output */
+/* probe hook: per-workgroup clocks of the following k_conv_cl launches on this thread ({wall start, stage cycles,
+ * compute cycles, wall end} x workgroups, linear block order); NULL stops. */
+int fo_conv_set_trace(void* trace);
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 /* xs / num_kernels (+ global feature, models.py:233-238), channel-last */
 int fo_scale_add_cl(float* y, int B, int T, int C, float sc, const float* g, hipStream_t s);
