@@ -166,18 +166,50 @@ __global__ void k_conv_cache_update(float* cache, const int* slots, const float*
 
 // Dialog-state head (models/audioLLM.py:486-493,521-524): logits = W h + b over 4 classes for the
 // selected row of each sequence; softmax over classes 0..2; writes probs[s][0..2].
-__global__ __launch_bounds__(256) void k_state_head(const float* h, int ldh, const int* rows, const float* W,
-                                                    const float* bias, int D, float* probs) {
-  __shared__ float red[4];
+// One pass over the row for all three logits, 1024 threads, every load of a 4096-wide slab issued before its use
+// (the row and the three weight rows are cold: a dependent load chain per element was the launch's whole time).
+__global__ __launch_bounds__(1024) void k_state_head(const float* h, int ldh, const int* rows, const float* W,
+                                                     const float* bias, int D, float* probs) {
+  __shared__ float red[3][16];
   const float* x = h + (size_t)rows[blockIdx.x] * ldh;
-  float lg[3];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int base = 0; base < D; base += 4096) {
+    float xv[4], w0[4], w1[4], w2[4];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < D; i += 256) s += x[i] * W[(size_t)c * D + i];
-    lg[c] = block_sum<4>(s, red) + bias[c];
+    for (int k = 0; k < 4; ++k) {
+      const int i = base + k * 1024 + (int)threadIdx.x;
+      const bool ok = i < D;
+      xv[k] = ok ? x[i] : 0.f;
+      w0[k] = ok ? W[i] : 0.f;
+      w1[k] = ok ? W[(size_t)D + i] : 0.f;
+      w2[k] = ok ? W[2 * (size_t)D + i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a0 += xv[k] * w0[k];
+      a1 += xv[k] * w1[k];
+      a2 += xv[k] * w2[k];
+    }
   }
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = a0;
+    red[1][w] = a1;
+    red[2][w] = a2;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    float lg[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float t = bias[c];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t += red[c][j];
+      lg[c] = t;
+    }
     const float m = fmaxf(lg[0], fmaxf(lg[1], lg[2]));
     const float e0 = expf(lg[0] - m), e1 = expf(lg[1] - m), e2 = expf(lg[2] - m);
     const float z = e0 + e1 + e2;
@@ -275,7 +307,7 @@ int fo_conv_cache_update(float* cache, const int* slots, const float* x, int B, 
 int fo_state_head(const float* h, int ldh, const int* rows, int S, const float* W, const float* bias, int D,
                   float* probs, hipStream_t s) {
   FO_REQUIRE(S > 0, "fo_state_head: no rows");
-  hipLaunchKernelGGL(k_state_head, dim3(S), dim3(256), 0, s, h, ldh, rows, W, bias, D, probs);
+  hipLaunchKernelGGL(k_state_head, dim3(S), dim3(1024), 0, s, h, ldh, rows, W, bias, D, probs);
   return fo::check_launch("fo_state_head");
 }
 
