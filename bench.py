@@ -867,8 +867,11 @@ def run_duplex(eng, args, seconds, sync, probe=False):
                 s.enqueue_audio_data(ident, {"audio": chunks[u][k][ident], "sr": 16000, "enc": "s16le",
                                              "time_stamp": k * ch / 16000.0})
         if probe:
-            for s in sch.sessions:   # the host stages of tick() (VAD, gating + fbank, serialisation), timed apart
-                s.pump()
+            from fo.duplex import deliver_deferred
+            defer = []   # the host stages of tick() (VAD, gating + one fbank launch, serialisation), timed apart
+            for s in sch.sessions:
+                s.pump(defer)
+            deliver_deferred(defer)
             t_host = time.perf_counter()
             eng.stage_probe = []
         done = sch.tick()

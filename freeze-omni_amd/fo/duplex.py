@@ -19,6 +19,7 @@ installed): it labels chunks from a speech-interval schedule with the same outpu
 """
 import collections
 import copy
+import os
 
 import numpy as np
 import torch
@@ -221,9 +222,11 @@ class DuplexSession:
         self.raw[identity].append((audio, audio_data_dict["time_stamp"]))
 
     # ------------------------------------------------------------------ :405-684 as one synchronous pass
-    def pump(self):
+    def pump(self, defer=None):
         """Run VAD annotation and feature gating over every complete VAD chunk received so far; gated
-        features go to the context serializer."""
+        features go to the context serializer.  defer (a list): the gating of each chunk is queued there as
+        (session, identity, annotation, fbank request) instead, for DuplexScheduler.tick to compute every
+        session's fbank rows in one launch and deliver them in order (deliver_deferred)."""
         for ident in ("user", "system"):
             vad, n = self.vad[ident], self.vad[ident].get_chunk_size()
             while self.raw[ident]:
@@ -231,11 +234,11 @@ class DuplexSession:
                 buf = np.concatenate([self.pending[ident], audio])
                 self.pending_ts[ident] = ts
                 while buf.shape[0] >= n:
-                    self._annotate(ident, vad.predict({"audio": buf[:n], "time_stamp": ts}))
+                    self._annotate(ident, vad.predict({"audio": buf[:n], "time_stamp": ts}), defer)
                     buf = buf[n:]
                 self.pending[ident] = buf
 
-    def _annotate(self, ident, ann):
+    def _annotate(self, ident, ann, defer=None):
         status = ann["status"]
         if status == "ipu_sl":                                     # :484-526
             if self.current_ipu[ident] is not None:
@@ -265,7 +268,14 @@ class DuplexSession:
             ev.emit_vad_event(self.socketio, self.sid, status, ident)
             ev.emit_tm_audio_chunk(self.socketio, self.tm_sid, ident, status, ann["audio"], ann["time_stamp"],
                                    ann.get("cached_audio"))
-        gated = self.feature_gater[ident].process_and_gate(ann)
+        gater = self.feature_gater[ident]
+        if defer is not None and hasattr(gater, "prepare"):
+            defer.append((self, ident, ann, gater.prepare(ann)))
+            return
+        self._deliver(ident, ann, gater.process_and_gate(ann))
+
+    def _deliver(self, ident, ann, gated):
+        """Feature gating's output to the context serializer (:639-670)."""
         if not gated:
             return
         ser = self.context_serializer
@@ -319,6 +329,22 @@ class DuplexSession:
         return self.apply(data, self.pipeline.speech_dialogue(**self.request(data)))
 
 
+# every session's fbank rows of a tick in one launch (FO_DUPLEX_BATCH_FBANK=0: one launch per chunk, A/B only)
+BATCH_FBANK = os.environ.get("FO_DUPLEX_BATCH_FBANK", "1") != "0"
+
+
+def deliver_deferred(defer):
+    """Gate the chunks DuplexSession.pump(defer) queued: every session's fbank rows in one launch (sessions whose
+    gaters share a framing and device; models.AudioFeatureGating.fbank_batch), then each chunk finished and
+    delivered in queue order, which is chunk order within every session and identity."""
+    if not defer:
+        return
+    from models.AudioFeatureGating import fbank_batch
+    feats = fbank_batch([s.feature_gater[i] for s, i, _, _ in defer], [r for _, _, _, r in defer])
+    for (s, ident, ann, _), f in zip(defer, feats):
+        s._deliver(ident, ann, s.feature_gater[ident].finish(ann, f))
+
+
 class DuplexScheduler:
     """Every duplex session of one replica (one GPU).  tick(): pump each session, take at most one
     serialized feature per session, and prefill all of them with ONE speech_dialogue_batch call."""
@@ -332,9 +358,12 @@ class DuplexScheduler:
         return session
 
     def tick(self):
+        defer = [] if BATCH_FBANK else None
+        for s in self.sessions:
+            s.pump(defer)
+        deliver_deferred(defer)
         work = []
         for s in self.sessions:
-            s.pump()
             d = s.next_feature()
             if d is not None:
                 work.append((s, d))

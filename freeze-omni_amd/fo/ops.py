@@ -387,7 +387,12 @@ def h2d(a, device, dtype=None):
     if torch.cuda.is_current_stream_capturing():
         raise RuntimeError("ops.h2d inside a graph capture")
     p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-    p.copy_(t)
+    if t.dtype in (torch.float32, torch.int32, torch.int64, torch.float64) and t.is_contiguous():
+        # numpy's single-threaded copy: torch's copy_ of >= 32K elements fans out over the OpenMP pool, whose
+        # spinning threads, on a CPU-quota'd host, got the process throttled (~60 ms duplex ticks, r05z)
+        p.numpy()[...] = t.numpy()
+    else:
+        p.copy_(t)
     return p.to(device, non_blocking=True)
 
 

@@ -70,13 +70,40 @@ class FbankGPU:
         w, c, s, m = tables.kaldi_tables(wl, nfft)
         self.device = torch.device(device)
         self.window, self.tw_cos, self.tw_sin, self.mel = (t.to(self.device) for t in (w, c, s, m))
+        # pinned staging of the calls: a ring of 4 slots (grown on demand), each reused once its copy has run
+        self._pins, self._evs, self._k = [None] * 4, [None] * 4, 0
+
+    def _stage(self, host):
+        """host float32 [n] -> a new device tensor: through this object's own pinned ring and one async copy on the
+        current stream.  The batched duplex gating (one call for every session's chunk, ~0.25-0.5 MB) through
+        ops.h2d's per-call pinned blocks, copied by torch's OpenMP-parallel copy_, stalled a tick for ~60 ms every
+        few ticks (scripts/duplex_tick_probe.py).  A slot is rewritten four calls later, after its copy's event (long done: the listen pipelines keep at
+        most one chunk's fbank queued ahead)."""
+        n = host.shape[0]
+        if self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+            return ops.h2d(host, self.device)
+        k = self._k
+        self._k = (k + 1) % len(self._pins)
+        if self._evs[k] is not None:
+            self._evs[k].synchronize()
+        if self._pins[k] is None or self._pins[k].numel() < n:
+            self._pins[k] = torch.empty(max(n, 2 * (0 if self._pins[k] is None else self._pins[k].numel())),
+                                        dtype=F32, pin_memory=True)
+        pin = self._pins[k]
+        pin[:n].numpy()[:] = host   # (a numpy copy: torch's copy_ of >= 32K elements fans out over the OpenMP pool)
+        dev = torch.empty(n, dtype=F32, device=self.device)
+        dev.copy_(pin[:n], non_blocking=True)
+        if self._evs[k] is None:
+            self._evs[k] = torch.cuda.Event()
+        self._evs[k].record(torch.cuda.current_stream(self.device))
+        return dev
 
     def __call__(self, windows, firsts):
         """windows: np.float32 [B][n_samples]; firsts: list[bool] -> device feats [B, R, 80]."""
         B = len(firsts)
         host = np.concatenate([np.ascontiguousarray(windows, np.float32).reshape(-1),
                                np.asarray([self.ov if f else 0 for f in firsts], np.int32).view(np.float32)])
-        dev = ops.h2d(host, self.device)   # samples + the per-row zero-row counts (int32 bits), one async copy
+        dev = self._stage(host)   # samples + the per-row zero-row counts (int32 bits), one async copy
         samples = dev[:B * self.n_samples].view(B, self.n_samples)
         zero_rows = dev[B * self.n_samples:].view(I32)
         out = torch.empty(B, self.R * 80, dtype=F32, device=self.device)

@@ -55,8 +55,24 @@ class AudioFeatureGating:
         return self.fbank(w[None], [first])  # [1, R, 80] device
 
     def process_and_gate(self, annotated_audio):
+        return self.finish(annotated_audio, self.fbank(*self._one(self.prepare(annotated_audio))))
+
+    @staticmethod
+    def _one(req):
+        w, first = req
+        return w[None], [first]
+
+    # process_and_gate in two halves, so that a scheduler holding many gaters (fo.duplex.DuplexScheduler) frames
+    # every session's chunk first and computes all their fbank rows in one launch (fbank_batch)
+    def prepare(self, annotated_audio):
+        """Host half: push the chunk through the framer (the carried samples advance here).  Returns the fbank
+        request (window [n_samples] float32, first chunk?) that finish() consumes, in chunk order."""
+        return self.framer.push(np.asarray(annotated_audio["audio"], dtype=np.float32))
+
+    def finish(self, annotated_audio, feat):
+        """Device half: feat = this chunk's fbank rows [1, R, 80] (device) -> the gated output, or None outside
+        an IPU (the chunk then only enters the onset history)."""
         status = annotated_audio["status"]
-        feat = self._extract_fbank(annotated_audio["audio"])
         if status is None:
             if self.cache_history_size > 0:
                 self.history = torch.cat([self.history[1:], feat])
@@ -67,3 +83,15 @@ class AudioFeatureGating:
             last = self.history[-self.onset_input_chunk_cache_size:].unsqueeze(1)
             out["feature_last_chunk"] = last if self.as_tensor else last.cpu().numpy().tolist()
         return out
+
+
+def fbank_batch(gaters, requests):
+    """One fbank launch for chunks prepared by several gaters of the same framing and device (one row per
+    request; k_fbank computes every (row, frame) on its own, so each row equals its single-chunk launch).
+    Returns each request's [1, R, 80] device rows."""
+    g0 = gaters[0]
+    for g in gaters:
+        if g.kind != g0.kind or g.device != g0.device:
+            raise ValueError("fbank_batch: gaters of different framings or devices")
+    feats = g0.fbank(np.stack([w for w, _ in requests]), [f for _, f in requests])
+    return [feats[i:i + 1] for i in range(len(requests))]

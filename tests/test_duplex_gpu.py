@@ -191,3 +191,35 @@ def test_duplex_encoder_graph_and_two_streams_match_eager(pipe):
         eng.use_graphs = True
     assert with_graphs == eager
     assert any(x[0] == "system" for s, _, _ in with_graphs for x in s)   # both parties took part
+
+
+def test_batched_fbank_matches_single_chunk_gating(dev):
+    """DuplexScheduler.tick frames every session's chunk first and computes all their fbank rows in one launch
+    (AudioFeatureGating.prepare / fbank_batch / finish): each chunk's gated features, onset replay included, are
+    bit-identical to the one-chunk process_and_gate of an identical gater."""
+    import torch
+
+    from fo.duplex import DEFAULT_CONFIG
+    from models.AudioFeatureGating import AudioFeatureGating, fbank_batch
+    g = DEFAULT_CONFIG["audio_feature_gating"]
+    # (an onset replay of 6 chunks: the fork's config replays none)
+    mk = lambda: AudioFeatureGating(16000, g["feature_gating_history_size"], 6, g["fbank"], device="cuda:0",  # noqa: E731
+                                    as_tensor=True)
+    single, batched = [mk() for _ in range(3)], [mk() for _ in range(3)]
+    n = single[0].expected_frames_per_audio_chunk
+    statuses = [None, None, "ipu_sl", "ipu_cl", "ipu_el"]
+    for k, st in enumerate(statuses):
+        anns = [{"audio": _pcm(n, 100 * k + i).astype(np.float32), "status": st} for i in range(3)]
+        want = [gt.process_and_gate(a) for gt, a in zip(single, anns)]
+        reqs = [gt.prepare(a) for gt, a in zip(batched, anns)]
+        got = [gt.finish(a, f) for gt, a, f in zip(batched, anns, fbank_batch(batched, reqs))]
+        for w, o in zip(want, got):
+            if w is None:
+                assert o is None
+                continue
+            assert w["status"] == o["status"]
+            assert torch.equal(w["feature"], o["feature"])
+            if st == "ipu_sl":
+                assert torch.equal(w["feature_last_chunk"], o["feature_last_chunk"])
+    for a, b in zip(single, batched):
+        assert torch.equal(a.history, b.history)
