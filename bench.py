@@ -1047,6 +1047,11 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
+    if world > 1:
+        # N ranks on one node: no rank's host loop fans a large CPU tensor op over a 16-thread OpenMP pool (whose
+        # spinning threads, N times over, can exhaust a CPU quota and stall every rank's ticks: r05z); the engine's
+        # host code needs no intra-op parallelism (same rate at 1 thread at N = 1, profiles/r05zb_omp_threads_ab.txt)
+        torch.set_num_threads(1)
     dev = torch.device("cuda", local)
     from fo.engine import FreezeOmniEngine
     model_dir = os.path.join(ROOT, "configs", args.config)
