@@ -340,13 +340,17 @@ def deliver_deferred(defer):
     if not defer:
         return
     from models.AudioFeatureGating import fbank_batch
-    # the batch's rows grouped by identity (user rows, then system rows, each in queue order), so that one identity's
-    # features of the tick are adjacent rows of one tensor and its encoder stage takes them with one copy
-    order = sorted(range(len(defer)), key=lambda q: defer[q][1] != "user")
-    rows = fbank_batch([defer[q][0].feature_gater[defer[q][1]] for q in order], [defer[q][3] for q in order])
+    gaters = [s.feature_gater[i] for s, i, _, _ in defer]
+    # one launch per (framing, device) among the tick's gaters (one in practice); the batch's rows grouped by
+    # identity (user rows, then system rows, each in queue order), so that one identity's features of the tick are
+    # adjacent rows of one tensor and its encoder stage takes them with one copy
+    groups = {}
+    for q in sorted(range(len(defer)), key=lambda q: defer[q][1] != "user"):
+        groups.setdefault((gaters[q].kind, str(gaters[q].device)), []).append(q)
     feats = [None] * len(defer)
-    for q, f in zip(order, rows):
-        feats[q] = f
+    for order in groups.values():
+        for q, f in zip(order, fbank_batch([gaters[q] for q in order], [defer[q][3] for q in order])):
+            feats[q] = f
     for (s, ident, ann, _), f in zip(defer, feats):
         s._deliver(ident, ann, s.feature_gater[ident].finish(ann, f))
 
