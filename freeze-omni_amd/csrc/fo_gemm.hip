@@ -1522,6 +1522,14 @@ int g_xsk_min_mb = [] {
   const char* e = getenv("FO_XSK_MIN_MB");
   return e ? atoi(e) : 128;
 }();
+// 33..48-row split-K stream shape: 5 k-steps per wave and 2 units in flight (K split 3 ways on the Qwen2 gate/up
+// instead of 4, 15 on the down instead of 19: a quarter fewer partial-slab bytes); FO_XSK_RB3=4: the round-4 shape
+// (4 k-steps, 3 units).  Measured (scripts/gemm_mid_probe.py, profiles/r05ze_xsk_rb3_ab.txt): gate/up at 40 / 48
+// rows 73.0 / 74.8 -> 69.6 / 70.0 us, down 40.8 / 41.9 -> 38.9 / 40.3 us
+const int g_xsk_rb3 = [] {
+  const char* e = getenv("FO_XSK_RB3");
+  return e ? atoi(e) : 5;
+}();
 int g_xsk = -1;  // X-stationary split-K kernel for eligible 17..64-row GEMMs: -1 = FO_GEMM_XSK (default on)
 inline bool xsk_mode() {
   if (g_xsk < 0) {
@@ -1789,7 +1797,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     const int RBk = (M + 15) / 16;
     // 8 waves x KPW k-steps of X per split (hi in VGPRs, lo in LDS: KPW shrinks as the row blocks grow), UA units of
     // weights in flight per wave (~28 KiB, k_gemm_xs's depth); every split has work (K >= 56 k-steps)
-    const int NWk = 8, KPWk = RBk == 2 ? 7 : (RBk == 3 ? 4 : 3);
+    const int NWk = 8, KPWk = RBk == 2 ? 7 : (RBk == 3 ? (g_xsk_rb3 == 5 ? 5 : 4) : 3);
     const int KSk = K >> 5;
     const int S = (KSk + NWk * KPWk - 1) / (NWk * KPWk);
     const int units = a.ntiles / 2;
@@ -1803,6 +1811,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (sgroups) *sgroups = (N + 255) / 256;
     const dim3 grid(8 * ((S * G + 7) / 8));
     if (RBk == 2) hipLaunchKernelGGL((k_gemm_xsk<8, 7, 2, 2>), grid, dim3(512), 0, stream, a, units, G);
+    else if (RBk == 3 && KPWk == 5) hipLaunchKernelGGL((k_gemm_xsk<8, 5, 3, 2>), grid, dim3(512), 0, stream, a, units, G);
     else if (RBk == 3) hipLaunchKernelGGL((k_gemm_xsk<8, 4, 3, 3>), grid, dim3(512), 0, stream, a, units, G);
     else hipLaunchKernelGGL((k_gemm_xsk<8, 3, 4, 4>), grid, dim3(512), 0, stream, a, units, G);
     int rc = fo::check_launch("fo_gemm/xsk");
