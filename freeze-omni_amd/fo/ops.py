@@ -554,13 +554,32 @@ def rope_kv_write(qkv, T, H, KVH, hd, pos, slot, cos_t, sin_t, q_out, kc, vc, PS
               stream(qkv.device))
 
 
-# keys per split of the decode attention: r03c's sweep (scripts/attn_kps_sweep.py, Qwen2 28/4 heads, 8 sessions
-# x 1-2 new tokens) puts 128 first or tied at every context from 100 to 800 keys (800 keys: 21.7 us vs 24.2 at 256)
-ATTN_KEYS_PER_SPLIT = int(os.environ.get("FO_ATTN_KPS", "128"))
+# keys per split of the multi-row attention: 0 (default) = attn_keys_per_split() per launch; FO_ATTN_KPS fixes it
+# (round 4: 128 everywhere)
+ATTN_KEYS_PER_SPLIT = int(os.environ.get("FO_ATTN_KPS", "0"))
+_CUS = {}
+
+
+def attn_keys_per_split(max_keys, n_items, KVH, hd, device=None):
+    """Keys per split of a k_attn_mfma launch with the in-launch merge: the smallest multiple of 64, at least 128,
+    that keeps its grid (items x kv heads x splits) within one workgroup per CU.  The head-dim-128 kernel holds 256
+    VGPRs a lane, so one 8-wave workgroup fills a CU and a larger grid runs in rounds, each paying the staging,
+    partial stores and merge again: a duplex tick's 19 items x 4 kv heads x 7 splits of 128 keys were 532
+    workgroups in 3 rounds.  At 8 sessions x 1-2 tokens (32 items x kv heads) this stays 128 up to 1024 keys,
+    where r03c's sweep put 128 first (scripts/attn_kps_sweep.py: 800 keys 21.7 us vs 24.2 at 256)."""
+    if hd != 128:
+        return 128
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    cus = _CUS.get(dev)
+    if cus is None:
+        cus = _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
+    slots = max(1, cus // max(1, n_items * KVH))
+    per = -(-int(max_keys) // slots)
+    return max(128, -(-per // 64) * 64)
 
 
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,
-              part_ml, part_o, out, tickets=None, keys_per_split=ATTN_KEYS_PER_SPLIT, opack=None):
+              part_ml, part_o, out, tickets=None, keys_per_split=128, opack=None):
     """tickets: zeroed int32 [>= n_items * KVH] -> splits sized from each item's key count (at most
     nsplit) merged inside the launch; None -> nsplit static splits + a combine launch.
     items None: a uniform batch, T / n_items tokens per sequence in sequence order (item b = sequence b); a

@@ -125,6 +125,7 @@ class DecoderStack:
                   meta.block_table.shape[1] * self.pool.PS <= 4096)
         if fuse_o:
             xgp = attp = None
+        kps = self.attn_kps or ops.attn_keys_per_split(meta.max_keys, meta.n_items, KVH, hd, x.device)
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
@@ -142,7 +143,7 @@ class DecoderStack:
             else:
                 ops.attention(q, T, None if dense else meta.items, meta.n_items, meta.max_rows, meta.tok_nvis,
                               meta.block_table, self.pool.PS, self.pool.k[li], self.pool.v[li], H, KVH, hd, scale,
-                              nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=self.attn_kps,
+                              nsplit, part_ml, part_o, att, tickets=ws["tickets"], keys_per_split=kps,
                               opack=attp)
                 L.o(att, out=x, residual=True, M=T, stats_out=sB.set(L.ln2, xg), xpack=attp, ypack=xgp)
             L.gu(xg, out=m, M=T, norm=(sB, self.eps), xpack=xgp)
