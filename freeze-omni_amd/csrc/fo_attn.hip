@@ -58,9 +58,9 @@ __global__ __launch_bounds__(256) void k_rope_kv_write(const float* qkv, int ldq
 
 #include "fo_attn_rows.h"
 
-template <int HD, int NW = 4, int RT = 1>
+template <int HD, int NW = 4, int RT = 1, bool TR = false>
 __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
-  attn_rows_body<HD, NW, RT>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  attn_rows_body<HD, NW, RT, TR>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Single-row decode attention (the AR speech decoder's step, models/decoder/decoder.py:341-349: one
@@ -667,6 +667,7 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   }
   dim3 grid(n_items, KVH, nsplit);
   if (hd == 128 && attn_waves() == 8 && max_rows > 16) hipLaunchKernelGGL((k_attn_mfma<128, 8, 2>), grid, dim3(512), 0, s, a);
+  else if (hd == 128 && attn_waves() == 8 && a.trc) hipLaunchKernelGGL((k_attn_mfma<128, 8, 1, true>), grid, dim3(512), 0, s, a);
   else if (hd == 128 && attn_waves() == 8) hipLaunchKernelGGL((k_attn_mfma<128, 8>), grid, dim3(512), 0, s, a);
   else if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);
   else if (hd == 64) hipLaunchKernelGGL((k_attn_mfma<64>), grid, dim3(256), 0, s, a);

@@ -165,7 +165,9 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
 // while the current tile computes.  Every fp32 operand is split into bf16 hi + lo and each product
 // uses three MFMAs (hi*hi + hi*lo + lo*hi), so scores and outputs keep ~fp32 accuracy.  Online
 // softmax per row with the running max exchanged across the 4 waves through LDS.
-template <int HD, int NW, int RT = 1>   // RT: 16-row query tiles per item (2: up to 32 rows share the K / V loads)
+// RT: 16-row query tiles per item (2: up to 32 rows share the K / V loads); TR: the probe build with per-workgroup
+// clocks (a.trc) -- a compile-time switch: the runtime-null hook cost the product launches ~6 % (r05zz vs r05m)
+template <int HD, int NW, int RT = 1, bool TR = false>
 __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, const int kvh, const int sp) {
   constexpr int KT = 16 * NW;           // keys per tile: one 16-key column block per wave
   constexpr int NTH = NW * 64;
@@ -193,7 +195,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   const int grp = lane >> 4, col = lane & 15;
   const int* bt = a.block_table + (size_t)seq * a.maxb;
   unsigned long long* const tr =
-      a.trc ? a.trc + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+      TR ? a.trc + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
   if (tr && tid == 0) tr[0] = wall_clock64();
   // this lane's q row slices, requested before anything that waits (they depend only on t0)
   float4 qraw[RT][2 * DC];

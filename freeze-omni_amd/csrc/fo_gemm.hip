@@ -198,6 +198,13 @@ __device__ __forceinline__ int rope_col(const GemmArgs& a, int P, int c) {
 // zero words a lane loads instead of an operand that does not exist (branch-free prologues)
 __device__ float g_zeros[4];
 
+// The per-workgroup clock hook of the grid kernels (fo_gemm_set_trace) exists only in the probe library (make probe
+// -> fo/libfo_hip_probe.so, loaded through FO_LIB_PATH by scripts/gemm_trace.py): compiled into the product, even
+// never armed, it cost the AR decode step 178 -> 172.5 us and the encoder stage 1239 -> 1227 us (r05zj).
+#ifndef FO_GEMM_TRACE
+#define FO_GEMM_TRACE 0
+#endif
+
 template <int NT, int RB, bool XF32, int NW, int U, bool SW, bool LN = false, bool PIPE = false, bool XPK = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   using XT = typename std::conditional<XF32, float, bf16_t>::type;
@@ -214,8 +221,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
   const int m0 = mt * ROWS;
   int rbeff = (a.M - m0 + 15) >> 4;
   if (rbeff > RB) rbeff = RB;
-  unsigned long long* const trc =
-      a.trc ? a.trc + (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 24 : nullptr;
+  unsigned long long* const trc = (FO_GEMM_TRACE && a.trc)
+      ? a.trc + (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 24 : nullptr;
   if (trc && threadIdx.x == 0) trc[0] = wall_clock64();
 
   // Epilogue operands prefetched when every output element of the workgroup has its own thread (the small-M,
@@ -2164,6 +2171,9 @@ int fo_probe_seam(const float* xo, int M, const void* wo, const float* bo, float
 }
 
 int fo_gemm_set_trace(void* trace) {
+  FO_REQUIRE(FO_GEMM_TRACE || !trace,
+             "fo_gemm_set_trace: this library is built without the GEMM clock hook (make probe -> fo/libfo_hip_probe.so, "
+             "loaded with FO_LIB_PATH)");
   g_trc = reinterpret_cast<unsigned long long*>(trace);
   return 0;
 }

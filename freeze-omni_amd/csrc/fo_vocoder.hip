@@ -57,7 +57,7 @@ constexpr int CONV_KMAX = 11;
 __host__ __device__ constexpr int nks_per_chunk(int K, int CK) { return ((K * CK + 31) / 32 + 1) & ~1; }
 __host__ __device__ constexpr int conv_wmax(int CK) { return nks_per_chunk(CONV_KMAX, CK); }
 
-template <int MTW, int NTW, int CK>
+template <int MTW, int NTW, int CK, bool TR = false>   // TR: the probe build with per-workgroup clocks (mc.trc)
 __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
   constexpr int TW = 64 * NTW;     // time steps per workgroup (4 waves x 16*NTW)
   constexpr int ROWS = TW + HALO;
@@ -80,8 +80,9 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
   for (int m = 0; m < MTW; ++m)
 #pragma unroll
     for (int n = 0; n < NTW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (a compile-time switch: the runtime-null hook cost the product launches 2-4 %, r05zz vs r05m)
   unsigned long long* const tr =
-      mc.trc ? mc.trc + 4 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+      TR ? mc.trc + 4 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
   unsigned long long t_stage = 0, t_comp = 0;
   if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
 
@@ -650,21 +651,27 @@ static int conv_launch(ConvMulti& mc, int Tq_max, hipStream_t s) {
   if (halft && MTW <= 2 && NTW == 8 / MTW && CK <= 32) NTW /= 2;
   dim3 grid((Tq_max + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B * zg);
   if (MTW == 1 && CK == 64) grid.x = (Tq_max + 255) / 256;
-  if (MTW == 2 && NTW == 2 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 2, 64>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 2 && NTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 2, 32>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 2 && NTW == 2 && CK == 16) hipLaunchKernelGGL((k_conv_cl<2, 2, 16>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 1 && NTW == 4 && CK == 32) hipLaunchKernelGGL((k_conv_cl<1, 4, 32>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 1 && NTW == 4 && CK == 16) hipLaunchKernelGGL((k_conv_cl<1, 4, 16>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<4, 2, 64>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 2 && NTW == 4 && CK == 64) hipLaunchKernelGGL((k_conv_cl<2, 4, 64>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 2 && CK == 32) hipLaunchKernelGGL((k_conv_cl<2, 4, 32>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 1 && CK == 32) hipLaunchKernelGGL((k_conv_cl<1, 8, 32>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 1 && CK == 16) hipLaunchKernelGGL((k_conv_cl<1, 8, 16>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 4 && CK == 32) hipLaunchKernelGGL((k_conv_cl<4, 2, 32>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 4 && CK == 16) hipLaunchKernelGGL((k_conv_cl<4, 2, 16>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 2 && CK == 16) hipLaunchKernelGGL((k_conv_cl<2, 4, 16>), grid, dim3(256), 0, s, mc);
-  else if (MTW == 1 && CK == 64) hipLaunchKernelGGL((k_conv_cl<1, 4, 64>), grid, dim3(256), 0, s, mc);
+#define FO_CONV(A, B, C)                                                                       \
+  do {                                                                                         \
+    if (mc.trc) hipLaunchKernelGGL((k_conv_cl<A, B, C, true>), grid, dim3(256), 0, s, mc);     \
+    else hipLaunchKernelGGL((k_conv_cl<A, B, C, false>), grid, dim3(256), 0, s, mc);           \
+  } while (0)
+  if (MTW == 2 && NTW == 2 && CK == 64) FO_CONV(2, 2, 64);
+  else if (MTW == 2 && NTW == 2 && CK == 32) FO_CONV(2, 2, 32);
+  else if (MTW == 2 && NTW == 2 && CK == 16) FO_CONV(2, 2, 16);
+  else if (MTW == 1 && NTW == 4 && CK == 32) FO_CONV(1, 4, 32);
+  else if (MTW == 1 && NTW == 4 && CK == 16) FO_CONV(1, 4, 16);
+  else if (MTW == 4 && CK == 64) FO_CONV(4, 2, 64);
+  else if (MTW == 2 && NTW == 4 && CK == 64) FO_CONV(2, 4, 64);
+  else if (MTW == 2 && CK == 32) FO_CONV(2, 4, 32);
+  else if (MTW == 1 && CK == 32) FO_CONV(1, 8, 32);
+  else if (MTW == 1 && CK == 16) FO_CONV(1, 8, 16);
+  else if (MTW == 4 && CK == 32) FO_CONV(4, 2, 32);
+  else if (MTW == 4 && CK == 16) FO_CONV(4, 2, 16);
+  else if (MTW == 2 && CK == 16) FO_CONV(2, 4, 16);
+  else if (MTW == 1 && CK == 64) FO_CONV(1, 4, 64);
   else FO_REQUIRE(false, "fo_conv_cl: no variant for Cout=%d Cin=%d", Cout, Cin);
+#undef FO_CONV
   return fo::check_launch("fo_conv_cl");
 }
 

@@ -125,7 +125,10 @@ class DecoderStack:
                   meta.block_table.shape[1] * self.pool.PS <= 4096)
         if fuse_o:
             xgp = attp = None
-        kps = self.attn_kps or ops.attn_keys_per_split(meta.max_keys, meta.n_items, KVH, hd, x.device)
+        # (a captured graph's meta carries its capacity, not the replay's keys: graphs keep 128-key splits, which fill
+        # the chip at the listen / text shapes, r03c; eager launches -- duplex ticks, prefills -- size them per launch)
+        eager = x.is_cuda and not torch.cuda.is_current_stream_capturing()
+        kps = self.attn_kps or (ops.attn_keys_per_split(meta.max_keys, meta.n_items, KVH, hd, x.device) if eager else 128)
         for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,

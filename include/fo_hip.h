@@ -114,7 +114,8 @@ int fo_probe_seam(const float* xo, int M, const void* wo, const float* bo, float
 int fo_gemm_set_merge(int on);
 /* probe hook: the calling thread's following fo_gemm launches (grid kernels) write per-workgroup wall clocks
  * (100 MHz) to trace[wg * 24 + slot]: 0 start, 1 + w the end of wave w's weight stream, 17 the K reduce done,
- * 18 the epilogue issued.  nullptr turns it off (the default).  Returns 0. */
+ * 18 the epilogue issued.  nullptr turns it off (the default).  Returns 0.  The hook is compiled into the probe
+ * library only (csrc: make probe -> fo/libfo_hip_probe.so); the product library refuses a non-NULL trace (-2). */
 int fo_gemm_set_trace(void* trace);
 /* Packed activations (fo/ops.py XPack / XPack32).  A packed buffer holds an fp32 activation of <= 64 rows in MFMA
  * A-fragment order: k-step k (32 columns), row block b (16 rows), lane l = row 16 b + (l & 15), columns 32 k +
@@ -222,7 +223,9 @@ int fo_record_ids(const int* ids, int B, int* dst, int ld, const int* row, hipSt
  * 8-wave head-dim-128 kernel (two 16-row tiles sharing the K / V loads), else 16. */
 int fo_attn_max_rows(int hd);
 /* probe hook: per-workgroup wall clocks of the following multi-row fo_attention launches on this thread (8 slots a
- * workgroup in linear block order: start, staged, tile loop done, partials stored, end, 1 + splits); NULL stops. */
+ * workgroup in linear block order: start, staged, tile loop done, partials stored, end, 1 + splits); NULL stops.
+ * Armed, the head-dim-128 8-wave launches run a traced instance of the kernel (the product instance has no hook);
+ * other variants run untraced. */
 int fo_attention_set_trace(void* trace);
 int fo_attn_nsplit(int max_keys, int n_items, int KVH);
 /* RoPE (rotate_half, host cos/sin tables) + paged KV append: transformers apply_rotary_pos_emb +
@@ -359,7 +362,8 @@ int fo_conv_pair_multi(const FoPairDesc* descs, int G, int B, int C, int T, int 
                        const float* gadd, hipStream_t s);
 /* Quantizer.embed (models/decoder/ticodec/models.py:661-700), channel-last output */
 /* probe hook: per-workgroup clocks of the following k_conv_cl launches on this thread ({wall start, stage cycles,
- * compute cycles, wall end} x workgroups, linear block order); NULL stops. */
+ * compute cycles, wall end} x workgroups, linear block order); NULL stops.  Armed, they run a traced instance of the
+ * kernel (the product instance has no hook). */
 int fo_conv_set_trace(void* trace);
 int fo_codec_embed_cl(const void* table, int E, int n_codes, const int* ids, int B, int T, float* out, hipStream_t s);
 /* xs / num_kernels (+ global feature, models.py:233-238), channel-last */

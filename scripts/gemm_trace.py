@@ -3,12 +3,16 @@ last launch of a graph-replayed sequence over six weight copies (beyond the Infi
 hot shapes below 64 MB (Qwen2 o and q|k|v, the TTS decoder's).  Prints, over the workgroups: dispatch skew
 (start - first start), weight-stream time (start -> last wave's loop end), K reduce, epilogue, and the
 kernel span (first start -> last epilogue issue) beside the graph-timed per-launch time.
-python scripts/gemm_trace.py (GPU only)."""
+python scripts/gemm_trace.py (GPU only; needs the probe library: make -C freeze-omni_amd/csrc probe)."""
 import os
 import sys
 
 import numpy as np
 import torch
+
+# the clock hook lives in the probe library only (freeze-omni_amd/csrc: make probe)
+os.environ.setdefault("FO_LIB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "freeze-omni_amd", "fo", "libfo_hip_probe.so"))
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gemm_pipe_ab import PackedLinear, lib  # noqa: E402
