@@ -555,7 +555,7 @@ class ListenGraph:
     ordered by events.  The state decision of chunk c does not depend on chunk c+1, so the results are
     those of the sequential order."""
 
-    def __init__(self, eng, ident, B, R, max_keys, slots=1, wave=None):
+    def __init__(self, eng, ident, B, R, max_keys, slots=1):
         dev = eng.device
         self.eng, self.ident, self.B, self.R, self.max_keys = eng, ident, B, R, max_keys
         enc, ada, llm = eng.enc[ident], eng.ada[ident], eng.llm
@@ -595,34 +595,10 @@ class ListenGraph:
         # the encoder stage is captured on the stream it replays on, so its split-K scratch (ops.Runtime)
         # is not the LLM stage's while the two overlap
         self.enc_exec = [self._capture(self.side, lambda k=k: self._enc_body(k), ENC_GEMM_TUNE) for k in range(slots)]
+        self.llm_exec = [self._capture(self.main, lambda k=k: self._llm_body(k)) for k in range(slots)]
         self.ev_enc = [self._event() for _ in range(slots)]
         self.ev_llm = [self._event() for _ in range(slots)]
         self.llm_used = [False] * slots
-        # wave mode (slots == 2): slot k's LLM stage runs on its own stream with its own metadata, workspace and
-        # state-head output, as one captured graph per layer; chunk c + 1's layer l waits only for chunk c's layer l
-        # (the K / V rows it attends to), so consecutive chunks' stages overlap a layer apart -- the latency-bound
-        # q|k|v / o / attention of one beside the weight streams of the other.  Same kernels, same order per chunk.
-        self.wave = (LISTEN_WAVE if wave is None else wave) and slots == 2
-        if self.wave:
-            nl = len(llm.stack.layers)
-            self.lstreams = [self.main, ops.engine_stream(dev, name="listen_wave")]
-            self.lmeta_w = [torch.zeros(3 * n + B * self.maxb, dtype=I32, device=dev) for _ in range(2)]
-            self.lring_w = [_HostRing(3 * n + B * self.maxb) for _ in range(2)]
-            self.meta_w = []
-            for k in range(2):
-                m = self.lmeta_w[k]
-                self.meta_w.append(SimpleNamespace(T=n, S=B, tok_pos=m[0:n], tok_slot=m[n:2 * n], tok_nvis=m[2 * n:3 * n],
-                                                   block_table=m[3 * n:].view(B, self.maxb), items=items, n_items=B,
-                                                   max_rows=To * G, max_keys=max_keys, uniform=True))
-            self.ws_w = [self.ws, llm.stack.workspace(n, ops.attn_nsplit(max_keys, B, llm.KVH), dev)]
-            self.probs_w = [self.probs, torch.empty(B, 3, dtype=F32, device=dev)]
-            self.layer_exec = [[self._capture(self.lstreams[k], lambda k=k, l=l: self._layer_body(k, l))
-                                for l in range(nl)] for k in range(2)]
-            self.head_exec = [self._capture(self.lstreams[k], lambda k=k: self._head_body(k)) for k in range(2)]
-            self.ev_layer = [[self._event() for _ in range(nl)] for _ in range(2)]
-            self.llm_exec = []
-        else:
-            self.llm_exec = [self._capture(self.main, lambda k=k: self._llm_body(k)) for k in range(slots)]
         self.exec = True
 
     @staticmethod
@@ -661,15 +637,6 @@ class ListenGraph:
         if self.predict:
             ops.state_head(x, self.rows, llm.head_w, llm.head_b, self.probs)
 
-    def _layer_body(self, k, l):   # wave mode: layer l of slot k's LLM stage
-        self.llm.stack.forward(self.xs[k], self.meta_w[k], self.ws_w[k], layers=(l, l + 1))
-
-    def _head_body(self, k):       # wave mode: final norm + state head of slot k
-        llm, x = self.llm, self.xs[k]
-        ops.rmsnorm(x, llm.norm, llm.eps, out=x)
-        if self.predict:
-            ops.state_head(x, self.rows, llm.head_w, llm.head_b, self.probs_w[k])
-
     # ---------------------------------------------------------------- stages
     def submit_encoder(self, items, k=0):
         """Encoder stage of one chunk into x slot k (side stream when pipelined).  Advances the
@@ -703,8 +670,7 @@ class ListenGraph:
         wait=False only queues the stage and its state-head copy: collect_llm(k) reads them later."""
         B, To, maxb = self.B, self.To, self.maxb
         n = B * To
-        lring = self.lring_w[k] if self.wave else self.lring
-        j, h = lring.next()
+        j, h = self.lring.next()
         bt = h[3 * n:].reshape(B, maxb)
         for b, it in enumerate(items):
             kv = it["kv"]
@@ -719,28 +685,14 @@ class ListenGraph:
                 h[2 * n + r] = old + i + 1
             bt[b, :len(kv.pages)] = kv.pages
             kv.length = old + To
-        if self.wave:
-            st = self.lstreams[k]
-            lring.upload(j, self.lmeta_w[k], st)
+        st = self.main
+        self.lring.upload(j, self.lmeta_d, st)
+        if self.side is not self.main:
             _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_enc[k])
-            o = 1 - k
-            for l, ex in enumerate(self.layer_exec[k]):
-                if self.llm_used[o]:   # the previous chunk's layer l has appended the K / V rows this layer reads
-                    _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_layer[o][l])
-                _lib.call("fo_graph_launch", ex, st.cuda_stream)
-                _lib.call("fo_event_record", self.ev_layer[k][l], st.cuda_stream)
-            _lib.call("fo_graph_launch", self.head_exec[k], st.cuda_stream)
-            probs = self.probs_w[k]
-        else:
-            st = self.main
-            lring.upload(j, self.lmeta_d, st)
-            if self.side is not self.main:
-                _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_enc[k])
-            _lib.call("fo_graph_launch", self.llm_exec[k], st.cuda_stream)
-            probs = self.probs
+        _lib.call("fo_graph_launch", self.llm_exec[k], st.cuda_stream)
         if self.predict:
             with torch.cuda.stream(st):
-                self.probs_host[k].copy_(probs, non_blocking=True)
+                self.probs_host[k].copy_(self.probs, non_blocking=True)
         _lib.call("fo_event_record", self.ev_llm[k], st.cuda_stream)
         self.llm_used[k] = True
         self.inflight[k] = (items, new_pe)
@@ -773,13 +725,6 @@ class ListenGraph:
                 _lib.call("fo_event_destroy", e)
             self.ering.destroy()
             self.lring.destroy()
-            if self.wave:
-                for ex in [x for row in self.layer_exec for x in row] + self.head_exec:
-                    _lib.call("fo_graph_destroy", ex)
-                for e in [x for row in self.ev_layer for x in row]:
-                    _lib.call("fo_event_destroy", e)
-                for r in self.lring_w:
-                    r.destroy()
             self.exec = None
 
 
@@ -897,8 +842,6 @@ class TextGraph:
 # probe knob: FO_ENC_TUNE="waves,tiles" forces the GEMM shape of the pipelined encoder stage's graph (the stage
 # beside the Qwen2 stage, off the critical path: fewer, wider workgroups re-read its activations less often)
 ENC_GEMM_TUNE = tuple(int(v) for v in os.environ["FO_ENC_TUNE"].split(",")) if os.environ.get("FO_ENC_TUNE") else None
-# pipelined listens: consecutive chunks' Qwen2 stages as a wavefront on two streams (ListenGraph wave mode)
-LISTEN_WAVE = os.environ.get("FO_LISTEN_WAVE", "0") == "1"
 
 
 class ListenPipe:

@@ -92,13 +92,11 @@ class DecoderStack:
             ws["part_o"] = torch.empty(T * H * nsplit * hd, dtype=F32, device=device)
         return ws
 
-    def forward(self, x, meta: BatchMeta, ws=None, pre_normed=False, final_norm=None, layers=None):
+    def forward(self, x, meta: BatchMeta, ws=None, pre_normed=False, final_norm=None):
         """x: fp32 [T, D] residual stream, updated in place; KV for meta's tokens is appended.
         ws: optional workspace() of at least meta.T tokens (then nothing is allocated here).
         pre_normed: ws["h"] already holds the first layer's input RMSNorm of x (written by the
         previous decode step's sampler, fo_sample_embed).
-        layers: (l0, l1) -- run only layers l0 .. l1-1 (the listen wavefront launches the stack a layer at a time; the
-        state between layers -- x, the packed / normed inputs and row statistics in ws -- carries over).
         final_norm: gamma of the norm after the stack; the last down projection then also writes
         ws["xg"] = x * gamma and ws["sA"] row statistics, so the consumer GEMM (the output head) applies
         that RMSNorm on load instead of a separate norm launch."""
@@ -131,9 +129,7 @@ class DecoderStack:
         # the chip at the listen / text shapes, r03c; eager launches -- duplex ticks, prefills -- size them per launch)
         eager = x.is_cuda and not torch.cuda.is_current_stream_capturing()
         kps = self.attn_kps or (ops.attn_keys_per_split(meta.max_keys, meta.n_items, KVH, hd, x.device) if eager else 128)
-        l0, l1 = (0, len(self.layers)) if layers is None else layers
-        for i in range(l0, l1):
-            L = self.layers[i]
+        for i, L in enumerate(self.layers):
             li = self.kv_layer0 + i
             rope = (meta.tok_pos, meta.tok_slot, self.cos, self.sin, q, self.pool.k[li], self.pool.v[li], H, KVH,
                     self.pool.PS)

@@ -16,24 +16,6 @@ def eng(dev):
     return FreezeOmniEngine(os.path.join(ROOT, "configs", "tiny"), device=dev, max_sessions=16)
 
 
-@pytest.fixture(params=[False, True], ids=["serial", "wave"])
-def wave(request, eng):
-    """The pipelined listen's LLM stages one after another on the engine stream, or as a wavefront on two streams
-    (fo.engine.LISTEN_WAVE, ListenGraph wave mode); the engine's cached listen graphs are rebuilt for each."""
-    import fo.engine as fe
-
-    def reset():
-        for g in eng._lgraphs.values():
-            g.destroy()
-        eng._lgraphs.clear()
-    old = fe.LISTEN_WAVE
-    reset()
-    fe.LISTEN_WAVE = request.param
-    yield request.param
-    reset()
-    fe.LISTEN_WAVE = old
-
-
 def _session_run(eng, feats_seq, graph, n_users):
     base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
     kvs = [base.fork() for _ in range(n_users)]
@@ -111,7 +93,7 @@ def _session_pipe(eng, feats_seq, n_users, first_in_pipe=False):
 
 
 @pytest.mark.parametrize("first_in_pipe", [False, True])
-def test_listen_pipe_matches_sequential(eng, dev, first_in_pipe, wave):
+def test_listen_pipe_matches_sequential(eng, dev, first_in_pipe):
     """Encoder stage of chunk c+1 overlapped with the LLM stage of chunk c gives the sequential results; with
     first_in_pipe chunk 0 (its chat prefix from the shared-context prefix cache) enters the pipe too."""
     g = np.load(os.path.join(G, "fbank.npz"))
@@ -129,7 +111,7 @@ def test_listen_pipe_matches_sequential(eng, dev, first_in_pipe, wave):
             np.testing.assert_array_equal(a, b)
 
 
-def test_listen_pipe_decide_stops_and_rolls_back(eng, dev, wave):
+def test_listen_pipe_decide_stops_and_rolls_back(eng, dev):
     """decide(results of chunk c-1) returning False (dialog_ss) rolls back chunk c's speculatively queued LLM
     stage: the context holds exactly the chunks before it, and the states seen match the sequential run's."""
     g = np.load(os.path.join(G, "fbank.npz"))
@@ -155,7 +137,6 @@ def test_listen_pipe_decide_stops_and_rolls_back(eng, dev, wave):
                 state[u] = dict(enc_cache=r["enc_cache"], ada_cache=r["ada_cache"], pe_index=r["pe_index"])
             continue
         pe, _ = pipe.push(items, decide)
-        assert pipe.g.wave == wave
         for u in range(n_users):
             state[u]["pe_index"] = pe[u]
         if pipe.stopped:
