@@ -156,3 +156,56 @@ def test_scheduler_batches_one_feature_per_session_and_matches_sequential():
     a, b = run(True), run(False)
     for (sa, na, ca), (sb, nb, cb) in zip(a, b):
         assert [x[:3] for x in sa] == [x[:3] for x in sb] and na == nb and ca == cb
+
+
+def test_deferred_gating_one_fbank_launch_per_framing_group():
+    """DuplexScheduler.tick's batched gating (fo.duplex.deliver_deferred): the queued chunks of every session are
+    computed by one fbank call per (framing, device) group of their gaters, user rows before system rows inside a
+    group (one identity's rows adjacent), and finished / delivered in queue order with their own rows."""
+    import torch
+
+    from fo.duplex import deliver_deferred
+
+    class _Fbank:
+        def __init__(self):
+            self.calls = []
+
+        def __call__(self, windows, firsts):   # row i of the batch = the window's first sample, as a [R, 80] block
+            self.calls.append([float(w[0]) for w in windows])
+            return torch.tensor([[[float(w[0])] * 80] * 2 for w in windows])
+
+    class _Gater:
+        def __init__(self, kind, fb):
+            self.kind, self.device, self.fbank = kind, torch.device("cpu"), fb
+            self.got = []
+
+        def finish(self, ann, feat):
+            self.got.append((ann["n"], float(feat[0, 0, 0])))
+            return {"feature": feat, "status": ann["status"], "feature_last_chunk": []}
+
+    class _Sess:
+        def __init__(self, gaters):
+            self.feature_gater = gaters
+            self.delivered = []
+
+        def _deliver(self, ident, ann, gated):
+            self.delivered.append((ident, ann["n"], float(gated["feature"][0, 0, 0])))
+
+    fa, fb_ = _Fbank(), _Fbank()
+    s0 = _Sess({"user": _Gater("B", fa), "system": _Gater("B", fa)})
+    s1 = _Sess({"user": _Gater("B", fa), "system": _Gater("A", fb_)})
+    defer = []
+    n = 0
+    for s in (s0, s1):
+        for ident in ("user", "system"):
+            for _ in range(2):
+                n += 1
+                defer.append((s, ident, {"n": n, "status": "ipu_cl"}, (np.full(4, float(n), np.float32), False)))
+    deliver_deferred(defer)
+    # framing B: s0 user 1 2, s1 user 5 6 first, then s0 system 3 4; framing A: s1 system 7 8 on its own call
+    assert fa.calls == [[1.0, 2.0, 5.0, 6.0, 3.0, 4.0]]
+    assert fb_.calls == [[7.0, 8.0]]
+    # every chunk delivered in queue order with its own rows
+    assert s0.delivered == [("user", 1, 1.0), ("user", 2, 2.0), ("system", 3, 3.0), ("system", 4, 4.0)]
+    assert s1.delivered == [("user", 5, 5.0), ("user", 6, 6.0), ("system", 7, 7.0), ("system", 8, 8.0)]
+    deliver_deferred([])   # nothing queued: nothing to launch
