@@ -1399,6 +1399,10 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int
   const int sp = w / G, gx = w - sp * G;
   const int ub = (int)((long)units * gx / G);
   const int ue = (int)((long)units * (gx + 1) / G);
+  // probe library only (FO_GEMM_TRACE): {wall start, wall X staged, wall end, compute cycles, reduce cycles, units}
+  unsigned long long* const tr = (FO_GEMM_TRACE && a.trc) ? a.trc + 8 * (size_t)blockIdx.x : nullptr;
+  unsigned long long t_comp = 0, t_red = 0;
+  if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
   const int ks0 = sp * KW + wave * KPW;                 // this wave's first k-step
   const int nj = max(0, min(KPW, KS - ks0));            // its k-steps inside K (wave-uniform)
   const unsigned long long wbase = (unsigned long long)a.Wp;
@@ -1464,16 +1468,19 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int
   };
   const int Ncols = a.ntiles * 16;
   float* slab = a.ws + (size_t)sp * ROWS * Ncols;
+  if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
   for (int u0 = ub; u0 < ue; u0 += UA) {
 #pragma unroll
     for (int q = 0; q < UA; ++q) {
       const int u = u0 + q;
       if (u < ue) {   // workgroup-uniform: the barriers below are reached by every wave
+        const unsigned long long c0 = tr ? clock64() : 0;
         f32x4 c[2][RB];
         compute(wb[2 * q], c[0]);
         issue(wb[2 * q], 2 * (u + UA));
         compute(wb[2 * q + 1], c[1]);
         issue(wb[2 * q + 1], 2 * (u + UA) + 1);
+        const unsigned long long c1 = tr ? clock64() : 0;
 #pragma unroll
         for (int t0 = 0; t0 < 2; t0 += PT) {
           __syncthreads();  // the previous reduction has read part[]
@@ -1492,8 +1499,18 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int
             slab[(size_t)rr * Ncols + (2 * u + t0 + p) * 16 + cc] = v;
           }
         }
+        if (tr) {
+          t_comp += c1 - c0;
+          t_red += clock64() - c1;
+        }
       }
     }
+  }
+  if (tr && threadIdx.x == 0) {
+    tr[2] = wall_clock64();
+    tr[3] = t_comp;
+    tr[4] = t_red;
+    tr[5] = (unsigned long long)(ue - ub);
   }
 }
 
