@@ -1087,19 +1087,32 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xs(GemmArgs a, int units) {
     const int row = min(lane & 15, a.M - 1);
     const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)row * a.ldx + 8 * (lane >> 4) +
                       (size_t)wave * KPW * 32;
+    // the k-steps' loads in groups of XG issued before any is used (one load behind the previous one's LDS store
+    // each was KPW round trips before the first unit, r05zv); XG bounded by the 128-VGPR budget of 16 waves
+    constexpr int XG = KPW > 4 ? (KPW + 1) / 2 : KPW;
 #pragma unroll
-    for (int j = 0; j < KPW; ++j) {
-      const float4 p0 = reinterpret_cast<const float4*>(xp + j * 32)[0];
-      const float4 p1 = reinterpret_cast<const float4*>(xp + j * 32)[1];
-      const float f[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-      bf16x8 lo;
+    for (int j0 = 0; j0 < KPW; j0 += XG) {
+      float4 p[XG][2];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const __bf16 h = (__bf16)f[i];
-        xh[j][i] = h;
-        lo[i] = (__bf16)(f[i] - (float)h);
-      }
-      xlo[wave][j][lane] = lo;
+      for (int g = 0; g < XG; ++g)
+        if (j0 + g < KPW) {
+          p[g][0] = reinterpret_cast<const float4*>(xp + (j0 + g) * 32)[0];
+          p[g][1] = reinterpret_cast<const float4*>(xp + (j0 + g) * 32)[1];
+        }
+#pragma unroll
+      for (int g = 0; g < XG; ++g)
+        if (j0 + g < KPW) {
+          const int j = j0 + g;
+          const float f[8] = {p[g][0].x, p[g][0].y, p[g][0].z, p[g][0].w, p[g][1].x, p[g][1].y, p[g][1].z, p[g][1].w};
+          bf16x8 lo;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const __bf16 h = (__bf16)f[i];
+            xh[j][i] = h;
+            lo[i] = (__bf16)(f[i] - (float)h);
+          }
+          xlo[wave][j][lane] = lo;
+        }
     }
   }
   if (a.rstats) {  // RMSNorm consumer: rstd of each row from the producer's partial sums
