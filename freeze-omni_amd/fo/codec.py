@@ -222,9 +222,12 @@ class CodecEngine:
         bf = self._graphs.pop(key, None)
         if bf is None:
             if len(self._graphs) >= self.MAX_GRAPHS:   # least recently used (dict order) goes
-                old = self._graphs.pop(next(iter(self._graphs)))
+                okey = next(iter(self._graphs))
+                old = self._graphs.pop(okey)
                 if old.exec is not None:
-                    torch.cuda.synchronize(self.device)
+                    # its last replay ran on its own stream: wait for that one (a device-wide synchronize would also
+                    # wait on -- and, mid-capture, invalidate -- another serving thread's stream)
+                    torch.cuda.ExternalStream(okey[2], device=self.device).synchronize()
                     _lib.call("fo_graph_destroy", old.exec)
             bf = self._buffers(B, T)
         self._graphs[key] = bf

@@ -287,8 +287,9 @@ class FreezeOmniEngine:
         g = self._egraphs.pop(key, None)
         if g is None:
             if len(self._egraphs) >= self.MAX_ENC_GRAPHS:
-                torch.cuda.synchronize(self.device)
-                self._egraphs.pop(next(iter(self._egraphs))).destroy()
+                okey = next(iter(self._egraphs))
+                torch.cuda.ExternalStream(okey[3], device=self.device).synchronize()   # its last replay's stream only
+                self._egraphs.pop(okey).destroy()
             g = EncoderGraph(self, ident, B, R, st)
         self._egraphs[key] = g
         return g

@@ -66,6 +66,8 @@ def engine_stream(device, side=False, name=None):
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
     key = (idx, name if name is not None else bool(side))
+    if idx in getattr(_SERVE_TLS, "devices", ()):
+        return _serve_stream(idx, key[1], name)
     if key not in _ENGINE_STREAMS:
         h = ctypes.c_void_p()
         with torch.cuda.device(idx):
@@ -88,6 +90,30 @@ def engine_stream(device, side=False, name=None):
                 _lib.call("fo_stream_create", ctypes.byref(h))
         _ENGINE_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
     return _ENGINE_STREAMS[key]
+
+
+# The serving threads (fo.serve: one per replica for the listen / text work, one for speech) own their device's work:
+# on such a thread engine_stream() hands out a private family of NON-blocking streams instead of the blocking ones
+# above.  A caller thread of the reference's threading model (bin/dialog_state_pred.py:802-804) may then run work on
+# the legacy default stream (a .cpu() of a PCM segment, a gater's fbank) while the serving thread captures a graph:
+# a blocking stream would sync implicitly with that legacy work and invalidate the capture.  The serving thread
+# orders its inputs (caller events) and outputs (synchronised before a call returns) itself.
+_SERVE_TLS = threading.local()
+_SERVE_STREAMS = {}
+
+
+def serve_streams(idx):
+    """Make engine_stream() on the calling thread return the serving stream family of device idx."""
+    _SERVE_TLS.devices = tuple(getattr(_SERVE_TLS, "devices", ())) + (idx,)
+
+
+def _serve_stream(idx, part, name):
+    key = (idx, "serve", part)
+    if key not in _SERVE_STREAMS:
+        hi = name is not None and name.startswith(HIGH_PRIORITY_STREAMS)
+        # torch's own streams are created hipStreamNonBlocking; priority -1 is the device's greatest
+        _SERVE_STREAMS[key] = torch.cuda.Stream(device=torch.device("cuda", idx), priority=-1 if hi else 0)
+    return _SERVE_STREAMS[key]
 
 
 class Runtime:

@@ -16,6 +16,8 @@ Batched: one launch sequence serves all users of a replica; per-user state lives
 import math
 import os
 
+import threading
+
 import numpy as np
 import torch
 
@@ -72,6 +74,9 @@ class FbankGPU:
         self.window, self.tw_cos, self.tw_sin, self.mel = (t.to(self.device) for t in (w, c, s, m))
         # pinned staging of the calls: a ring of 4 slots (grown on demand), each reused once its copy has run
         self._pins, self._evs, self._k = [None] * 4, [None] * 4, 0
+        # the reference gates every session's audio in a thread of its own (bin/dialog_state_pred.py:240-288) and the
+        # gaters of one engine share this object: one caller at a time in the staging ring
+        self._lock = threading.Lock()
 
     def _stage(self, host):
         """host float32 [n] -> a new device tensor: through this object's own pinned ring and one async copy on the
@@ -100,6 +105,10 @@ class FbankGPU:
 
     def __call__(self, windows, firsts):
         """windows: np.float32 [B][n_samples]; firsts: list[bool] -> device feats [B, R, 80]."""
+        with self._lock:
+            return self._call(windows, firsts)
+
+    def _call(self, windows, firsts):
         B = len(firsts)
         host = np.concatenate([np.ascontiguousarray(windows, np.float32).reshape(-1),
                                np.asarray([self.ov if f else 0 for f in firsts], np.int32).view(np.float32)])

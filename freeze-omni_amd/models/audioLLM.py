@@ -11,6 +11,7 @@ The text decode step that the fork removed is reconstructed 
 contract in bin/inference.py:133-187: generate_step(...).
 """
 import copy
+import os
 
 import torch
 
@@ -107,7 +108,21 @@ class AudioLLM:
     def set_system_role(self, extra_inputs=None):
         extra_inputs = extra_inputs or {}
         assert extra_inputs.get("past_key_values", None) is None, "past key values already exist!!!"
-        return PastKeyValues(self.engine.system_role(extra_inputs.get("role_prompt", None)))
+        return PastKeyValues(self._run(self.engine.system_role, extra_inputs.get("role_prompt", None)))
+
+    # every entry below runs on the replica's serving thread (fo.serve.ReplicaScheduler): the reference calls one
+    # pipeline from many session threads (bin/dialog_state_pred.py:802-804); FO_SERVE=0 runs on the caller's thread
+    SERVE = os.environ.get("FO_SERVE", "1") != "0"
+
+    def _scheduler(self):
+        if not self.SERVE:
+            return None
+        from fo.serve import ReplicaScheduler
+        return ReplicaScheduler.for_device(self.device)
+
+    def _run(self, fn, *args, **kw):
+        sch = self._scheduler()
+        return fn(*args, **kw) if sch is None else sch.call(fn, *args, **kw)
 
     # ------------------------------------------------------------------ models/audioLLM.py:350-429
     def recognize(self, speech, extra_inputs=None):
@@ -115,13 +130,20 @@ class AudioLLM:
 
     def recognize_batch(self, requests):
         """Batched recognize: requests = [(speech [1,T,80], extra_inputs)] -> list of 5-tuples.
-        All users' chunks run through one encoder/adapter/LLM launch sequence."""
-        items = []
-        for speech, ex in requests:
+        All users' chunks run through one encoder/adapter/LLM launch sequence (on the serving thread, together with
+        the concurrent calls of other sessions)."""
+        for speech, ex in requests:   # the reference's protocol errors, raised in the caller's thread
             assert ex.get("past_key_values", None) is not None, "must set system role first!!!"
             ident = ex.get("identity")
             if ident not in ("user", "system"):
                 raise ValueError(f"Unknown identity: {ident}. Must be 'user' or 'system'.")
+        sch = self._scheduler()
+        return self._recognize_now(requests) if sch is None else sch.listen(self, requests)
+
+    def _recognize_now(self, requests):
+        items = []
+        for speech, ex in requests:
+            ident = ex.get("identity")
             feats = torch.as_tensor(speech)
             feats = feats.reshape(feats.shape[-2], feats.shape[-1]).to(self.device, F32)
             items.append(dict(identity=ident, status=ex.get("status"), feats=feats,
@@ -131,7 +153,6 @@ class AudioLLM:
         out = []
         for (speech, ex), r in zip(requests, res):
             out.append((r["probs"], ex["past_key_values"], r["ada_cache"], r["enc_cache"], r["pe_index"]))
-            self._last_hidden = r["hidden_row"]
         return out
 
     # ------------------------------------------------------------------ models/audioLLM.py:431-477
@@ -140,11 +161,14 @@ class AudioLLM:
         431-477): temperature, top_k > 0 keeps the k largest (0 = no top-k filtering: the whole
         vocabulary), top_p > 0 the nucleus, then one draw (fo_sample).  The draw comes from the
         kernel's counter stream: `seed` pins it, otherwise each call takes the next stream."""
-        lg = torch.as_tensor(output).reshape(1, -1).to(self.device, F32).contiguous()
-        V = lg.shape[1]
         if seed is None:
             self._draws = getattr(self, "_draws", 0) + 1
             seed = self._draws
+        return self._run(self._post_decode_now, output, temperature, top_k, top_p, seed)
+
+    def _post_decode_now(self, output, temperature, top_k, top_p, seed):
+        lg = torch.as_tensor(output).reshape(1, -1).to(self.device, F32).contiguous()
+        V = lg.shape[1]
         out = torch.empty(1, dtype=I32, device=self.device)
         chk = ops.sample_check(self.device)
         ops.sample(lg, V, out, torch.tensor([int(top_k)], dtype=I32).to(self.device),
@@ -157,11 +181,19 @@ class AudioLLM:
     # ------------------------------------------------------------------ A17: text decode step
     def generate_step(self, past_key_values, input_ids, top_k=None, top_p=None, temperature=None):
         """Forward `input_ids` on the session context and sample the next token from the last
-        position.  Returns (token id, last hidden state [1, 1, D] device)."""
-        ids, hid = self.engine.text_step([(past_key_values.seq, list(input_ids))],
-                                         top_k=self.top_k if top_k is None else top_k,
-                                         top_p=self.top_p if top_p is None else top_p,
-                                         temperature=self.temperature if temperature is None else temperature)
+        position.  Returns (token id, last hidden state [1, 1, D] device).  Concurrent one-token steps of other
+        sessions with the same sampler settings share one text step on the serving thread."""
+        top_k = self.top_k if top_k is None else top_k
+        top_p = self.top_p if top_p is None else top_p
+        temperature = self.temperature if temperature is None else temperature
+        sch = self._scheduler()
+        if sch is None:
+            return self._generate_now(past_key_values, input_ids, top_k, top_p, temperature)
+        return sch.text(self, past_key_values, input_ids, top_k, top_p, temperature)
+
+    def _generate_now(self, past_key_values, input_ids, top_k, top_p, temperature):
+        ids, hid = self.engine.text_step([(past_key_values.seq, list(input_ids))], top_k=top_k, top_p=top_p,
+                                         temperature=temperature)
         return ids[0], hid.view(1, 1, -1)
 
     def prefix_ids(self, identity):
