@@ -218,7 +218,10 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   for (int i = 0; i < tn; ++i) Lmax = max(Lmax, a.tok_nvis[t0 + i]);
   int ns = a.nsplit;
   if (a.cnt) {
-    ns = min(ns, max(1, (Lmax + a.kps - 1) / a.kps));
+    // never fewer splits than keep each within the LDS page table (fo_attn_nsplit's `need` term): a large
+    // keys_per_split on a long sequence would otherwise take the poison branch below
+    const int need = (Lmax + MAXPG * a.PS - 1) / (MAXPG * a.PS);
+    ns = min(ns, max(need, max(1, (Lmax + a.kps - 1) / a.kps)));
     if (sp >= ns) return;  // beyond this item's splits: never counted, never read
   }
   const int per = ((Lmax + ns - 1) / ns + KT - 1) / KT * KT;

@@ -601,7 +601,12 @@ def attn_keys_per_split(max_keys, n_items, KVH, hd, device=None):
         cus = _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
     slots = max(1, cus // max(1, n_items * KVH))
     per = -(-int(max_keys) // slots)
-    return max(128, -(-per // 64) * 64)
+    # at most one split's LDS page table (256 pages of 16 keys; the kernel also keeps its split count at least
+    # ceil(keys / 4096), so a longer sequence never takes the poison branch)
+    return min(ATTN_MAX_SPLIT_KEYS, max(128, -(-per // 64) * 64))
+
+
+ATTN_MAX_SPLIT_KEYS = 4096
 
 
 def attention(q, T, items, n_items, max_rows, tok_nvis, block_table, PS, kc, vc, H, KVH, hd, scale, nsplit,

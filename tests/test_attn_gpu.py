@@ -141,3 +141,52 @@ def test_decode_attention_fused_with_o_projection(dev, B, lens):
     ss = (ref ** 2).sum(1)
     assert torch.allclose(st.buf[:B].cpu().double(), ss, rtol=1e-5)
     assert int(tickets.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("kps", [None, 8192])
+def test_long_sequence_prefill_splits_stay_within_the_page_table(dev, kps):
+    """an eager prefill of 40 work items (80 tokens at GQA 7) against a sequence of more than 4096 keys.
+    The per-launch keys_per_split (ops.attn_keys_per_split: one split per item when the items fill the CUs) and a
+    larger one passed directly (8192) must both keep every split within the 256-page LDS table -- the kernel never
+    takes fewer than ceil(keys / 4096) splits -- and give the static-split result (no poisoned NaN rows)."""
+    H, KVH, hd = 28, 4, 128
+    g = torch.Generator().manual_seed(77)
+    pool = KVPool(1, KVH, hd, 400, 16, dev)
+    pool.k.copy_(torch.randn(pool.k.shape, generator=g))
+    pool.v.copy_(torch.randn(pool.v.shape, generator=g))
+    seq = KVSeq(pool)
+    BatchMeta([(seq, 5000, 0, True)], dev)
+    meta = BatchMeta([(seq, 80, seq.length, True)], dev, gqa=H // KVH, rows=16)
+    assert meta.n_items == 40 and meta.max_keys == 5080
+    T = meta.T
+    q = torch.randn(T, H * hd, generator=g).to(dev)
+    scale = 1 / math.sqrt(hd)
+    ns = ops.attn_nsplit(meta.max_keys, meta.n_items, KVH)
+    assert ns >= 2
+    k_eff = ops.attn_keys_per_split(meta.max_keys, meta.n_items, KVH, hd, dev) if kps is None else kps
+    assert k_eff <= 4096 or kps is not None
+    part_ml = torch.empty(T * H * ns * 2, device=dev)
+    part_o = torch.empty(T * H * ns * hd, device=dev)
+    static = torch.empty(T, H * hd, device=dev)
+    ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0],
+                  pool.v[0], H, KVH, hd, scale, ns, part_ml, part_o, static)
+    out = torch.full((T, H * hd), float("nan"), device=dev)
+    tickets = torch.zeros(meta.n_items * KVH, dtype=torch.int32, device=dev)
+    ops.attention(q, T, meta.items, meta.n_items, meta.max_rows, meta.tok_nvis, meta.block_table, pool.PS, pool.k[0],
+                  pool.v[0], H, KVH, hd, scale, ns, part_ml, part_o, out, tickets=tickets, keys_per_split=k_eff)
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any() and not torch.isnan(static).any()
+    torch.testing.assert_close(out, static, atol=2e-5, rtol=1e-4)
+    assert int(tickets.abs().sum()) == 0
+    # and the static result against a float64 reference on a few rows (the sequence's K / V gathered once)
+    pages = torch.tensor(seq.pages, dtype=torch.long)
+    K = pool.k[0].cpu().double()[pages].permute(1, 0, 2, 3).reshape(KVH, -1, hd)
+    V = pool.v[0].cpu().double()[pages].permute(1, 0, 2, 3).reshape(KVH, -1, hd)
+    nvis = meta.tok_nvis.cpu().tolist()
+    qd = q.cpu().double()
+    for t in (0, 41, T - 1):
+        for h in (0, 13, 27):
+            kh = h // (H // KVH)
+            sc = K[kh, :nvis[t]] @ qd[t, h * hd:(h + 1) * hd] * scale
+            ref = torch.softmax(sc, 0) @ V[kh, :nvis[t]]
+            torch.testing.assert_close(static[t, h * hd:(h + 1) * hd].cpu().double(), ref, atol=2e-5, rtol=1e-4)

@@ -9,7 +9,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "include", "fo_hip.h")
-LIB = os.path.join(ROOT, "freeze-omni_amd", "fo", "libfo_hip.so")
+LIB = os.environ.get("FO_LIB_PATH") or os.path.join(ROOT, "freeze-omni_amd", "fo", "libfo_hip.so")
 
 
 def header_decls():

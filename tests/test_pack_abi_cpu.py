@@ -8,7 +8,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "freeze-omni_amd", "fo", "libfo_hip.so")
+LIB = os.environ.get("FO_LIB_PATH") or os.path.join(ROOT, "freeze-omni_amd", "fo", "libfo_hip.so")
 pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="libfo_hip.so not built (run __graft_entry__.build())")
 
 FAKE = 1 << 20   # dummy device addresses: never dereferenced by a refused call
