@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="listen chunk by chunk (default: encoder stage of chunk c+1 overlaps the LLM of chunk c)")
+    ap.add_argument("--listen-chunks", type=int, default=int(os.environ.get("FO_LISTEN_CHUNKS", "1")),
+                    help="consecutive 160 ms chunks of the offline input per Qwen2 stage (fo.engine.ListenGroupGraph; "
+                         "1: one chunk per stage)")
     ap.add_argument("--scenario", default="turn", choices=["turn", "duplex"],
                     help="turn: config 3 (default, the headline line); duplex: config 5 sessions")
     ap.add_argument("--duplex-sec", type=float, default=60.0, help="duplex: seconds of audio per session")
@@ -200,7 +203,7 @@ def run_turn(engine, base_kv, pcms, args, sync):
     fb = engine.fbank("A")
     CH = turns[0].framer.chunk
     n_chunks = int(math.ceil(len(pcms[0]) / CH))
-    pipe = engine.listen_pipe() if args.pipeline else None
+    pipe = engine.listen_pipe(args.listen_chunks) if args.pipeline else None
     from fo import ops
     side = ops.engine_stream(engine.device, side=True)
     for c in range(n_chunks):
@@ -497,13 +500,15 @@ def vocoder_calls(n, chunk=40, pad=10):
 
 def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.0e12, mfma=2.5e15):
     """Speed-of-light time of one turn's work (each stage against its own bound, the turn as
-    Σ max(bytes / HBM BW, flops / dense bf16 MFMA peak)).  Algorithmic bytes of this implementation's
-    layouts: bf16 weights streamed once per batched step, fp32 paged KV read per token
-    (Qwen2 114,688 B, AR decoder 28,672 B), vocoder as 2*Cin*Cout*K*Tout FLOPs.  ctx0: per-user LLM context
-    when the listen starts (system prompt)."""
+    Σ max(bytes / HBM BW, flops / dense bf16 MFMA peak)).  Algorithmic bytes: bf16 weights
+    streamed once per batched step, the KV read per token at the reference's bf16 (autocast k_proj / v_proj outputs,
+    models/pipeline.py:67-68): Qwen2 57,344 B, AR decoder 14,336 B; vocoder as 2*Cin*Cout*K*Tout FLOPs.  This build
+    keeps its paged KV in fp32: the bytes that layout reads beyond the bf16 figure are reported apart
+    ("kv_fp32_extra_GB"), never counted as work.  ctx0: per-user LLM context when the listen starts (system prompt)."""
     llm = eng.llm
-    kv_llm = llm.stack.n * llm.KVH * llm.hd * 2 * 4
-    kv_tts = eng.tts.main.n * eng.tts.H * eng.tts.hd * 2 * 4
+    kv_llm = llm.stack.n * llm.KVH * llm.hd * 2 * 2
+    kv_tts = eng.tts.main.n * eng.tts.H * eng.tts.hd * 2 * 2
+    kv_extra = 0.0   # bytes per (algorithmic bf16) KV byte the fp32 layout adds
     w_listen = eng.enc["user"].weight_bytes + eng.ada["user"].weight_bytes + llm.stack.weight_bytes
     rows = 2   # LLM tokens per 160 ms chunk (framing A)
     listen_b = 0.0
@@ -511,10 +516,12 @@ def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.
     for c in range(n_chunks):
         L += rows + (len(eng.prefix_ids["user"]) if c == 0 else 0)
         listen_b += w_listen + B * L * kv_llm
+        kv_extra += B * L * kv_llm
     text_b = 0.0
     L += len(eng.prefix_ids["system"])
     for t in range(text_tokens):
         text_b += llm.stack.weight_bytes + llm.lm_head.nbytes + B * L * kv_llm
+        kv_extra += B * L * kv_llm
         L += 1
     speak_b, speak_f = 0.0, 0.0
     pre_w = eng.tts.pre.weight_bytes + eng.tts.main.weight_bytes + (eng.tts.prefix.weight_bytes if eng.tts.prefix else 0)
@@ -523,11 +530,12 @@ def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.
         P = 2 * 4 * (text_tokens // max(1, len(codec_per_sentence)))   # prefix + prefill rows (4 sub-tokens each)
         for i in range(n):
             speak_b += eng.tts.weight_bytes_per_step + B * (P + i) * kv_tts
+            kv_extra += B * (P + i) * kv_tts
         speak_f += B * sum(eng.codec.flops(T) for T in vocoder_calls(n))
     ms = {"listen": listen_b / bw * 1e3, "text": text_b / bw * 1e3,
           "speak": max(speak_b / bw, 0.0) * 1e3 + speak_f / mfma * 1e3}
     return ms, {"listen_GB": listen_b / 1e9, "text_GB": text_b / 1e9, "speak_GB": speak_b / 1e9,
-                "vocoder_TFLOP": speak_f / 1e12}
+                "vocoder_TFLOP": speak_f / 1e12, "kv_fp32_extra_GB": kv_extra / 1e9}
 
 
 def codec_ids_check(eng):
@@ -879,10 +887,11 @@ def run_duplex(eng, args, seconds, sync, probe=False):
         if probe:
             marks, eng.stage_probe = eng.stage_probe, None
             st = {"host_gating": (t_host - t) * 1e3, "items": len(done), "tick": ticks[-1] * 1e3}
-            # algorithmic bytes of the tick (DESIGN §5 U1 at framing B): each identity's encoder + adapter weights
-            # once, the Qwen2 layers once, every prefilled session's KV read
+            # algorithmic bytes of the tick (SURVEY §8(d) U1 at framing B): each identity's encoder + adapter weights
+            # once, the Qwen2 layers once, every prefilled session's KV read at the reference's bf16 (57,344 B a token;
+            # the fp32 paged layout's extra half is not work)
             llm = eng.llm
-            kv_tok = llm.stack.n * llm.KVH * llm.hd * 2 * 4
+            kv_tok = llm.stack.n * llm.KVH * llm.hd * 2 * 2
             idents = {d["identity"] for _, d, _ in done}
             st["bytes"] = (sum(eng.enc[i].weight_bytes + eng.ada[i].weight_bytes for i in idents) +
                            llm.stack.weight_bytes + sum(ss.past_key_values.get_seq_length() for ss, _, _ in done) * kv_tok)
@@ -1171,7 +1180,7 @@ def main():
                                    + ("starts at its boundary beside the text decode" if args.concurrent_tts else
                                       "runs inside the text loop (bin/inference.py order)"),
                        "text_tokens": args.text_tokens, "sentences": stats[0]["n_sent"],
-                       "codec_tokens": args.codec_tokens,
+                       "codec_tokens": args.codec_tokens, "listen_chunks_per_stage": args.listen_chunks,
                        "model": f"Freeze-Omni ({args.config}): speech encoder + adapter + Qwen2-7B + AR decoder + "
                                 "TiCodec", "users_per_gpu": args.users, "global_users": args.users * world,
                        "parallelism": f"dp{world} (session-pinned replicas)"},

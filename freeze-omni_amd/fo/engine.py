@@ -257,25 +257,29 @@ class FreezeOmniEngine:
         To = self.ada[ident].out_len(self.enc[ident].dims(R)[2])
         return To * (self.llm.H // self.llm.KVH) <= 16
 
-    def _listen_graph_for(self, items, slots=1, extra=64):
+    def _listen_graph_for(self, items, slots=1, extra=64, chunks=1):
         ident = items[0]["identity"]
         B, R = len(items), items[0]["feats"].shape[0]
         need = max(it["kv"].length for it in items) + extra
-        key = (ident, B, R, slots)
+        key = (ident, B, R, slots) if chunks == 1 else (ident, B, R, "group", chunks)
         g = self._lgraphs.get(key)
         if g is None or g.max_keys < need:
             if g is not None:
                 g.destroy()
-            g = ListenGraph(self, ident, B, R, max(need + 1024, 2048), slots=slots)
+            if chunks == 1:
+                g = ListenGraph(self, ident, B, R, max(need + 1024, 2048), slots=slots)
+            else:
+                g = ListenGroupGraph(self, ident, B, R, max(need + 1024, 2048), chunks)
             self._lgraphs[key] = g
         return g
 
     def _listen_graph(self, items):
         return self._listen_graph_for(items).run(items)
 
-    def listen_pipe(self):
-        """A ListenPipe over this engine (encoder stage of chunk c+1 overlapped with the LLM of chunk c)."""
-        return ListenPipe(self)
+    def listen_pipe(self, chunks=1):
+        """A ListenPipe over this engine (encoder stage of chunk c+1 overlapped with the LLM of chunk c); chunks > 1:
+        that many consecutive chunks per Qwen2 stage (ListenGroupGraph)."""
+        return ListenPipe(self, chunks)
 
     MAX_ENC_GRAPHS = 32
 
@@ -729,6 +733,170 @@ class ListenGraph:
             self.exec = None
 
 
+class ListenGroupGraph:
+    """C consecutive steady-state chunks of B sessions in ONE Qwen2 stage (the listen of an offline input: the
+    reference feeds a wav's chunks back to back, bin/inference.py:119-150).  Each chunk's encoder stage is its own
+    captured replay (the encoder is chunk-recurrent), writing its rows into the group's x slot chunk-major
+    ([chunk][session][token]); the LLM stage then prefills all C x B x To rows at once -- each session's C chunks are
+    its next C*To positions, causal, so chunk j's rows see chunks < j of the same stage as the sequential order does
+    -- and the dialog-state head reads every chunk's last row (one decision per chunk, models/audioLLM.py:420-429).
+    Work items are (session, chunk): To tokens each, as in ListenGraph.  The Qwen2 weights stream once per C chunks
+    instead of once per chunk; the GEMMs run at C x 16 rows (k_gemm_xsk / the 17..64-row paths), whose row-count
+    dependent tilings give the sequential results to fp32 rounding, not bit for bit.  A group of m < C chunks (the
+    end of the input) replays an LLM stage captured for m.  Two slots: the encoder stages of group g+1 run on the side
+    stream while group g's LLM stage runs (ListenPipe)."""
+
+    def __init__(self, eng, ident, B, R, max_keys, C):
+        dev = eng.device
+        self.eng, self.ident, self.B, self.R, self.max_keys, self.C = eng, ident, B, R, max_keys, C
+        enc, ada, llm = eng.enc[ident], eng.ada[ident], eng.llm
+        self.enc, self.ada, self.llm = enc, ada, llm
+        self.feats = torch.empty(B, R, 80, dtype=F32, device=dev)
+        self.eb = enc.buffers(B, R)
+        self.T = enc.dims(R)[2]
+        self.ab = ada.buffers(B, self.T)
+        self.To = To = ada.out_len(self.T)
+        G = llm.H // llm.KVH
+        assert To * G <= 16, "listen group graph: one attention work item per (session, chunk)"
+        self.n1 = n1 = B * To
+        self.n = n = C * n1
+        PS = llm.pool.PS
+        self.maxb = (max_keys + PS - 1) // PS
+        self.emeta_d = torch.zeros(5 * B, dtype=I32, device=dev)
+        self.lmeta_d = torch.zeros(3 * n + B * self.maxb, dtype=I32, device=dev)
+        self.ering, self.lring = _HostRing(5 * B), _HostRing(3 * n + B * self.maxb)
+        self.eb["meta"] = self.emeta_d[0:4 * B]
+        self.ab["slots"] = self.emeta_d[4 * B:5 * B]
+        lm = self.lmeta_d
+        self.items = torch.tensor([[b, j * n1 + b * To, To] for j in range(C) for b in range(B)],
+                                  dtype=I32).reshape(-1).to(dev)
+        self.rows = torch.tensor([j * n1 + b * To + To - 1 for j in range(C) for b in range(B)], dtype=I32).to(dev)
+        bt = lm[3 * n:].view(B, self.maxb)
+        self.metas = {m: SimpleNamespace(T=m * n1, S=B, tok_pos=lm[0:m * n1], tok_slot=lm[n:n + m * n1],
+                                         tok_nvis=lm[2 * n:2 * n + m * n1], block_table=bt,
+                                         items=self.items[:3 * m * B], n_items=m * B, max_rows=To * G,
+                                         max_keys=max_keys, uniform=False)
+                      for m in range(1, C + 1)}
+        self.xs = [torch.empty(n, llm.D, dtype=F32, device=dev) for _ in range(2)]
+        self.ws = llm.stack.workspace(n, ops.attn_nsplit(max_keys, C * B, llm.KVH), dev)
+        self.predict = ident == "user" and bool(eng.predict_usr_state) and llm.head_w is not None
+        self.probs = torch.empty(C * B, 3, dtype=F32, device=dev)
+        self.probs_host = [torch.empty(C * B, 3, dtype=F32).pin_memory() for _ in range(2)]
+        self.inflight = [None, None]
+        self.main = ops.engine_stream(dev)
+        self.side = ops.engine_stream(dev, side=True)
+        self.enc_exec = [[ListenGraph._capture(self.side, lambda k=k, j=j: self._enc_body(k, j), ENC_GEMM_TUNE)
+                          for j in range(C)] for k in range(2)]
+        self.llm_exec = [{}, {}]   # slot -> {chunks in the group: captured LLM stage}
+        self.ev_enc = [ListenGraph._event() for _ in range(2)]
+        self.ev_llm = [ListenGraph._event() for _ in range(2)]
+        self.llm_used = [False, False]
+        self.exec = True
+
+    def _enc_body(self, k, j):
+        xe, T = self.enc.run(self.feats, self.B, self.R, self.eb)
+        emb, To = self.ada.run(xe, self.B, T, self.ab)
+        ops.gather_rows(emb, None, out=self.xs[k][j * self.n1:(j + 1) * self.n1], round_fp16=True)   # .half()
+
+    def _llm_body(self, k, m):
+        llm, x = self.llm, self.xs[k][:m * self.n1]
+        llm.stack.forward(x, self.metas[m], self.ws)
+        ops.rmsnorm(x, llm.norm, llm.eps, out=x)
+        if self.predict:
+            ops.state_head(x, self.rows[:m * self.B], llm.head_w, llm.head_b, self.probs)
+
+    def submit_encoder(self, items, k, j):
+        """Chunk j of the group in slot k: its encoder stage (side stream) into rows j of x slot k.  Advances the
+        encoder caches; returns the per-session pe_index after this chunk."""
+        B = self.B
+        caches = [it["enc_cache"] for it in items]
+        emeta, new_pe = self.enc.host_meta(caches, [it["pe_index"] or 0 for it in items])
+        q, h = self.ering.next()
+        h[0:4 * B] = emeta
+        h[4 * B:5 * B] = [it["ada_cache"].slot for it in items]
+        st = self.side
+        if j == 0 and self.llm_used[k]:
+            _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_llm[k])   # slot k's last reader is done
+        with torch.cuda.stream(st):
+            f0 = items[0]["feats"]
+            if f0.is_contiguous() and all(it["feats"].data_ptr() == f0.data_ptr() + b * self.R * 80 * 4
+                                          for b, it in enumerate(items)):
+                self.feats.copy_(f0.as_strided((B, self.R, 80), (self.R * 80, 80, 1)))
+            else:
+                for b, it in enumerate(items):
+                    self.feats[b].copy_(it["feats"])
+        self.ering.upload(q, self.emeta_d, st)
+        _lib.call("fo_graph_launch", self.enc_exec[k][j], st.cuda_stream)
+        _lib.call("fo_event_record", self.ev_enc[k], st.cuda_stream)
+        self.enc.advance(caches, self.T)
+        return new_pe
+
+    def submit_llm(self, groups, pes, k):
+        """The LLM stage of the m = len(groups) chunks whose encoder stages filled slot k (engine stream); appends
+        m * To KV rows per session.  collect_llm(k) reads its results."""
+        B, To, n1, n, maxb = self.B, self.To, self.n1, self.n, self.maxb
+        m = len(groups)
+        ex = self.llm_exec[k].get(m)
+        if ex is None:
+            ex = self.llm_exec[k][m] = ListenGraph._capture(self.main, lambda: self._llm_body(k, m))
+        q, h = self.lring.next()
+        bt = h[3 * n:].reshape(B, maxb)
+        for b, it in enumerate(groups[0]):
+            kv = it["kv"]
+            old = kv.length
+            kv.reserve(old + m * To)
+            if len(kv.pages) > maxb:
+                raise RuntimeError("listen group graph block table too small")
+            for j in range(m):
+                for i in range(To):
+                    r = j * n1 + b * To + i
+                    pos = old + j * To + i
+                    h[r] = pos
+                    h[n + r] = kv.slot(pos)
+                    h[2 * n + r] = pos + 1
+            bt[b, :len(kv.pages)] = kv.pages
+            kv.length = old + m * To
+        st = self.main
+        self.lring.upload(q, self.lmeta_d, st)
+        _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_enc[k])
+        _lib.call("fo_graph_launch", ex, st.cuda_stream)
+        if self.predict:
+            with torch.cuda.stream(st):
+                self.probs_host[k][:m * B].copy_(self.probs[:m * B], non_blocking=True)
+        _lib.call("fo_event_record", self.ev_llm[k], st.cuda_stream)
+        self.llm_used[k] = True
+        self.inflight[k] = (groups, pes)
+
+    def collect_llm(self, k):
+        """Results of the LLM stage queued in slot k (waits for it): one result list per chunk, in chunk order."""
+        groups, pes = self.inflight[k]
+        self.inflight[k] = None
+        B, To, n1 = self.B, self.To, self.n1
+        _lib.call("fo_event_sync", self.ev_llm[k])
+        probs = self.probs_host[k].numpy() if self.predict else None
+        out = []
+        for j, (items, pe) in enumerate(zip(groups, pes)):
+            res = []
+            for b, it in enumerate(items):
+                r = {"enc_cache": it["enc_cache"], "ada_cache": it["ada_cache"], "pe_index": pe[b],
+                     "hidden_row": (self.xs[k], j * n1 + b * To + To - 1), "probs": None}
+                if probs is not None:
+                    r["probs"] = {"state_1": float(probs[j * B + b, 1]), "state_2": float(probs[j * B + b, 2])}
+                res.append(r)
+            out.append(res)
+        return out
+
+    def destroy(self):
+        if self.exec is not None:
+            for ex in [e for row in self.enc_exec for e in row] + [e for d in self.llm_exec for e in d.values()]:
+                _lib.call("fo_graph_destroy", ex)
+            for e in self.ev_enc + self.ev_llm:
+                _lib.call("fo_event_destroy", e)
+            self.ering.destroy()
+            self.lring.destroy()
+            self.exec = None
+
+
 class TextGraph:
     """One text-decode step for B sessions (A17 reconstruction, the caller contract of
     bin/inference.py:152-179: one token per session in, the next token out) as one captured hipGraph:
@@ -865,14 +1033,18 @@ class ListenPipe:
     Every push must be graphable (same identity and batch, no chat prefix, open caches); the results
     are identical to calling listen() chunk by chunk."""
 
-    def __init__(self, eng):
+    def __init__(self, eng, chunks=1):
         self.eng, self.g, self.pending, self.k = eng, None, None, 0
         self.stopped = False
+        self.C = int(chunks)
+        self.acc = []   # chunks > 1: (items, pe) of the group being assembled in slot k
 
     def push(self, items, decide=None):
         eng = self.eng
         if self.stopped:
             raise RuntimeError("ListenPipe: decide() stopped this pipe (flush and start a new one)")
+        if self.C > 1:
+            return self._push_group(items, decide)
         with torch.cuda.stream(ops.engine_stream(eng.device)):
             if not eng._graphable(items):
                 raise ValueError("ListenPipe.push: items must be steady-state chunks (no chat prefix, open caches)")
@@ -907,8 +1079,77 @@ class ListenPipe:
         self.pending = None
 
     def flush(self):
+        if self.C > 1:
+            return self._flush_group()
         if self.pending is None:
             return None
         with torch.cuda.stream(ops.engine_stream(self.eng.device)):
             k, self.pending = self.pending, None
             return self.g.collect_llm(k)
+
+    # ---- chunks > 1 (ListenGroupGraph): push returns (pe after this chunk, None or the per-chunk result lists of the
+    # previous group, in chunk order); decide() is asked chunk by chunk, and a refusal rolls back every later chunk
+    # already in a stage (the rest of its group and the speculative next group)
+    def _push_group(self, items, decide):
+        eng = self.eng
+        with torch.cuda.stream(ops.engine_stream(eng.device)):
+            if not eng._graphable(items):
+                raise ValueError("ListenPipe.push: items must be steady-state chunks (no chat prefix, open caches)")
+            g = eng._listen_graph_for(items, extra=64 * 2 * self.C, chunks=self.C)
+            if self.g is not None and g is not self.g:
+                raise RuntimeError("ListenPipe: the batch changed (flush before changing sessions)")
+            self.g = g
+            k = self.k
+            pe = g.submit_encoder(items, k, len(self.acc))
+            self.acc.append((items, pe))
+            self.kvs = [it["kv"] for it in items]
+            out = None
+            if len(self.acc) == self.C:
+                g.submit_llm([a for a, _ in self.acc], [p for _, p in self.acc], k)
+                self.acc = []
+                if self.pending is not None:
+                    out = g.collect_llm(self.pending)
+                self.pending = k
+                self.k = 1 - k
+                if decide is not None and out is not None:
+                    self._decide_group(out, decide, newer=[k])
+            return pe, out
+
+    def _decide_group(self, out, decide, newer):
+        """Ask decide() chunk by chunk; on a refusal drop the chunks after it from `out` and from every session's KV,
+        together with every stage in `newer` (waited for first): the context holds exactly the chunks up to the
+        refused one, as in the sequential order."""
+        for j, res in enumerate(out):
+            if decide(res):
+                continue
+            g = self.g
+            drop = (len(out) - 1 - j) * g.To
+            for k in newer:
+                if g.inflight[k] is not None:
+                    _lib.call("fo_event_sync", g.ev_llm[k])
+                    drop += len(g.inflight[k][0]) * g.To
+                    g.inflight[k] = None
+            for kv in self.kvs:
+                kv.truncate(kv.length - drop)
+            del out[j + 1:]
+            self.pending = None
+            self.acc = []
+            self.stopped = True
+            return
+
+    def _flush_group(self):
+        g = self.g
+        if g is None:
+            return None
+        with torch.cuda.stream(ops.engine_stream(self.eng.device)):
+            out = []
+            if self.pending is not None:
+                out += g.collect_llm(self.pending)
+                self.pending = None
+            if self.acc:   # the end of the input: a partial group of m < C chunks
+                k = self.k
+                g.submit_llm([a for a, _ in self.acc], [p for _, p in self.acc], k)
+                self.acc = []
+                out += g.collect_llm(k)
+                self.k = 1 - k
+            return out or None

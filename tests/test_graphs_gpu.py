@@ -152,6 +152,82 @@ def test_listen_pipe_decide_stops_and_rolls_back(eng, dev):
     base.free()
 
 
+def _group_pipe(eng, feats_seq, n_users, C, decide=None):
+    """The bench's order (chunk 0 after apply_chat_prefix, then every chunk through the pipe) with C chunks per
+    Qwen2 stage; returns the per-chunk results in order and the final KV lengths."""
+    base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
+    kvs = [base.fork() for _ in range(n_users)]
+    state = [dict(enc_cache=None, ada_cache=None, pe_index=0) for _ in range(n_users)]
+    out = []
+    pipe = eng.listen_pipe(C)
+
+    def record(groups):
+        for res in groups or []:
+            out.append(([(r["probs"]["state_1"], r["probs"]["state_2"]) for r in res],
+                        [r["hidden_row"][0][r["hidden_row"][1]].cpu().numpy().copy() for r in res],
+                        [r["pe_index"] for r in res]))
+
+    for c, f in enumerate(feats_seq):
+        items = [dict(identity="user", status="ipu_sl" if c == 0 else "ipu_cl", feats=f[u], kv=kvs[u], **state[u])
+                 for u in range(n_users)]
+        if c == 0:
+            items = eng.apply_chat_prefix(items)
+            for u, it in enumerate(items):
+                state[u] = dict(enc_cache=it["enc_cache"], ada_cache=it["ada_cache"], pe_index=it["pe_index"])
+        pe_next, prev = pipe.push(items, decide)
+        for u in range(n_users):
+            state[u]["pe_index"] = pe_next[u]
+        record(prev)
+        if pipe.stopped:
+            break
+    if not pipe.stopped:
+        record(pipe.flush())
+    lens = [kv.length for kv in kvs]
+    for kv in kvs:
+        kv.free()
+    base.free()
+    return out, lens, c
+
+
+@pytest.mark.parametrize("C,n_chunks", [(2, 9), (4, 10), (3, 3)])
+def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
+    """C consecutive chunks per Qwen2 stage (fo.engine.ListenGroupGraph, the offline input's listen): every chunk's
+    state probabilities and last hidden row equal the one-chunk-per-stage pipe's to fp32 rounding (the GEMMs tile C x
+    the rows), its pe_index and the context lengths exactly; a partial last group (n_chunks % C) is flushed."""
+    g = np.load(os.path.join(G, "fbank.npz"))
+    n_users = 3
+    feats = torch.from_numpy(g["A_feats"]).to(dev)
+    seq = [torch.stack([feats[(c + 5 * u) % 13] for u in range(n_users)]) for c in range(n_chunks)]
+    ref, lens_ref, _ = _group_pipe(eng, seq, n_users, 1)
+    got, lens, _ = _group_pipe(eng, seq, n_users, C)
+    assert len(got) == len(ref) == n_chunks and lens == lens_ref
+    for (pr, hr, qr), (pg, hg, qg) in zip(ref, got):
+        assert qr == qg
+        np.testing.assert_allclose(np.array(pg), np.array(pr), atol=2e-5)
+        for a, b in zip(hg, hr):
+            np.testing.assert_allclose(a, b, atol=5e-5, rtol=1e-4)
+
+
+def test_listen_group_pipe_decide_rolls_back_the_rest(eng, dev):
+    """A refusal on chunk 4 (the second chunk of group 2 at C = 3; group 3 already queued) leaves exactly chunks
+    0..4 in the context, as the one-chunk pipe's refusal does."""
+    g = np.load(os.path.join(G, "fbank.npz"))
+    n_users = 2
+    feats = torch.from_numpy(g["A_feats"]).to(dev)
+    seq = [torch.stack([feats[(c + 3 * u) % 13] for u in range(n_users)]) for c in range(12)]
+    seen = []
+
+    def decide(res):
+        seen.append(1)
+        return len(seen) < 5     # refuse chunk 4
+    got, lens, last = _group_pipe(eng, seq, n_users, 3, decide)
+    ref, lens_ref, _ = _group_pipe(eng, seq[:5], n_users, 1)
+    assert len(got) == 5 and lens == lens_ref
+    for (pr, _, qr), (pg, _, qg) in zip(ref, got):
+        assert qr == qg
+        np.testing.assert_allclose(np.array(pg), np.array(pr), atol=2e-5)
+
+
 def _text_run(eng, graph, n_users, steps, top_k):
     base = eng.system_role("<|im_start|>system\nYou are a helpful assistant.")
     kvs = [base.fork() for _ in range(n_users)]
