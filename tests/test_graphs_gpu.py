@@ -177,11 +177,12 @@ def _group_pipe(eng, feats_seq, n_users, C, decide=None):
         pe_next, prev = pipe.push(items, decide)
         for u in range(n_users):
             state[u]["pe_index"] = pe_next[u]
-        record(prev)
+        record([prev] if C == 1 and prev is not None else prev)
         if pipe.stopped:
             break
     if not pipe.stopped:
-        record(pipe.flush())
+        last = pipe.flush()
+        record([last] if C == 1 and last is not None else last)
     lens = [kv.length for kv in kvs]
     for kv in kvs:
         kv.free()
