@@ -455,6 +455,20 @@ class FreezeOmniEngine:
         return g
 
 
+def _rows_of_one_tensor(items, n):
+    """The items' feature tensors are consecutive [R, 80] rows of ONE storage (a batched fbank's output), so one
+    strided copy takes them all.  Separate tensors that merely sit next to each other in the caching allocator's
+    memory (each session's features uploaded on its own) do not qualify: a view over the first one's storage would
+    run past its end."""
+    f0 = items[0]["feats"]
+    st = f0.untyped_storage()
+    base, size = st.data_ptr(), st.nbytes()
+    return (f0.data_ptr() - base + len(items) * n * 4 <= size and
+            all(it["feats"].is_contiguous() and it["feats"].numel() == n and
+                it["feats"].untyped_storage().data_ptr() == base and
+                it["feats"].data_ptr() == f0.data_ptr() + b * n * 4 for b, it in enumerate(items)))
+
+
 class _HostRing:
     """Pinned host staging buffers for one metadata block, reused once their upload has run."""
 
@@ -525,10 +539,7 @@ class EncoderGraph:
         with torch.cuda.stream(st):
             # the duplex tick's batched fbank puts one identity's rows next to each other (deliver_deferred): one copy
             f0, n = items[0]["feats"], self.R * 80
-            base = f0.untyped_storage().data_ptr()
-            if all(it["feats"].is_contiguous() and it["feats"].numel() == n and
-                   it["feats"].untyped_storage().data_ptr() == base and
-                   it["feats"].data_ptr() == f0.data_ptr() + b * n * 4 for b, it in enumerate(items)):
+            if _rows_of_one_tensor(items, n):
                 self.feats.copy_(f0.as_strided((B, self.R, 80), (n, 80, 1)))
             else:
                 for b, it in enumerate(items):
@@ -657,8 +668,7 @@ class ListenGraph:
             _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_llm[k])  # slot k's last reader is done
         with torch.cuda.stream(st):
             f0 = items[0]["feats"]
-            if f0.is_contiguous() and all(it["feats"].data_ptr() == f0.data_ptr() + b * self.R * 80 * 4
-                                          for b, it in enumerate(items)):
+            if _rows_of_one_tensor(items, self.R * 80):
                 self.feats.copy_(f0.as_strided((B, self.R, 80), (self.R * 80, 80, 1)))  # one batched tensor
             else:
                 for b, it in enumerate(items):
@@ -751,8 +761,9 @@ class ListenGroupGraph:
         self.eng, self.ident, self.B, self.R, self.max_keys, self.C = eng, ident, B, R, max_keys, C
         enc, ada, llm = eng.enc[ident], eng.ada[ident], eng.llm
         self.enc, self.ada, self.llm = enc, ada, llm
-        self.feats = torch.empty(B, R, 80, dtype=F32, device=dev)
-        self.eb = enc.buffers(B, R)
+        # the group's features, chunk-major ([chunk][session] windows): each push copies its chunk's rows in
+        self.feats = torch.empty(C * B, R, 80, dtype=F32, device=dev)
+        self.eb = enc.buffers(C * B, R)
         self.T = enc.dims(R)[2]
         self.ab = ada.buffers(B, self.T)
         self.To = To = ada.out_len(self.T)
@@ -762,11 +773,13 @@ class ListenGroupGraph:
         self.n = n = C * n1
         PS = llm.pool.PS
         self.maxb = (max_keys + PS - 1) // PS
-        self.emeta_d = torch.zeros(5 * B, dtype=I32, device=dev)
+        # encoder metadata [chunk j: enc 4B] x C | ada slots B -- filled chunk by chunk on the host, uploaded once
+        self.emeta_d = torch.zeros(4 * B * C + B, dtype=I32, device=dev)
+        self.hmeta = np.zeros(4 * B * C + B, np.int32)
         self.lmeta_d = torch.zeros(3 * n + B * self.maxb, dtype=I32, device=dev)
-        self.ering, self.lring = _HostRing(5 * B), _HostRing(3 * n + B * self.maxb)
-        self.eb["meta"] = self.emeta_d[0:4 * B]
-        self.ab["slots"] = self.emeta_d[4 * B:5 * B]
+        self.ering, self.lring = _HostRing(4 * B * C + B), _HostRing(3 * n + B * self.maxb)
+        self.eb["meta"] = self.emeta_d[0:4 * B * C]
+        self.ab["slots"] = self.emeta_d[4 * B * C:]
         lm = self.lmeta_d
         self.items = torch.tensor([[b, j * n1 + b * To, To] for j in range(C) for b in range(B)],
                                   dtype=I32).reshape(-1).to(dev)
@@ -785,18 +798,23 @@ class ListenGroupGraph:
         self.inflight = [None, None]
         self.main = ops.engine_stream(dev)
         self.side = ops.engine_stream(dev, side=True)
-        self.enc_exec = [[ListenGraph._capture(self.side, lambda k=k, j=j: self._enc_body(k, j), ENC_GEMM_TUNE)
-                          for j in range(C)] for k in range(2)]
+        self.enc_exec = [{}, {}]   # slot -> {chunks in the group: captured encoder stage}
         self.llm_exec = [{}, {}]   # slot -> {chunks in the group: captured LLM stage}
+        self.enc_todo = [0, 0]     # chunks whose features are in the slot but whose encoder stage is not queued
         self.ev_enc = [ListenGraph._event() for _ in range(2)]
         self.ev_llm = [ListenGraph._event() for _ in range(2)]
         self.llm_used = [False, False]
         self.exec = True
 
-    def _enc_body(self, k, j):
-        xe, T = self.enc.run(self.feats, self.B, self.R, self.eb)
-        emb, To = self.ada.run(xe, self.B, T, self.ab)
-        ops.gather_rows(emb, None, out=self.xs[k][j * self.n1:(j + 1) * self.n1], round_fp16=True)   # .half()
+    def _enc_body(self, k, m):
+        """The encoder stage of m chunks: one encoder pass over all their rows (SpeechEncoderEngine.run(chunks=m)),
+        then the adapter chunk by chunk (its causal conv cache carries from one to the next), each chunk's rows
+        rounded to fp16 into its block of x slot k."""
+        B, ne = self.B, self.B * self.T
+        xe, T = self.enc.run(self.feats, B, self.R, self.eb, chunks=m)
+        for j in range(m):
+            emb, To = self.ada.run(xe[j * ne:(j + 1) * ne], B, T, self.ab)
+            ops.gather_rows(emb, None, out=self.xs[k][j * self.n1:(j + 1) * self.n1], round_fp16=True)   # .half()
 
     def _llm_body(self, k, m):
         llm, x = self.llm, self.xs[k][:m * self.n1]
@@ -806,36 +824,54 @@ class ListenGroupGraph:
             ops.state_head(x, self.rows[:m * self.B], llm.head_w, llm.head_b, self.probs)
 
     def submit_encoder(self, items, k, j):
-        """Chunk j of the group in slot k: its encoder stage (side stream) into rows j of x slot k.  Advances the
-        encoder caches; returns the per-session pe_index after this chunk."""
+        """Chunk j of the group in slot k: its ring / position metadata (the encoder caches advanced as the
+        sequential order does) and its features into the slot's group buffers; the group's encoder stage (side
+        stream) is queued with its last chunk (launch_encoder).  Returns the per-session pe_index after this chunk."""
         B = self.B
         caches = [it["enc_cache"] for it in items]
         emeta, new_pe = self.enc.host_meta(caches, [it["pe_index"] or 0 for it in items])
-        q, h = self.ering.next()
-        h[0:4 * B] = emeta
-        h[4 * B:5 * B] = [it["ada_cache"].slot for it in items]
+        self.hmeta[4 * B * j:4 * B * (j + 1)] = emeta
+        if j == 0:
+            self.hmeta[4 * B * self.C:] = [it["ada_cache"].slot for it in items]
         st = self.side
         if j == 0 and self.llm_used[k]:
             _lib.call("fo_stream_wait_event", st.cuda_stream, self.ev_llm[k])   # slot k's last reader is done
         with torch.cuda.stream(st):
-            f0 = items[0]["feats"]
-            if f0.is_contiguous() and all(it["feats"].data_ptr() == f0.data_ptr() + b * self.R * 80 * 4
-                                          for b, it in enumerate(items)):
-                self.feats.copy_(f0.as_strided((B, self.R, 80), (self.R * 80, 80, 1)))
+            dst = self.feats[j * B:(j + 1) * B]
+            if _rows_of_one_tensor(items, self.R * 80):
+                dst.copy_(items[0]["feats"].as_strided((B, self.R, 80), (self.R * 80, 80, 1)))
             else:
                 for b, it in enumerate(items):
-                    self.feats[b].copy_(it["feats"])
-        self.ering.upload(q, self.emeta_d, st)
-        _lib.call("fo_graph_launch", self.enc_exec[k][j], st.cuda_stream)
-        _lib.call("fo_event_record", self.ev_enc[k], st.cuda_stream)
+                    dst[b].copy_(it["feats"])
         self.enc.advance(caches, self.T)
+        self.enc_todo[k] = j + 1
+        if j + 1 == self.C:
+            self.launch_encoder(k)
         return new_pe
+
+    def launch_encoder(self, k):
+        """Queue slot k's encoder stage over the chunks submitted to it (C, or fewer at the end of the input)."""
+        m = self.enc_todo[k]
+        if m == 0:
+            return
+        ex = self.enc_exec[k].get(m)
+        if ex is None:
+            ex = self.enc_exec[k][m] = ListenGraph._capture(self.side, lambda: self._enc_body(k, m), ENC_GEMM_TUNE)
+        q, h = self.ering.next()
+        h[:] = self.hmeta
+        st = self.side
+        self.ering.upload(q, self.emeta_d, st)
+        _lib.call("fo_graph_launch", ex, st.cuda_stream)
+        _lib.call("fo_event_record", self.ev_enc[k], st.cuda_stream)
+        self.enc_todo[k] = 0
 
     def submit_llm(self, groups, pes, k):
         """The LLM stage of the m = len(groups) chunks whose encoder stages filled slot k (engine stream); appends
         m * To KV rows per session.  collect_llm(k) reads its results."""
         B, To, n1, n, maxb = self.B, self.To, self.n1, self.n, self.maxb
         m = len(groups)
+        if self.enc_todo[k]:   # a partial group (the end of the input): its encoder stage is queued now
+            self.launch_encoder(k)
         ex = self.llm_exec[k].get(m)
         if ex is None:
             ex = self.llm_exec[k][m] = ListenGraph._capture(self.main, lambda: self._llm_body(k, m))
@@ -888,7 +924,7 @@ class ListenGroupGraph:
 
     def destroy(self):
         if self.exec is not None:
-            for ex in [e for row in self.enc_exec for e in row] + [e for d in self.llm_exec for e in d.values()]:
+            for ex in [e for d in self.enc_exec + self.llm_exec for e in d.values()]:
                 _lib.call("fo_graph_destroy", ex)
             for e in self.ev_enc + self.ev_llm:
                 _lib.call("fo_event_destroy", e)

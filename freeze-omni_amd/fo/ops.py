@@ -490,7 +490,8 @@ def im2col_3x3s2(x, B, C, H, W, strides, out, mean=None, istd=None):
 
 def subsample(feats, B, R, F, mean, istd, w1, b1, C, y1, w2p, b2, z):
     """Conv2dSubsampling4 (+ GlobalCMVN) up to its output Linear: feats [B, R, F] -> z [B * H2, C * W2]
-    (fo_subsample; split-K scratch at the tail of the stream's Runtime workspace)."""
+    (fo_subsample; split-K scratch at the HEAD of the stream's Runtime workspace -- the same floats the GEMMs' split-K
+    slabs use, which is safe because launches on one stream run in order)."""
     n = int(_lib.load().fo_subsample_ws_floats(B, R, F, C))
     rt = Runtime.get(feats.device)
     if n > rt.ws.numel():

@@ -262,20 +262,30 @@ class SpeechEncoderEngine:
             c.start = (c.start + total - keep) % self.cap
             c.len = keep
 
-    def run(self, feats, B, R, bufs):
-        """The device part of infer(): bufs from buffers(B, R) with bufs['meta'] already uploaded."""
+    def run(self, feats, B, R, bufs, chunks=1):
+        """The device part of infer(): bufs from buffers(B, R) with bufs['meta'] already uploaded.
+        chunks > 1: `chunks` consecutive chunks of the same B sessions in one pass (an offline input's listen,
+        fo.engine.ListenGroupGraph): feats [chunks * B, R, 80] chunk-major, bufs from buffers(chunks * B, R), meta
+        [chunks][4 B] (each chunk's ring / position metadata, host_meta after the chunks before it).  Every row-wise
+        step (the Conv2dSubsampling4 front end -- each chunk's window carries its own context frames --, the embed,
+        the norms, q|k|v, linear_out, the FFN) runs once over all the rows; the rel-pos attention runs chunk by chunk
+        in order, each launch appending its chunk's K / V to the ring the next one reads (attention.py:407-459), so
+        chunk j sees exactly the left context the sequential order gives it."""
         H1, W1, H2, W2 = self.dims(R)
         T, C = H2, self.C
-        ops.subsample(feats, B, R, 80, self.mean, self.istd, self.conv1_w, self.conv1_b, C, bufs["y1"],
+        N = B * chunks
+        ops.subsample(feats, N, R, 80, self.mean, self.istd, self.conv1_w, self.conv1_b, C, bufs["y1"],
                       self.conv2.packed, self.conv2.bias, bufs["z"])
-        self.out(bufs["z"], out=bufs["o"])
-        x = self.embed(bufs["o"], out=bufs["x"])
-        ops.layernorm(x, *self.embed_ln, out=x, relu=True)
-        ops.scale_(x, math.sqrt(self.d))
+        self.out(bufs["z"], out=bufs["o"], M=N * T)
+        x = self.embed(bufs["o"], out=bufs["x"], M=N * T)
+        ops.layernorm(x, *self.embed_ln, out=x, relu=True, M=N * T)
+        ops.scale_(x[:N * T], math.sqrt(self.d))
         meta = bufs["meta"]
-        st, ln, rg, ps = meta[:B], meta[B:2 * B], meta[2 * B:3 * B], meta[3 * B:]
         h, qkv, att, f = bufs["h"], bufs["qkv"], bufs["att"], bufs["f"]
         scale = 1.0 / math.sqrt(self.dk)
+        if chunks > 1:
+            return self._run_chunks(x, B, T, chunks, bufs, meta, scale)
+        st, ln, rg, ps = meta[:B], meta[B:2 * B], meta[2 * B:3 * B], meta[3 * B:]
         # pre-norms applied by the GEMMs on load (fo_gemm_ln) from the residual producers' row sums
         fuse_ln = B * T <= 64 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
         sA, sB = bufs["sA"], bufs["sB"]
@@ -320,6 +330,44 @@ class SpeechEncoderEngine:
                                        L["bu"], L["bv"], B, T, self.h, self.dk, scale, att, opack=attp)
             if fuse_ln:
                 L["out"].rowstats(att, x, sB, residual=True, xpack=attp, ypack32=xp32)
+                L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp, xpack32=xp32)
+            else:
+                L["out"](att, out=x, residual=True)
+                ops.layernorm(x, *L["ln2"], out=h)
+                L["ff1"](h, out=f, act="relu")
+            if fuse_ln and i < last:
+                L["ff2"].rowstats(f, x, sA, residual=True, xpack=fp, ypack32=xp32)
+            else:
+                L["ff2"](f, out=x, residual=True, xpack=fp)
+        ops.layernorm(x, *self.after, out=x)
+        return x, T
+
+    def _run_chunks(self, x, B, T, chunks, bufs, meta, scale):
+        """run(chunks > 1): the blocks over chunks * B * T rows, the attention chunk by chunk (rows chunk-major)."""
+        N = B * chunks
+        M = N * T
+        n1 = B * T
+        h, qkv, att, f = bufs["h"][:M], bufs["qkv"][:M], bufs["att"][:M], bufs["f"][:M]
+        fuse_ln = M <= 64 and os.environ.get("FO_ENC_LN_ON_LOAD", "1") != "0"
+        sA, sB = bufs["sA"], bufs["sB"]
+        # (the attention output is written per chunk, so it is not packed for linear_out: the packed image's rows are
+        # the launch's own)
+        fp, xp32 = (bufs.get("fp"), bufs.get("xp32")) if fuse_ln else (None, None)
+        last = len(self.layers) - 1
+        x = x[:M]
+        for i, L in enumerate(self.layers):
+            if fuse_ln and i > 0:
+                L["qkv"].ln(x, *L["ln1"], sA, out=qkv, xpack32=xp32)
+            else:
+                ops.layernorm(x, *L["ln1"], out=h)
+                L["qkv"](h, out=qkv)
+            for j in range(chunks):
+                mj = meta[4 * B * j:4 * B * (j + 1)]
+                ops.relpos_attention_fused(qkv[j * n1:(j + 1) * n1], self.kr[i], self.vr[i], self.cap, mj[:B],
+                                           mj[B:2 * B], mj[2 * B:3 * B], self.ptab[i], mj[3 * B:], L["bu"], L["bv"],
+                                           B, T, self.h, self.dk, scale, att[j * n1:(j + 1) * n1])
+            if fuse_ln:
+                L["out"].rowstats(att, x, sB, residual=True, ypack32=xp32)
                 L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp, xpack32=xp32)
             else:
                 L["out"](att, out=x, residual=True)

@@ -19,7 +19,8 @@ from .ops import F32, PackedLinear
 # FO_ATTN_DENSE=0 passes the item table even for one-token-per-sequence batches (A/B against a
 # library older than fo_attention's items == NULL form)
 ATTN_DENSE = os.environ.get("FO_ATTN_DENSE", "1") == "1"
-# FO_ATTN_O=0: the decode attention and the o projection as two launches (A/B against k_attn_decode_o)
+# FO_ATTN_O=1 (opt-in, A/B only): the decode attention fused with the o projection (k_attn_decode_o); the default (0)
+# runs them as two launches, which measured faster
 ATTN_O = os.environ.get("FO_ATTN_O", "0") == "1"
 # FO_XPACK_SMALL=1: packed q|k|v / o inputs also at <= 8 rows for wide stacks (the Qwen2 text step; A/B)
 XPACK_SMALL = os.environ.get("FO_XPACK_SMALL", "0") == "1"

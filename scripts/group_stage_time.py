@@ -62,7 +62,7 @@ for C in Cs:
         g.collect_llm(0)
         for j in range(C):
             g.submit_encoder(items, 1, j)
-        llm_ex, enc_ex = g.llm_exec[0][C], g.enc_exec[1]
+        llm_ex, enc_ex = g.llm_exec[0][C], [g.enc_exec[1][C]]
     torch.cuda.synchronize()
     main, side = g.main.cuda_stream, g.side.cuda_stream
 
@@ -78,6 +78,8 @@ for C in Cs:
 
     t = timed(llm_only, main)
     tb = timed(both, main)
+    te = timed(lambda: [_lib.call("fo_graph_launch", ex, main) for ex in enc_ex], main)
+    print(f"C={C}: encoder stage {te:8.1f} us for {C} chunk(s) = {te / C:7.1f} us/chunk", flush=True)
     print(f"C={C}: Qwen2 stage {t:8.1f} us for {C} chunk(s) = {t / C:7.1f} us/chunk "
           f"({wb / t / 1e6:.2f} TB/s over the layer weights); with the encoder stages beside it {tb:8.1f} us = "
           f"{tb / C:7.1f} us/chunk", flush=True)

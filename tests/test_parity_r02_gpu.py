@@ -223,6 +223,47 @@ def test_real_geometry_encoder_adapter_match_reference(dev):
             close(emb, ref, rtol=2e-3, atol=2e-3 * float(np.abs(ref).max()))
 
 
+@pytest.mark.parametrize("C", [4, 3])
+def test_real_geometry_encoder_chunk_groups_match_reference(dev, C):
+    """SpeechEncoderEngine.run(chunks=C) (the offline listen's encoder stage, fo.engine.ListenGroupGraph): C
+    consecutive chunks of 2 sessions in one pass -- the front end, norms and GEMMs over all C x B x T rows, the rel-pos
+    attention chunk by chunk on the ring -- against the reference's chunk-by-chunk outputs: framing A for 20 chunks
+    (the 64-frame ring fills and trims inside a group), framing B for 8 chunks across the RelPE wrap (a partial last
+    group); then the adapter chunk by chunk on the group's rows."""
+    from fo.speech import AdapterEngine, SpeechEncoderEngine
+    g = load("real_encoder_t2.npz")
+    src = _t2_source(dev, {**encoder_shapes(T2, "user"), **adapter_shapes(T2, "user")})
+    enc = SpeechEncoderEngine(src, T2, "user", dev, max_sessions=8)
+    ada = AdapterEngine(src, T2, "user", dev, max_sessions=8)
+    B = 2
+    for kind in ("A", "B"):
+        feats = g[f"{kind}_feats"]
+        n = feats.shape[0]
+        ecs, acs, pes = [enc.new_cache() for _ in range(B)], [ada.new_cache() for _ in range(B)], [int(g[f"{kind}_pe0"])] * B
+        R = feats.shape[1]
+        T = enc.dims(R)[2]
+        for c0 in range(0, n, C):
+            m = min(C, n - c0)
+            f = torch.from_numpy(np.concatenate([np.repeat(feats[c0 + j][None], B, 0) for j in range(m)])).to(dev)
+            bufs = enc.buffers(m * B, R)
+            metas = []
+            for j in range(m):
+                meta, pes = enc.host_meta(ecs, pes)
+                metas.append(meta)
+                enc.advance(ecs, T)
+                assert pes == [int(g[f"{kind}_pe"][c0 + j])] * B
+            bufs["meta"].copy_(torch.from_numpy(np.concatenate(metas)).to(dev))
+            out, T2_ = enc.run(f.contiguous(), B, R, bufs, chunks=m)
+            assert T2_ == T
+            for j in range(m):
+                ref_e, ref_a = g[f"{kind}_enc"][c0 + j], g[f"{kind}_ada"][c0 + j]
+                rows = out[j * B * T:(j + 1) * B * T]
+                emb, To = ada(rows, T, acs)
+                for b in range(B):
+                    close(rows[b * T:(b + 1) * T], ref_e, rtol=2e-3, atol=2e-3 * float(np.abs(ref_e).max()))
+                    close(emb[b * To:(b + 1) * To], ref_a, rtol=2e-3, atol=2e-3 * float(np.abs(ref_a).max()))
+
+
 @pytest.mark.parametrize("fused", [2, 1, 0])
 def test_real_geometry_batched_framing_b_encoder_matches_reference(dev, fused):
     """The duplex tick's encoder shape at real geometry: 8 copies of real_encoder_t2's framing-B session in ONE batch
