@@ -153,6 +153,9 @@ class AudioLLM:
         out = []
         for (speech, ex), r in zip(requests, res):
             out.append((r["probs"], ex["past_key_values"], r["ada_cache"], r["enc_cache"], r["pe_index"]))
+            # (buffer, row) of the last request's final hidden row (a probe for single-caller tests: the buffer is the
+            # engine's and is rewritten by the next listen)
+            self._last_hidden = r["hidden_row"]
         return out
 
     # ------------------------------------------------------------------ models/audioLLM.py:431-477
