@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="listen chunk by chunk (default: encoder stage of chunk c+1 overlaps the LLM of chunk c)")
-    ap.add_argument("--listen-chunks", type=int, default=int(os.environ.get("FO_LISTEN_CHUNKS", "1")),
+    ap.add_argument("--listen-chunks", type=int, default=int(os.environ.get("FO_LISTEN_CHUNKS", "4")),
                     help="consecutive 160 ms chunks of the offline input per Qwen2 stage (fo.engine.ListenGroupGraph; "
                          "1: one chunk per stage)")
     ap.add_argument("--scenario", default="turn", choices=["turn", "duplex"],

@@ -193,8 +193,9 @@ def _group_pipe(eng, feats_seq, n_users, C, decide=None):
 @pytest.mark.parametrize("C,n_chunks", [(2, 9), (4, 10), (3, 3)])
 def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
     """C consecutive chunks per Qwen2 stage (fo.engine.ListenGroupGraph, the offline input's listen): every chunk's
-    state probabilities and last hidden row equal the one-chunk-per-stage pipe's to fp32 rounding (the GEMMs tile C x
-    the rows), its pe_index and the context lengths exactly; a partial last group (n_chunks % C) is flushed."""
+    state probabilities (2e-5) and last hidden row (1e-4 of the row's scale) equal the one-chunk-per-stage pipe's to fp32
+    rounding (the encoder and Qwen2 GEMMs tile C x the rows), its pe_index and the context lengths exactly; a partial
+    last group (n_chunks % C) is flushed."""
     g = np.load(os.path.join(G, "fbank.npz"))
     n_users = 3
     feats = torch.from_numpy(g["A_feats"]).to(dev)
@@ -206,7 +207,8 @@ def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
         assert qr == qg
         np.testing.assert_allclose(np.array(pg), np.array(pr), atol=2e-5)
         for a, b in zip(hg, hr):
-            np.testing.assert_allclose(a, b, atol=5e-5, rtol=1e-4)
+            # (the grouped encoder runs its norms and GEMMs over C x the rows: other kernels, fp32 rounding apart)
+            np.testing.assert_allclose(a, b, atol=1e-4 * float(np.abs(b).max()), rtol=1e-4)
 
 
 def test_listen_group_pipe_decide_rolls_back_the_rest(eng, dev):
