@@ -15,6 +15,7 @@
 #   duplex     the config-5 duplex line                                  -> <tag>_duplex.json
 #   profdup    rocprofv3 kernel trace + stats of a 20 s duplex run       -> <tag>_profdup/, <tag>_profdup_table.txt
 #   profstage  rocprofv3 kernel trace of scripts/llm_stage_time.py (LLM / encoder stage replays) -> <tag>_profstage_table.txt
+#   profgroup  rocprofv3 kernel trace of scripts/group_stage_time.py $GROUP_C (grouped listen stages) -> <tag>_profgroup_table.txt
 #   rehearsal  the N = 2 path on one GPU (FO_DIST_REHEARSAL, gloo)      -> <tag>_rehearsal_n2.json
 #   vocpmc     vocoder: MFMA counter passes + FETCH_SIZE + kernel trace of one 8-user call -> <tag>_vocoder_mfma.json
 #   ddp1       bench.py as one torch.distributed.run rank (world 1: RCCL init, broadcast, checksum) -> <tag>_ddp1.json
@@ -66,6 +67,9 @@ for S in "$@"; do
     profstage) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_profstage -o stage -f csv -- \
              python3 $ROOTD/scripts/llm_stage_time.py) > ${O}_profstage.log 2>&1; rc=$?
              [ $rc -eq 0 ] && python3 scripts/trace_table.py ${O}_profstage 45 stage > ${O}_profstage_table.txt 2>&1; head -48 ${O}_profstage_table.txt ;;
+    profgroup) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_profgroup -o stage -f csv -- \
+             python3 $ROOTD/scripts/group_stage_time.py ${GROUP_C:-4}) > ${O}_profgroup.log 2>&1; rc=$?
+             [ $rc -eq 0 ] && python3 scripts/trace_table.py ${O}_profgroup 60 stage > ${O}_profgroup_table.txt 2>&1; head -62 ${O}_profgroup_table.txt ;;
     text)  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof_text -o text -f csv -- \
              python3 $ROOTD/scripts/text_step_time.py) > ${O}_prof_text.log 2>&1; rc=$? ;;
     duplex) timeout -k 10 400 python -u bench.py --scenario duplex --out ${O}_duplex.json > ${O}_duplex.log 2>&1; rc=$?
