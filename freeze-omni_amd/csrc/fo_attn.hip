@@ -530,6 +530,151 @@ __global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq,
   }
 }
 
+// k_relpos_fused over C consecutive chunks of the same users in ONE launch (the offline listen's grouped encoder,
+// SpeechEncoderEngine.run(chunks=C)): per (user, head) the chunks run in order, each with its own ring / position
+// metadata (meta[chunk][start B | len B | ring B | pstart B], host_meta after the chunks before it) and the chunk's
+// rows of the group's q|k|v output (chunk-major: row (j * B + b) * T + i).  The ring rows that chunks < j of this
+// launch appended are read from their q|k|v rows, never re-read from the ring this launch writes (so no global
+// write-then-read inside the launch); every chunk still appends its rows to the ring for the launches after it.
+// Chunk j sees exactly the left context the sequential per-chunk launches give it.
+__global__ __launch_bounds__(256) void k_relpos_chunks(const float* qkv, int ldq, float* kr, float* vr, int cap,
+                                                       const int* meta, int B, int C, const float* ptab,
+                                                       const float* bu, const float* bv, int T, int h, int dk,
+                                                       float scale, float* out, int ldo) {
+  extern __shared__ float smem[];
+  const int KP = dk + 4;
+  float* k_s = smem;
+  float* v_s = k_s + cap * KP;
+  float* p_s = v_s + cap * KP;
+  float* qu = p_s + cap * KP;
+  float* qv = qu + T * dk;
+  float* sc = qv + T * dk;
+  const int b = blockIdx.x, hh = blockIdx.y;
+  const int d = h * dk;
+  const int D4 = dk / 4;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr int RB_ = 8;
+  for (int jc = 0; jc < C; ++jc) {
+    const int* m = meta + (size_t)jc * 4 * B;
+    const size_t rb = (size_t)m[2 * B + b];
+    const int Lold = m[B + b], Lk = Lold + T;
+    const int st = m[b];
+    const int ps = m[3 * B + b];
+    const size_t row0 = ((size_t)jc * B + b) * T;   // this chunk's first q|k|v row
+    float qx[2], qbu[2], qbv[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = threadIdx.x + r * 256;
+      const int i = e < T * dk ? e / dk : 0, c = e < T * dk ? e % dk : 0;
+      qx[r] = qkv[(row0 + i) * ldq + hh * dk + c];
+      qbu[r] = bu[hh * dk + c];
+      qbv[r] = bv[hh * dk + c];
+    }
+    for (int e0 = 0; e0 < Lk * D4; e0 += RB_ * 256) {
+      v4f kk[RB_], vv[RB_], pp[RB_];
+#pragma unroll
+      for (int q = 0; q < RB_; ++q) {
+        const int e = e0 + q * 256 + threadIdx.x;
+        const bool on = e < Lk * D4;
+        const int j = on ? e / D4 : 0, c = on ? (e % D4) * 4 : 0;
+        // row j of the context: the chunk's own (j >= Lold), one an earlier chunk of this launch appended (age <
+        // jc * T), or one in the ring from before the launch
+        const int age = Lold - 1 - j;
+        const float* src;
+        const float* ksrc;
+        const float* vsrc;
+        if (j >= Lold) {
+          src = qkv + (row0 + (j - Lold)) * ldq + hh * dk + c;
+          ksrc = src + d;
+          vsrc = src + 2 * d;
+        } else if (age < jc * T) {
+          const int jj = jc - 1 - age / T, t = T - 1 - age % T;
+          src = qkv + (((size_t)jj * B + b) * T + t) * ldq + hh * dk + c;
+          ksrc = src + d;
+          vsrc = src + 2 * d;
+        } else {
+          const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
+          ksrc = kr + ro;
+          vsrc = vr + ro;
+        }
+        kk[q] = *reinterpret_cast<const v4f*>(ksrc);
+        vv[q] = *reinterpret_cast<const v4f*>(vsrc);
+        pp[q] = *reinterpret_cast<const v4f*>(ptab + (size_t)(ps + j) * d + hh * dk + c);
+      }
+#pragma unroll
+      for (int q = 0; q < RB_; ++q) {
+        const int e = e0 + q * 256 + threadIdx.x;
+        if (e < Lk * D4) {
+          const int j = e / D4, c = (e % D4) * 4;
+          if (j >= Lold) {   // the chunk's new rows enter the ring (for the launches after this one)
+            const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
+            *reinterpret_cast<v4f*>(kr + ro) = kk[q];
+            *reinterpret_cast<v4f*>(vr + ro) = vv[q];
+          }
+          *reinterpret_cast<v4f*>(k_s + j * KP + c) = kk[q];
+          *reinterpret_cast<v4f*>(v_s + j * KP + c) = vv[q];
+          *reinterpret_cast<v4f*>(p_s + j * KP + c) = pp[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = threadIdx.x + r * 256;
+      if (e < T * dk) {
+        qu[e] = qx[r] + qbu[r];
+        qv[e] = qx[r] + qbv[r];
+      }
+    }
+    for (int e = threadIdx.x + 512; e < T * dk; e += blockDim.x) {
+      const int i = e / dk, c = e % dk;
+      const float x = qkv[(row0 + i) * ldq + hh * dk + c];
+      qu[i * dk + c] = x + bu[hh * dk + c];
+      qv[i * dk + c] = x + bv[hh * dk + c];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < T * Lk; e += blockDim.x) {
+      const int i = e / Lk, j = e % Lk;
+      const float* kk = k_s + j * KP;
+      const float* pp = p_s + j * KP;
+      const float* a1 = qu + i * dk;
+      const float* a2 = qv + i * dk;
+      float s1 = 0.f, s2 = 0.f;
+      for (int c = 0; c < dk; c += 4) {
+        const float4 k4 = *reinterpret_cast<const float4*>(kk + c), p4 = *reinterpret_cast<const float4*>(pp + c);
+        const float4 u4 = *reinterpret_cast<const float4*>(a1 + c), w4 = *reinterpret_cast<const float4*>(a2 + c);
+        s1 += u4.x * k4.x + u4.y * k4.y + u4.z * k4.z + u4.w * k4.w;
+        s2 += w4.x * p4.x + w4.y * p4.y + w4.z * p4.z + w4.w * p4.w;
+      }
+      sc[i * cap + j] = (s1 + s2) * scale;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = wave; i < T; i += blockDim.x / 64) {
+      float mx = -INFINITY;
+      for (int j = lane; j < Lk; j += 64) mx = fmaxf(mx, sc[i * cap + j]);
+      mx = wave_max(mx);
+      float sum = 0.f;
+      for (int j = lane; j < Lk; j += 64) {
+        const float e = expf(sc[i * cap + j] - mx);
+        sc[i * cap + j] = e;
+        sum += e;
+      }
+      sum = wave_sum(sum);
+      const float r = 1.f / sum;
+      for (int j = lane; j < Lk; j += 64) sc[i * cap + j] *= r;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < T * dk; e += blockDim.x) {
+      const int i = e / dk, c = e % dk;
+      const float* pr = sc + i * cap;
+      float acc = 0.f;
+      for (int j = 0; j < Lk; ++j) acc += pr[j] * v_s[j * KP + c];
+      out[(row0 + i) * ldo + hh * dk + c] = acc;
+    }
+    __syncthreads();   // the next chunk restages the LDS rows this one reads
+  }
+}
+
 // waves per work group of the multi-row MFMA attention at head_dim 128 (the Qwen2 listen / text rows): 8 (default:
 // 128-key tiles, so a 128-key split loads in one round instead of two) or 4 (64-key tiles); FO_ATTN_NW.  r03t
 // (scripts/attn_kps_sweep.py, 8 sessions, graph-replayed): 2 tokens x 200 keys 18.0 -> 15.2 us, 400 keys 21.2 ->
@@ -707,6 +852,20 @@ int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, i
   fo::count_launch(FO_L_RELPOS);
   if (oph) fo::count_launch(FO_L_ATTN_OPACK);
   return fo::check_launch("fo_relpos_attention_fused");
+}
+
+int fo_relpos_attention_chunks(const float* qkv, int ldq, float* kr, float* vr, int cap, const int* meta, int B, int C,
+                               const float* ptab, const float* bu, const float* bv, int T, int h, int dk, float scale,
+                               float* out, int ldo, hipStream_t s) {
+  FO_REQUIRE(B >= 1 && C >= 1 && T >= 1 && T <= cap && dk % 4 == 0 && (ldq % 4) == 0,
+             "fo_relpos_attention_chunks: B=%d C=%d T=%d dk=%d", B, C, T, dk);
+  FO_REQUIRE(C * T <= cap, "fo_relpos_attention_chunks: %d chunks of %d frames exceed the ring (%d)", C, T, cap);
+  const size_t lds = (size_t)(3 * cap * (dk + 4) + 2 * T * dk + T * cap) * sizeof(float);
+  FO_REQUIRE(lds <= 160 * 1024, "fo_relpos_attention_chunks: ring of %d x %d exceeds LDS", cap, dk);
+  hipLaunchKernelGGL(k_relpos_chunks, dim3(B, h), dim3(256), lds, s, qkv, ldq, kr, vr, cap, meta, B, C, ptab, bu, bv,
+                     T, h, dk, scale, out, ldo);
+  fo::count_launch(FO_L_RELPOS);
+  return fo::check_launch("fo_relpos_attention_chunks");
 }
 
 int fo_relpos_attention(const float* q, int ldq, const float* kr, const float* vr, int cap, const int* start,

@@ -121,6 +121,8 @@ _SIGS = {
     "fo_enc_kv_write": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "fo_relpos_attention_fused": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_int, c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),
+    "fo_relpos_attention_chunks": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                           c_int, c_int, c_float, c_vp, c_int, c_vp]),
     "fo_relpos_attention": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                     c_int, c_int, c_int, c_float, c_vp, c_int, c_vp]),
     "fo_fbank": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,

@@ -701,6 +701,16 @@ def _relpos_fused_call(qkv, kr, vr, cap, start, length, ring, ptab, pstart, bu, 
               bv.data_ptr(), B, T, h, dk, float(scale), out.data_ptr(), out.stride(0), stream(qkv.device))
 
 
+def relpos_attention_chunks(qkv, kr, vr, cap, meta, B, C, ptab, bu, bv, T, h, dk, scale, out):
+    """C consecutive chunks of B users' rel-pos attention in one launch (fo_relpos_attention_chunks); meta [C * 4 B]."""
+    if meta.numel() < 4 * B * C or qkv.shape[0] < B * C * T or out.shape[0] < B * C * T:
+        raise ValueError("relpos_attention_chunks: meta / q|k|v / out smaller than C chunks of B users x T rows")
+    _lib.call("fo_relpos_attention_chunks", qkv.data_ptr(), qkv.stride(0), kr.data_ptr(), vr.data_ptr(), cap,
+              meta.data_ptr(), B, C, ptab.data_ptr(), bu.data_ptr(), bv.data_ptr(), T, h, dk, float(scale),
+              out.data_ptr(), out.stride(0), stream(qkv.device))
+    return out
+
+
 def relpos_attention(q, kr, vr, cap, start, length, ring, ptab, pstart, bu, bv, B, T, h, dk, scale, out):
     _lib.call("fo_relpos_attention", q.data_ptr(), q.stride(0), kr.data_ptr(), vr.data_ptr(), cap, start.data_ptr(),
               length.data_ptr(), ptr(ring), ptab.data_ptr(), pstart.data_ptr(), bu.data_ptr(), bv.data_ptr(), B, T, h,

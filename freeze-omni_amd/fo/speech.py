@@ -149,6 +149,11 @@ class EncoderCache:
             pass
 
 
+# a listen group's encoder attention: every chunk in one launch (fo_relpos_attention_chunks); FO_ENC_CHUNK_ATTN=0: one
+# fo_relpos_attention_fused launch per chunk (A/B)
+CHUNK_ATTN = os.environ.get("FO_ENC_CHUNK_ATTN", "1") != "0"
+
+
 class SpeechEncoderEngine:
     def __init__(self, src, cfg, ident, device, max_sessions=64):
         ty = cfg["train_yaml"]
@@ -361,11 +366,15 @@ class SpeechEncoderEngine:
             else:
                 ops.layernorm(x, *L["ln1"], out=h)
                 L["qkv"](h, out=qkv)
-            for j in range(chunks):
-                mj = meta[4 * B * j:4 * B * (j + 1)]
-                ops.relpos_attention_fused(qkv[j * n1:(j + 1) * n1], self.kr[i], self.vr[i], self.cap, mj[:B],
-                                           mj[B:2 * B], mj[2 * B:3 * B], self.ptab[i], mj[3 * B:], L["bu"], L["bv"],
-                                           B, T, self.h, self.dk, scale, att[j * n1:(j + 1) * n1])
+            if CHUNK_ATTN:   # the chunks in order inside one launch per (user, head)
+                ops.relpos_attention_chunks(qkv, self.kr[i], self.vr[i], self.cap, meta, B, chunks, self.ptab[i],
+                                            L["bu"], L["bv"], T, self.h, self.dk, scale, att)
+            else:            # one launch per chunk (A/B)
+                for j in range(chunks):
+                    mj = meta[4 * B * j:4 * B * (j + 1)]
+                    ops.relpos_attention_fused(qkv[j * n1:(j + 1) * n1], self.kr[i], self.vr[i], self.cap, mj[:B],
+                                               mj[B:2 * B], mj[2 * B:3 * B], self.ptab[i], mj[3 * B:], L["bu"],
+                                               L["bv"], B, T, self.h, self.dk, scale, att[j * n1:(j + 1) * n1])
             if fuse_ln:
                 L["out"].rowstats(att, x, sB, residual=True, ypack32=xp32)
                 L["ff1"].ln(x, *L["ln2"], sB, out=f, act="relu", ypack=fp, xpack32=xp32)

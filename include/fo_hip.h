@@ -292,6 +292,14 @@ int fo_relpos_attention_fused(const float* qkv, int ldq, float* kr, float* vr, i
                               const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
                               const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,
                               hipStream_t s);
+/* fo_relpos_attention_fused over C consecutive chunks of the same B users in one launch (the offline listen's grouped
+ * encoder pass, SpeechEncoderEngine.run(chunks=C); replaces C sequential calls of MultiHeadedAttention.infer,
+ * models/encoder/attention.py:407-459): q|k|v rows chunk-major ((j*B + b)*T + i), meta [C][start B | len B | ring B |
+ * pstart B] (each chunk's ring state after the chunks before it), out rows as q|k|v.  Chunks run in order per
+ * (user, head); rows an earlier chunk of the launch appended are read from its q|k|v rows. */
+int fo_relpos_attention_chunks(const float* qkv, int ldq, float* kr, float* vr, int cap, const int* meta, int B, int C,
+                               const float* ptab, const float* bu, const float* bv, int T, int h, int dk, float scale,
+                               float* out, int ldo, hipStream_t s);
 int fo_relpos_attention(const float* q, int ldq, const float* kr, const float* vr, int cap, const int* start,
                         const int* len, const int* ring, const float* ptab, const int* pstart, const float* bu,
                         const float* bv, int B, int T, int h, int dk, float scale, float* out, int ldo,

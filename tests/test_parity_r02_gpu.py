@@ -223,14 +223,17 @@ def test_real_geometry_encoder_adapter_match_reference(dev):
             close(emb, ref, rtol=2e-3, atol=2e-3 * float(np.abs(ref).max()))
 
 
-@pytest.mark.parametrize("C", [4, 3])
-def test_real_geometry_encoder_chunk_groups_match_reference(dev, C):
+@pytest.mark.parametrize("C,one_launch", [(4, True), (3, True), (4, False)])
+def test_real_geometry_encoder_chunk_groups_match_reference(dev, C, one_launch, monkeypatch):
     """SpeechEncoderEngine.run(chunks=C) (the offline listen's encoder stage, fo.engine.ListenGroupGraph): C
     consecutive chunks of 2 sessions in one pass -- the front end, norms and GEMMs over all C x B x T rows, the rel-pos
     attention chunk by chunk on the ring -- against the reference's chunk-by-chunk outputs: framing A for 20 chunks
     (the 64-frame ring fills and trims inside a group), framing B for 8 chunks across the RelPE wrap (a partial last
-    group); then the adapter chunk by chunk on the group's rows."""
+    group); then the adapter chunk by chunk on the group's rows.  one_launch: the group's attention as one
+    fo_relpos_attention_chunks launch per layer (default), else one fo_relpos_attention_fused launch per chunk."""
+    import fo.speech
     from fo.speech import AdapterEngine, SpeechEncoderEngine
+    monkeypatch.setattr(fo.speech, "CHUNK_ATTN", one_launch)
     g = load("real_encoder_t2.npz")
     src = _t2_source(dev, {**encoder_shapes(T2, "user"), **adapter_shapes(T2, "user")})
     enc = SpeechEncoderEngine(src, T2, "user", dev, max_sessions=8)
