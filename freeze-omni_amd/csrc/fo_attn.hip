@@ -537,6 +537,13 @@ __global__ __launch_bounds__(256) void k_relpos_fused(const float* qkv, int ldq,
 // launch appended are read from their q|k|v rows, never re-read from the ring this launch writes (so no global
 // write-then-read inside the launch); every chunk still appends its rows to the ring for the launches after it.
 // Chunk j sees exactly the left context the sequential per-chunk launches give it.
+// k_relpos_fused over C consecutive chunks of the same users in ONE launch (the offline listen's grouped encoder,
+// SpeechEncoderEngine.run(chunks=C)): one workgroup per (user, head, chunk), all chunks at once -- chunk j's context is
+// the ring as it was before the launch (meta[chunk][start B | len B | ring B | pstart B]: host_meta after the chunks
+// before it) plus the k / v columns of the earlier chunks' q|k|v rows (chunk-major: row (j * B + b) * T + i), which the
+// group's q|k|v GEMM has already produced; nothing is read from ring slots this launch's appends
+// (k_relpos_chunks_append, the next launch) will write.  Chunk j sees exactly the left context the sequential
+// per-chunk launches give it.
 __global__ __launch_bounds__(256) void k_relpos_chunks(const float* qkv, int ldq, float* kr, float* vr, int cap,
                                                        const int* meta, int B, int C, const float* ptab,
                                                        const float* bu, const float* bv, int T, int h, int dk,
@@ -554,7 +561,8 @@ __global__ __launch_bounds__(256) void k_relpos_chunks(const float* qkv, int ldq
   const int D4 = dk / 4;
   typedef float v4f __attribute__((ext_vector_type(4)));
   constexpr int RB_ = 8;
-  for (int jc = 0; jc < C; ++jc) {
+  {
+    const int jc = blockIdx.z;
     const int* m = meta + (size_t)jc * 4 * B;
     const size_t rb = (size_t)m[2 * B + b];
     const int Lold = m[B + b], Lk = Lold + T;
@@ -606,11 +614,6 @@ __global__ __launch_bounds__(256) void k_relpos_chunks(const float* qkv, int ldq
         const int e = e0 + q * 256 + threadIdx.x;
         if (e < Lk * D4) {
           const int j = e / D4, c = (e % D4) * 4;
-          if (j >= Lold) {   // the chunk's new rows enter the ring (for the launches after this one)
-            const size_t ro = (rb * cap + (st + j) % cap) * d + hh * dk + c;
-            *reinterpret_cast<v4f*>(kr + ro) = kk[q];
-            *reinterpret_cast<v4f*>(vr + ro) = vv[q];
-          }
           *reinterpret_cast<v4f*>(k_s + j * KP + c) = kk[q];
           *reinterpret_cast<v4f*>(v_s + j * KP + c) = vv[q];
           *reinterpret_cast<v4f*>(p_s + j * KP + c) = pp[q];
@@ -671,7 +674,29 @@ __global__ __launch_bounds__(256) void k_relpos_chunks(const float* qkv, int ldq
       for (int j = 0; j < Lk; ++j) acc += pr[j] * v_s[j * KP + c];
       out[(row0 + i) * ldo + hh * dk + c] = acc;
     }
-    __syncthreads();   // the next chunk restages the LDS rows this one reads
+  }
+}
+
+// The ring appends of a listen group's C chunks, after k_relpos_chunks has read the ring: chunk j's T rows (k, v
+// columns of its q|k|v rows) at its sequential positions (start_j + len_j + t) % cap -- consecutive over the chunks, so
+// the ring ends as C sequential appends leave it (C * T <= cap).
+__global__ void k_relpos_chunks_append(const float* qkv, int ldq, float* kr, float* vr, int cap, const int* meta, int B,
+                                       int C, int T, int d) {
+  const int D4 = d / 4;
+  const long long n = (long long)C * B * T * D4;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % D4) * 4;
+    const long long r = e / D4;          // q|k|v row: (jc * B + b) * T + t
+    const int t = (int)(r % T);
+    const int b = (int)((r / T) % B);
+    const int jc = (int)(r / ((long long)T * B));
+    const int* m = meta + (size_t)jc * 4 * B;
+    const size_t rb = (size_t)m[2 * B + b];
+    const size_t ro = (rb * cap + (m[b] + m[B + b] + t) % cap) * d + c;
+    const float* src = qkv + (size_t)r * ldq + c;
+    *reinterpret_cast<v4f*>(kr + ro) = *reinterpret_cast<const v4f*>(src + d);
+    *reinterpret_cast<v4f*>(vr + ro) = *reinterpret_cast<const v4f*>(src + 2 * d);
   }
 }
 
@@ -862,10 +887,15 @@ int fo_relpos_attention_chunks(const float* qkv, int ldq, float* kr, float* vr, 
   FO_REQUIRE(C * T <= cap, "fo_relpos_attention_chunks: %d chunks of %d frames exceed the ring (%d)", C, T, cap);
   const size_t lds = (size_t)(3 * cap * (dk + 4) + 2 * T * dk + T * cap) * sizeof(float);
   FO_REQUIRE(lds <= 160 * 1024, "fo_relpos_attention_chunks: ring of %d x %d exceeds LDS", cap, dk);
-  hipLaunchKernelGGL(k_relpos_chunks, dim3(B, h), dim3(256), lds, s, qkv, ldq, kr, vr, cap, meta, B, C, ptab, bu, bv,
-                     T, h, dk, scale, out, ldo);
+  hipLaunchKernelGGL(k_relpos_chunks, dim3(B, h, C), dim3(256), lds, s, qkv, ldq, kr, vr, cap, meta, B, C, ptab, bu,
+                     bv, T, h, dk, scale, out, ldo);
   fo::count_launch(FO_L_RELPOS);
-  return fo::check_launch("fo_relpos_attention_chunks");
+  int rc = fo::check_launch("fo_relpos_attention_chunks");
+  if (rc) return rc;
+  const long long n = (long long)C * B * T * (h * dk / 4);
+  hipLaunchKernelGGL(k_relpos_chunks_append, dim3(grid_for(n)), dim3(256), 0, s, qkv, ldq, kr, vr, cap, meta, B, C, T,
+                     h * dk);
+  return fo::check_launch("fo_relpos_attention_chunks/append");
 }
 
 int fo_relpos_attention(const float* q, int ldq, const float* kr, const float* vr, int cap, const int* start,

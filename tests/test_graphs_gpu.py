@@ -193,7 +193,7 @@ def _group_pipe(eng, feats_seq, n_users, C, decide=None):
 @pytest.mark.parametrize("C,n_chunks", [(2, 9), (4, 10), (3, 3)])
 def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
     """C consecutive chunks per Qwen2 stage (fo.engine.ListenGroupGraph, the offline input's listen): every chunk's
-    state probabilities (2e-5) and last hidden row (1e-4 of the row's scale) equal the one-chunk-per-stage pipe's to fp32
+    state probabilities (2e-5) and last hidden row (2e-4 of the row's scale) equal the one-chunk-per-stage pipe's to fp32
     rounding (the encoder and Qwen2 GEMMs tile C x the rows), its pe_index and the context lengths exactly; a partial
     last group (n_chunks % C) is flushed."""
     g = np.load(os.path.join(G, "fbank.npz"))
@@ -208,7 +208,7 @@ def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
         np.testing.assert_allclose(np.array(pg), np.array(pr), atol=2e-5)
         for a, b in zip(hg, hr):
             # (the grouped encoder runs its norms and GEMMs over C x the rows: other kernels, fp32 rounding apart)
-            np.testing.assert_allclose(a, b, atol=1e-4 * float(np.abs(b).max()), rtol=1e-4)
+            np.testing.assert_allclose(a, b, atol=2e-4 * float(np.abs(b).max()), rtol=1e-4)
 
 
 def test_listen_group_pipe_decide_rolls_back_the_rest(eng, dev):
