@@ -789,17 +789,22 @@ def recorded_kernel_avg_us(kernel_regex):
     return None, None, None
 
 
-def gemm_probe(engine, M, reps=2):
-    """Average duration of the dominant kernel (Qwen2 gate/up SwiGLU weight stream, the X-stationary
-    k_gemm_xs<16,7> launch of every layer) with HIP events on the launching stream.
-    The launches walk all layers' gate/up weights in order, as a chunk step does, so no launch finds
-    its weights in the Infinity Cache from the previous one (273 MB per layer > 256 MB MALL)."""
+def gemm_probe(engine, M, reps=2, down=False):
+    """Average duration of the dominant kernel with HIP events on the launching stream: the Qwen2 gate/up SwiGLU
+    weight stream of every layer at M rows (M <= 16: the X-stationary k_gemm_xs<16,7>); down=True: the listen group's
+    17..64-row split-K stream, which both the gate/up and the down launch (k_gemm_xsk + its k_gemm_reduce): every
+    layer's gate/up, then its down, each timed with its reduce (so the reduce counts against the kernel).
+    The launches walk all layers' weights in order, as a stage does, so no launch finds its weights in the Infinity
+    Cache from the previous one (273 MB per layer > 256 MB MALL)."""
     import torch
     from fo import _lib, ops
     layers = engine.llm.stack.layers
     L = layers[0]
     x = torch.randn(M, engine.llm.D, device=engine.device)
     out = torch.empty(M, L.gu.N, device=engine.device)
+    if down:
+        xd = torch.randn(M, L.down.K if hasattr(L.down, "K") else L.gu.N, device=engine.device)
+        yd = torch.empty(M, engine.llm.D, device=engine.device)
     for Lw in layers[:3]:
         Lw.gu(x, out=out)
     lib = _lib.load()
@@ -814,14 +819,18 @@ def gemm_probe(engine, M, reps=2):
         for Lw in layers:
             Lw.gu(x, out=out)
             n += 1
+            if down:
+                Lw.down(xd, out=yd)
+                n += 1
     lib.fo_event_record(e1, s)
     ms = ctypes.c_float()
     lib.fo_event_elapsed_ms(e0, e1, ctypes.byref(ms))
     lib.fo_event_destroy(e0)
     lib.fo_event_destroy(e1)
     t = ms.value / n / 1e3
-    weight_bytes = L.gu.nbytes
-    algo = weight_bytes + M * engine.llm.D * 4 + M * L.gu.N * 4
+    algo = L.gu.nbytes + M * engine.llm.D * 4 + M * L.gu.N * 4
+    if down:   # per launch: the mean of a gate/up and a down launch
+        algo = (algo + L.down.nbytes + M * xd.shape[1] * 4 + M * engine.llm.D * 4) / 2
     return {"bytes": algo, "seconds": t, "gbps": algo / t / 1e9, "launches": n}
 
 
@@ -1136,7 +1145,10 @@ def main():
                   "first_audio_ms": round((s1["first"][0] - s1["t_ss"]) * 1e3, 2),
                   "first_pcm_ms": round((s1["first_pcm"][0] - s1["t_ss"]) * 1e3, 2),
                   "rtf_per_user": round(a1 / (s1["last"][0] - s1["t_ss"]), 3)}
-    probe = gemm_probe(eng, 2 * args.users)
+    # the dominant kernel by time in the turn: with C >= 2 chunks per listen stage the listen's gate/up and down run at
+    # 2 x users x C rows on the split-K stream (k_gemm_xsk), ahead of the text steps' <= 16-row gate/up (k_gemm_xs)
+    group_rows = 2 * args.users * args.listen_chunks if args.pipeline else 2 * args.users
+    probe = gemm_probe(eng, group_rows, down=16 < group_rows <= 64)
     codec_ok, codec_n = codec_ids_check(eng)
     n_chunks = int(math.ceil(n_samp / 2560))
     roof_ms, roof_units = turn_roofline(eng, args.users, n_chunks, args.text_tokens,
@@ -1153,8 +1165,15 @@ def main():
     if rank == 0:
         peak = 8000.0
         # the X-stationary SwiGLU M<=16 weight stream: Qwen2 gate/up of every layer (the shipped variant: template
-        # VAR 0, spelled out in the kernel name since round 5; the probe variants 1-4 never run in the bench)
-        kre = r"k_gemm_xs<\d+, \d+(, 0)?>"
+        # VAR 0, spelled out in the kernel name since round 5; the probe variants 1-4 never run in the bench); with
+        # listen groups of 17..64 rows the split-K stream of their gate/up and down, RB = ceil(rows / 16)
+        rb = (group_rows + 15) // 16
+        kre = r"k_gemm_xs<\d+, \d+(, 0)?>" if group_rows <= 16 else rf"k_gemm_xsk<\d+, \d+, {rb}, \d+>"
+        kname = ("k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all 28 layers in turn)"
+                 if group_rows <= 16 else
+                 f"k_gemm_xsk<8,KPW,{rb},UA> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and down "
+                 f"split-K weight streams, M={group_rows}, all 28 layers in turn; per launch = the mean of a gate/up "
+                 f"and a down, reduce included)")
         traffic, traffic_src = recorded_traffic(kre)
         rp_us, rp_calls, rp_src = recorded_kernel_avg_us(kre)
         cpu = None
@@ -1198,11 +1217,11 @@ def main():
                          "frac": round(probe["gbps"] / peak, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
-                         "kernel": "k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all "
-                                   "28 layers in turn)",
+                         "kernel": kname,
                          "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2),
-                         "frac_source": "live: HIP events around every layer's gate/up launch on the engine stream "
-                                        "(gemm_probe); rocprof_* = the committed rocprofv3 summary of this command",
+                         "frac_source": "live: HIP events around every layer's gate/up (and down) launch on the engine "
+                                        "stream (gemm_probe); rocprof_* = the committed rocprofv3 summary of this "
+                                        "command (split-K: the stream kernel alone, its reduce not included)",
                          "rocprof_avg_launch_us": None if rp_us is None else round(rp_us, 2),
                          "rocprof_calls": rp_calls,
                          "rocprof_frac": None if rp_us is None else round(probe["bytes"] / (rp_us * 1e-6) / 1e9 / peak, 4),

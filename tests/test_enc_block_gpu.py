@@ -106,3 +106,55 @@ def test_enc_attn_block_refuses_unsupported_geometry(dev):
                                torch.zeros(4, dtype=torch.int32, device=dev), z(200, d), z(d), z(d), out, 0.125,
                                z(h * T * d), torch.zeros(1, dtype=torch.int32, device=dev),
                                ops.RowStats(T, dev, with_sums=True))
+
+
+@pytest.mark.parametrize("dk,h,cap,T,C,B", [(64, 16, 72, 4, 4, 8), (8, 4, 16, 4, 4, 3), (64, 16, 72, 7, 3, 2),
+                                             (8, 4, 16, 4, 2, 2)])
+def test_relpos_chunks_equals_sequential_chunk_launches(dev, dk, h, cap, T, C, B):
+    """fo_relpos_attention_chunks (a listen group's encoder attention: one workgroup per (user, head, chunk), earlier
+    chunks' K / V from the q|k|v rows, the ring appends in a second launch) against C sequential
+    fo_relpos_attention_fused launches on a copy of the ring: outputs and the final ring bit for bit, from a full ring
+    (trimmed), a short one and an empty one; small rings wrap (cap 16 = C x T)."""
+    import math
+
+    import numpy as np
+    import torch
+
+    from fo import ops
+    d = h * dk
+    buffersize = cap - 8
+    g = torch.Generator().manual_seed(dk * 100 + C)
+    nb_slots = B + 2
+    for L0 in (buffersize, 5, 0):
+        kr = torch.randn(nb_slots, cap, d, generator=g).to(dev)
+        vr = torch.randn(nb_slots, cap, d, generator=g).to(dev)
+        qkv = torch.randn(C * B * T, 3 * d, generator=g).to(dev)
+        ptab = torch.randn(600, d, generator=g).to(dev)
+        bu, bv = torch.randn(d, generator=g).to(dev), torch.randn(d, generator=g).to(dev)
+        starts = [(3 * b + 1) % cap for b in range(B)]
+        lens = [min(L0, buffersize)] * B
+        rings = [nb_slots - 1 - b for b in range(B)]
+        pe = [40 + 4 * b for b in range(B)]
+        metas = []
+        for j in range(C):
+            metas.append(starts + lens + rings + [max(0, p - 3 * T) for p in pe])
+            for b in range(B):
+                total = lens[b] + T
+                keep = min(total, buffersize)
+                starts[b] = (starts[b] + total - keep) % cap
+                lens[b] = keep
+                pe[b] += T
+        meta = torch.tensor(np.concatenate(metas), dtype=torch.int32).to(dev)
+        scale = 1.0 / math.sqrt(dk)
+        kr1, vr1 = kr.clone(), vr.clone()
+        seq = torch.empty(C * B * T, d, device=dev)
+        n1 = B * T
+        for j in range(C):
+            mj = meta[4 * B * j:4 * B * (j + 1)]
+            ops.relpos_attention_fused(qkv[j * n1:(j + 1) * n1], kr1, vr1, cap, mj[:B], mj[B:2 * B], mj[2 * B:3 * B],
+                                       ptab, mj[3 * B:], bu, bv, B, T, h, dk, scale, seq[j * n1:(j + 1) * n1])
+        one = torch.empty_like(seq)
+        ops.relpos_attention_chunks(qkv, kr, vr, cap, meta, B, C, ptab, bu, bv, T, h, dk, scale, one)
+        torch.cuda.synchronize()
+        assert torch.equal(one, seq), (L0, float((one - seq).abs().max()))
+        assert torch.equal(kr, kr1) and torch.equal(vr, vr1), L0

@@ -193,7 +193,7 @@ def _group_pipe(eng, feats_seq, n_users, C, decide=None):
 @pytest.mark.parametrize("C,n_chunks", [(2, 9), (4, 10), (3, 3)])
 def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
     """C consecutive chunks per Qwen2 stage (fo.engine.ListenGroupGraph, the offline input's listen): every chunk's
-    state probabilities (2e-5) and last hidden row (2e-4 of the row's scale) equal the one-chunk-per-stage pipe's to fp32
+    state probabilities (1e-4) and last hidden row (2e-4 of the row's scale) equal the one-chunk-per-stage pipe's to fp32
     rounding (the encoder and Qwen2 GEMMs tile C x the rows), its pe_index and the context lengths exactly; a partial
     last group (n_chunks % C) is flushed."""
     g = np.load(os.path.join(G, "fbank.npz"))
@@ -205,7 +205,9 @@ def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
     assert len(got) == len(ref) == n_chunks and lens == lens_ref
     for (pr, hr, qr), (pg, hg, qg) in zip(ref, got):
         assert qr == qg
-        np.testing.assert_allclose(np.array(pg), np.array(pr), atol=2e-5)
+        # (the batched-vs-single bound of tests/test_duplex_gpu.py: the two pipes' graphs tile the Qwen2 stage and its
+        # attention splits differently)
+        np.testing.assert_allclose(np.array(pg), np.array(pr), atol=1e-4)
         for a, b in zip(hg, hr):
             # (the grouped encoder runs its norms and GEMMs over C x the rows: other kernels, fp32 rounding apart)
             np.testing.assert_allclose(a, b, atol=2e-4 * float(np.abs(b).max()), rtol=1e-4)
@@ -228,7 +230,7 @@ def test_listen_group_pipe_decide_rolls_back_the_rest(eng, dev):
     assert len(got) == 5 and lens == lens_ref
     for (pr, _, qr), (pg, _, qg) in zip(ref, got):
         assert qr == qg
-        np.testing.assert_allclose(np.array(pg), np.array(pr), atol=2e-5)
+        np.testing.assert_allclose(np.array(pg), np.array(pr), atol=1e-4)
 
 
 def _text_run(eng, graph, n_users, steps, top_k):
