@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="listen chunk by chunk (default: encoder stage of chunk c+1 overlaps the LLM of chunk c)")
-    ap.add_argument("--listen-chunks", type=int, default=int(os.environ.get("FO_LISTEN_CHUNKS", "4")),
+    ap.add_argument("--listen-chunks", type=int, default=int(os.environ.get("FO_LISTEN_CHUNKS", "8")),
                     help="consecutive 160 ms chunks of the offline input per Qwen2 stage (fo.engine.ListenGroupGraph; "
                          "1: one chunk per stage)")
     ap.add_argument("--scenario", default="turn", choices=["turn", "duplex"],
@@ -498,25 +498,32 @@ def vocoder_calls(n, chunk=40, pad=10):
     return calls
 
 
-def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.0e12, mfma=2.5e15):
+def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.0e12, mfma=2.5e15,
+                  chunks_per_stage=1):
     """Speed-of-light time of one turn's work (each stage against its own bound, the turn as
     Σ max(bytes / HBM BW, flops / dense bf16 MFMA peak)).  Algorithmic bytes: bf16 weights
     streamed once per batched step, the KV read per token at the reference's bf16 (autocast k_proj / v_proj outputs,
     models/pipeline.py:67-68): Qwen2 57,344 B, AR decoder 14,336 B; vocoder as 2*Cin*Cout*K*Tout FLOPs.  This build
     keeps its paged KV in fp32: the bytes that layout reads beyond the bf16 figure are reported apart
-    ("kv_fp32_extra_GB"), never counted as work.  ctx0: per-user LLM context when the listen starts (system prompt)."""
+    ("kv_fp32_extra_GB"), never counted as work.  ctx0: per-user LLM context when the listen starts (system prompt).
+    chunks_per_stage C: the listen's batched step is a group of C chunks (fo.engine.ListenGroupGraph), so its weights
+    stream once per group -- ceil(n_chunks / C) times; each chunk still reads its own context.  The one-chunk-per-step
+    figure (the reference's schedule, bin/inference.py:106-144) is returned beside it as listen_per_chunk_GB."""
     llm = eng.llm
     kv_llm = llm.stack.n * llm.KVH * llm.hd * 2 * 2
     kv_tts = eng.tts.main.n * eng.tts.H * eng.tts.hd * 2 * 2
     kv_extra = 0.0   # bytes per (algorithmic bf16) KV byte the fp32 layout adds
     w_listen = eng.enc["user"].weight_bytes + eng.ada["user"].weight_bytes + llm.stack.weight_bytes
     rows = 2   # LLM tokens per 160 ms chunk (framing A)
-    listen_b = 0.0
+    listen_kv = 0.0
     L = ctx0
     for c in range(n_chunks):
         L += rows + (len(eng.prefix_ids["user"]) if c == 0 else 0)
-        listen_b += w_listen + B * L * kv_llm
+        listen_kv += B * L * kv_llm
         kv_extra += B * L * kv_llm
+    stages = -(-n_chunks // max(1, chunks_per_stage))
+    listen_b = stages * w_listen + listen_kv
+    listen_one = n_chunks * w_listen + listen_kv
     text_b = 0.0
     L += len(eng.prefix_ids["system"])
     for t in range(text_tokens):
@@ -534,7 +541,8 @@ def turn_roofline(eng, B, n_chunks, text_tokens, codec_per_sentence, ctx0, bw=8.
         speak_f += B * sum(eng.codec.flops(T) for T in vocoder_calls(n))
     ms = {"listen": listen_b / bw * 1e3, "text": text_b / bw * 1e3,
           "speak": max(speak_b / bw, 0.0) * 1e3 + speak_f / mfma * 1e3}
-    return ms, {"listen_GB": listen_b / 1e9, "text_GB": text_b / 1e9, "speak_GB": speak_b / 1e9,
+    return ms, {"listen_GB": listen_b / 1e9, "listen_stages": stages, "listen_per_chunk_GB": listen_one / 1e9,
+                "text_GB": text_b / 1e9, "speak_GB": speak_b / 1e9,
                 "vocoder_TFLOP": speak_f / 1e12, "kv_fp32_extra_GB": kv_extra / 1e9}
 
 
@@ -1148,11 +1156,12 @@ def main():
     # the dominant kernel by time in the turn: with C >= 2 chunks per listen stage the listen's gate/up and down run at
     # 2 x users x C rows on the split-K stream (k_gemm_xsk), ahead of the text steps' <= 16-row gate/up (k_gemm_xs)
     group_rows = 2 * args.users * args.listen_chunks if args.pipeline else 2 * args.users
-    probe = gemm_probe(eng, group_rows, down=16 < group_rows <= 64)
+    probe = gemm_probe(eng, group_rows, down=16 < group_rows <= 128)
     codec_ok, codec_n = codec_ids_check(eng)
     n_chunks = int(math.ceil(n_samp / 2560))
     roof_ms, roof_units = turn_roofline(eng, args.users, n_chunks, args.text_tokens,
-                                        [args.codec_tokens // stats[0]["n_sent"]] * stats[0]["n_sent"], base_kv.length)
+                                        [args.codec_tokens // stats[0]["n_sent"]] * stats[0]["n_sent"], base_kv.length,
+                                        chunks_per_stage=args.listen_chunks if args.pipeline else 1)
     if dist is not None:
         t = torch.tensor([wall, audio], dtype=torch.float64, device=dev)
         allw = [torch.zeros_like(t) for _ in range(world)]
@@ -1168,12 +1177,20 @@ def main():
         # VAR 0, spelled out in the kernel name since round 5; the probe variants 1-4 never run in the bench); with
         # listen groups of 17..64 rows the split-K stream of their gate/up and down, RB = ceil(rows / 16)
         rb = (group_rows + 15) // 16
-        kre = r"k_gemm_xs<\d+, \d+(, 0)?>" if group_rows <= 16 else rf"k_gemm_xsk<\d+, \d+, {rb}, \d+>"
-        kname = ("k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all 28 layers in turn)"
-                 if group_rows <= 16 else
-                 f"k_gemm_xsk<8,KPW,{rb},UA> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and down "
-                 f"split-K weight streams, M={group_rows}, all 28 layers in turn; per launch = the mean of a gate/up "
-                 f"and a down, reduce included)")
+        if group_rows <= 16:
+            kre = r"k_gemm_xs<\d+, \d+(, 0)?>"
+            kname = "k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all 28 layers in turn)"
+        elif group_rows <= 64:
+            kre = rf"k_gemm_xsk<\d+, \d+, {rb}, \d+>"
+            kname = (f"k_gemm_xsk<8,KPW,{rb},UA> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and down "
+                     f"split-K weight streams, M={group_rows}, all 28 layers in turn; per launch = the mean of a "
+                     f"gate/up and a down, reduce included)")
+        else:
+            kre = r"k_gemm_rows<"
+            kname = (f"k_gemm_rows<8,1,NTC,DW,DX> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and "
+                     f"down weight streams at M={group_rows}: 8 waves split the rows, the weight fragments shared "
+                     f"through an LDS-DMA ring; all 28 layers in turn; per launch = the mean of a gate/up and a down, "
+                     f"reduce included)")
         traffic, traffic_src = recorded_traffic(kre)
         rp_us, rp_calls, rp_src = recorded_kernel_avg_us(kre)
         cpu = None

@@ -1527,6 +1527,308 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int
   }
 }
 
+// ---- 65..128-row weight streams (k_gemm_rows): the weights once, every row block on the matrix cores.
+// A listen group of C chunks x 8 users x 2 tokens puts 128 rows through every Qwen2 GEMM (fo.engine.ListenGroupGraph,
+// C = 8); the X-stationary kernels hold one row block per 16 K-slice waves and run 65..128 rows as two 64-row launches
+// (the weights twice, k_gemm_xsk's per-unit cross-wave reduction each time).  Here the 4 waves of a workgroup split the
+// ROWS instead (wave w: row blocks RPW w .. RPW w + RPW - 1) and share each k-step's weight fragments through LDS, so
+// there is no cross-wave reduction and each weight byte is read from HBM once:
+//  * one LDS-DMA loader ring per workgroup (global_load_lds_dwordx4, issued by every wave for its share): DW k-steps
+//    of the workgroup's <= 4 TPW weight tiles ahead, DX k-steps of its fp32 X rows ahead (X comes from L2);
+//  * per k-step: one s_waitcnt on this wave's own DMA (the count of the DX - 1 younger k-steps' loads, fixed by
+//    padding every k-step to the same number of loads), one workgroup barrier (every wave's loads landed, and every
+//    wave is past the slot the next loads overwrite), then the wave's X fragments split into bf16 hi / lo and
+//    2 RPW MFMAs per tile;
+//  * workgroups = S K-splits x G tile groups (XCD-aware as k_gemm_xsk); each writes its fp32 partial tiles to split
+//    S's slab and k_gemm_reduce (the next launch) sums the slabs in split order and runs every epilogue (SwiGLU, the
+//    RMSNorm rstd, residual, row statistics).  Gate/up: S = 1 (one slab: the reduce is the epilogue pass).
+// The loads are asm (the compiler's own wait placement treats an LDS-DMA as aliasing every later LDS read and drains
+// the whole ring before each one); nothing else in the loop touches vector memory, so the manual counts are exact.
+template <bool NT = false>   // NT: the streaming (non-temporal) policy -- weights that must not evict X from L2
+__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte)
+                 : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte)
+                 : "memory");
+}
+template <typename T>
+__device__ __forceinline__ unsigned lds_addr(T* p) {
+  return (unsigned)(size_t)((__attribute__((address_space(3))) char*)(p));
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// this wave's DMA down to N outstanding and its LDS reads done, then the workgroup barrier -- one opaque statement, so
+// the compiler moves no LDS access across it (a bare s_barrier builtin orders no memory)
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+// PROBE (fo_gemm_set_rows 4 / 5, WRONG results, timing bounds): 1 = no X loads (the weight stream alone), 2 = no loads
+// XL: the X DMA's lane -> (row, 16-B chunk) map.  0: lane l fetches row l & 15, chunks 2 (l >> 4) + h of the k-step
+// (each load touches 16 rows x half a line); 1: load h fetches rows 8 h .. 8 h + 7 whole (8 full 128-B lines), lane
+// f = 8 c + (r & 7) + 8 h (mod 64) holding chunk c of row r, which keeps the consumer's two ds_read_b128 free of
+// bank conflicts (its 16-lane groups read 16 consecutive 16-B slots)
+template <int NWV, int RPW, int NTC, int DW, int DX, bool WNT = false, int PROBE = 0, int XL = 0>
+__global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int tiles_per) {
+  constexpr int RB = NWV * RPW;
+  constexpr int LPW = (NTC + NWV - 1) / NWV;   // weight loads per wave per k-step (tile t: wave t % NWV)
+  constexpr int PW = DW + 1, PX = DX + 1;
+  constexpr int OPS = LPW + 2 * RPW;           // DMA loads per wave per k-step
+  __shared__ bf16x8 wr[PW][NTC][64];         // weight ring: one 1 KiB fragment per (k-step slot, tile)
+  __shared__ float4 xr[PX][RB][2][64];       // X ring: fp32 rows of each row block, two 16-B halves per lane
+  __shared__ float4 dummy[64];               // the padding loads land here
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int KS = a.K >> 5;
+  const int total = a.S * G, per_x = (total + 7) >> 3;
+  const int wgi = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+  if (wgi >= total) return;
+  const int sp = wgi / G, gx = wgi - sp * G;
+  const int tb = gx * tiles_per, te = min(a.ntiles, tb + tiles_per);
+  const int nt = te - tb;   // <= NTC (host)
+  const int kb = (int)((long)KS * sp / a.S), ke = (int)((long)KS * (sp + 1) / a.S);
+  const int nk = ke - kb;
+  const char* wbase = reinterpret_cast<const char*>(a.Wp);
+  const float* xbase = reinterpret_cast<const float*>(a.X);
+  // this lane's X row of each of the wave's row blocks (rows >= M clamp to M - 1: computed, never stored)
+  const float* xrow[RPW][2];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      if constexpr (XL == 0) {
+        const int row = min((wave * RPW + r) * 16 + (lane & 15), a.M - 1);
+        xrow[r][hf] = xbase + (size_t)row * a.ldx + 8 * (lane >> 4) + 4 * hf;
+      } else {
+        const int row = min((wave * RPW + r) * 16 + 8 * hf + (lane & 7), a.M - 1);
+        const int c = ((lane >> 3) - hf) & 7;
+        xrow[r][hf] = xbase + (size_t)row * a.ldx + 4 * c;
+      }
+    }
+  // the consumer's two LDS slots (16-B lanes of the two loads' images)
+  int xs0, xs1, xh0;
+  if constexpr (XL == 0) {
+    xh0 = 0;
+    xs0 = xs1 = lane;
+  } else {
+    const int r = lane & 15, q = lane >> 4, h = r >> 3;
+    xh0 = h;
+    xs0 = (16 * q + (r & 7) + 8 * h) & 63;
+    xs1 = (xs0 + 8) & 63;
+  }
+  const unsigned dummy_l = __builtin_amdgcn_readfirstlane(lds_addr(&dummy[0]));
+  const void* dummy_g = wbase + (size_t)lane * 16;
+  // weights of k-step i (relative to kb) into ring slot i % PW: this wave's tiles wave, wave + NWV, ...
+  auto issue_w = [&](int i) {
+    if constexpr (PROBE == 2) return;
+#pragma unroll
+    for (int q = 0; q < LPW; ++q) {
+      const int t = q * NWV + wave;
+      if (i < nk && t < nt && t < NTC) {
+        const void* src = wbase + ((size_t)(tb + t) * KS + (kb + i)) * 1024 + (size_t)lane * 16;
+        dma16<WNT>(src, __builtin_amdgcn_readfirstlane(lds_addr(&wr[i % PW][t][0])));
+      } else {
+        dma16(dummy_g, dummy_l);
+      }
+    }
+  };
+  auto issue_x = [&](int i) {
+    if constexpr (PROBE != 0) return;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int rb = wave * RPW + r;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        if (i < nk) {
+          const void* src = xrow[r][hf] + (size_t)(kb + i) * 32;
+          dma16(src, __builtin_amdgcn_readfirstlane(lds_addr(&xr[i % PX][rb][hf][0])));
+        } else {
+          dma16(dummy_g, dummy_l);
+        }
+      }
+    }
+  };
+  f32x4 acc[NTC][RPW];
+#pragma unroll
+  for (int t = 0; t < NTC; ++t)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // prologue in the loop's issue order (k-step j - DW's weights, then k-step j - DX's X, for j = 0 .. DW - 1) so every
+  // k-step's wait below sees the same number of younger loads; X of negative k-steps: padding loads
+  for (int j = 0; j < DW; ++j) {
+    issue_w(j);
+    if (j - (DW - DX) >= 0) issue_x(j - (DW - DX));
+    else {
+#pragma unroll
+      for (int q = 0; q < 2 * RPW; ++q)
+        if constexpr (PROBE == 0) dma16(dummy_g, dummy_l);
+    }
+  }
+  for (int i = 0; i < nk; ++i) {
+    // this wave's loads of k-step i (weights and X) have landed; after the barrier every wave's have, and every wave
+    // is done reading k-step i - 1's slots, which the loads below overwrite
+    wait_vm_barrier<PROBE == 0 ? (DX - 1) * OPS : (PROBE == 1 ? (DW - 1) * LPW : 0)>();
+    issue_w(i + DW);
+    issue_x(i + DX);
+    // every read of the k-step issued before the first MFMA (one latency per k-step); tiles past the workgroup's nt
+    // and row blocks past M are computed on whatever the slots hold and never stored (no branch in the loop)
+    float4 xp[RPW][2];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      if constexpr (XL == 0) {
+        xp[r][0] = xr[i % PX][wave * RPW + r][0][lane];
+        xp[r][1] = xr[i % PX][wave * RPW + r][1][lane];
+      } else {
+        xp[r][0] = xr[i % PX][wave * RPW + r][xh0][xs0];
+        xp[r][1] = xr[i % PX][wave * RPW + r][xh0][xs1];
+      }
+    }
+    bf16x8 wf[NTC];
+#pragma unroll
+    for (int t = 0; t < NTC; ++t) wf[t] = wr[i % PW][t][lane];
+    bf16x8 xh[RPW], xl[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const float f[8] = {xp[r][0].x, xp[r][0].y, xp[r][0].z, xp[r][0].w,
+                          xp[r][1].x, xp[r][1].y, xp[r][1].z, xp[r][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const __bf16 h = (__bf16)f[e];
+        xh[r][e] = h;
+        xl[r][e] = (__bf16)(f[e] - (float)h);
+      }
+    }
+    // hi products of every (tile, row block), then the lo ones: no accumulator is read right after it is written
+#pragma unroll
+    for (int t = 0; t < NTC; ++t)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[r], wf[t], acc[t][r], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < NTC; ++t)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl[r], wf[t], acc[t][r], 0, 0, 0);
+  }
+  wait_vm<0>();   // (the padding loads past the last k-step) nothing of this workgroup's DMA outlives it
+  const int Ncols = a.ntiles * 16;
+  const int ROWS = RB * 16;
+  float* slab = a.ws + (size_t)sp * ROWS * Ncols;
+#pragma unroll
+  for (int t = 0; t < NTC; ++t)
+    if (t < nt)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = (wave * RPW + r) * 16 + 4 * (lane >> 4) + e;
+          if (row < a.M) slab[(size_t)row * Ncols + (tb + t) * 16 + (lane & 15)] = acc[t][r][e];
+        }
+}
+
+// ---- 33..128-row weight streams, second form (k_gemm_wrow): each wave owns ONE weight tile over the workgroup's K
+// range and streams its fragments straight into registers DW k-steps ahead (a register ring, compiler-counted loads,
+// ~DW KiB in flight per wave), while the X rows of the k-step are staged once per workgroup through LDS, already
+// split into bf16 hi / lo (row block r loaded and converted by wave r): per k-step a workgroup ingests its tiles' 1 KiB
+// fragments from HBM and ONE copy of the k-step's X from L2 -- k_gemm_rows (waves split the rows) pulled every tile
+// through an LDS-DMA ring of at most ~60 KiB in flight and read X fp32 per wave.  One barrier per k-step (the X slot
+// double-buffered); no cross-wave reduction; partial tiles into split sp's slab, k_gemm_reduce runs the epilogue.
+template <int NWV, int RB, int DW, int DXS>
+__global__ __launch_bounds__(NWV * 64) void k_gemm_wrow(GemmArgs a, int G) {
+  static_assert(DW % DXS == 0 && DW % 2 == 0 && RB <= NWV, "k_gemm_wrow: ring shapes");
+  __shared__ bf16x8 xhi[2][RB][64], xlo[2][RB][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // (uniform: SGPR offsets)
+  const int KS = a.K >> 5;
+  const int total = a.S * G, per_x = (total + 7) >> 3;
+  const int wgi = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+  if (wgi >= total) return;
+  const int sp = wgi / G, gx = wgi - sp * G;
+  const int tile = gx * NWV + wave;
+  const bool live = tile < a.ntiles;
+  const int kb = (int)((long)KS * sp / a.S), ke = (int)((long)KS * (sp + 1) / a.S);
+  const int nk = ke - kb;
+  // weight fragments through a buffer descriptor: k-steps past the split or a tile past ntiles address beyond its
+  // range, which the hardware drops (zeros, no memory access)
+  const unsigned long long wbase = (unsigned long long)a.Wp;
+  const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(wbase >> 32)) << 32) |
+                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)wbase)),
+      (short)0, __builtin_amdgcn_readfirstlane(a.ntiles * KS * 1024), 0x00020000);
+  const int voff = lane * 16;
+  const int beyond = a.ntiles * KS * 1024;
+  auto ldw = [&](int i) -> bf16x8 {
+    const int so = (live && i < nk) ? (tile * KS + kb + i) * 1024 : beyond;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srd, voff, so, 2));
+  };
+  // X staging: wave r < RB loads row block r's fragment of each k-step (lane: row 16 r + (l & 15), 8 columns)
+  const bool stager = wave < RB;
+  const int xrow = min(wave * 16 + (lane & 15), a.M - 1);
+  const float* xp = reinterpret_cast<const float*>(a.X) + (size_t)xrow * a.ldx + 8 * (lane >> 4) + (size_t)kb * 32;
+  auto ldx2 = [&](int i, float4 (&q)[2]) {
+    if (stager && i < nk) {
+      q[0] = reinterpret_cast<const float4*>(xp + (size_t)i * 32)[0];
+      q[1] = reinterpret_cast<const float4*>(xp + (size_t)i * 32)[1];
+    }
+  };
+  bf16x8 wq[DW];
+  float4 xq[DXS][2];
+#pragma unroll
+  for (int j = 0; j < DW; ++j) wq[j] = ldw(j);
+#pragma unroll
+  for (int j = 0; j < DXS; ++j) ldx2(j, xq[j]);
+  f32x4 acc[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i0 = 0; i0 < nk; i0 += DW) {
+#pragma unroll
+    for (int j = 0; j < DW; ++j) {
+      const int i = i0 + j;
+      if (i < nk) {          // workgroup-uniform
+      const int sl = j & 1;  // (i0 is a multiple of DW, which is even)
+      if (stager) {          // X of k-step i, split once into bf16 hi / lo for every wave
+        const float4 q0 = xq[j % DXS][0], q1 = xq[j % DXS][1];
+        const float f[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        bf16x8 h8, l8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const __bf16 h = (__bf16)f[e];
+          h8[e] = h;
+          l8[e] = (__bf16)(f[e] - (float)h);
+        }
+        xhi[sl][wave][lane] = h8;
+        xlo[sl][wave][lane] = l8;
+      }
+      ldx2(i + DXS, xq[j % DXS]);
+      __syncthreads();   // k-step i's X visible; every wave is past k-step i - 2's reads of this slot
+      const bf16x8 w = wq[j];
+      wq[j] = ldw(i + DW);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xhi[sl][r][lane], w, acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xlo[sl][r][lane], w, acc[r], 0, 0, 0);
+      }
+      }
+    }
+  }
+  if (!live) return;
+  const int Ncols = a.ntiles * 16;
+  float* slab = a.ws + (size_t)sp * (RB * 16) * Ncols;
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r * 16 + 4 * (lane >> 4) + e;
+      if (row < a.M) slab[(size_t)row * Ncols + tile * 16 + (lane & 15)] = acc[r][e];
+    }
+}
+
 // in-launch split-K merge: 0 off, 1 every eligible split, 2 (default) splits of small weights only -- measured
 // (profiles/r02t_*): the TTS down (8.7 MB) 184.8 -> 181.5 us per AR step, the Qwen2 down (136 MB) slower
 // (LLM stage 3313 -> 3340 us: every one of its 224 workgroups drains write-through partials before exiting),
@@ -1553,6 +1855,12 @@ inline bool xs_mode() {
 const bool g_row_split = [] {
   const char* e = getenv("FO_GEMM_ROW_SPLIT");
   return !(e && e[0] == '0');
+}();
+// 65..128-row GEMMs on the >= 128 MB weight streams take k_gemm_rows (FO_GEMM_ROWS=0: the row halves above)
+// (probe, fo_gemm_set_rows: 2 = k_gemm_wrow, one tile per wave)
+int g_rows = [] {
+  const char* e = getenv("FO_GEMM_ROWS");
+  return (e && e[0] == '0') ? 0 : 1;
 }();
 // weights of at least this many MiB take the 17..64-row split-K stream (fo_gemm_set_xsk_min_mb: probes)
 int g_xsk_min_mb = [] {
@@ -1699,13 +2007,46 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   // each) instead of 64-row tiles, which stream the whole weight once per row tile at ~1.4-2.5 TB/s (r05i duplex
   // table: gate/up 193.8 us, down 110.4 us per layer at 72 rows).  Both halves take k_gemm_xsk, so their row
   // statistics have the same group count ((N + 255) / 256) and the halves' rows tile the [M][groups] layout.
+  // 65..128 rows on the large weight streams: k_gemm_rows (the weights once) when its split-K slabs fit the workspace
+  bool rows_ok = false;
+  int rows_S = 1, rows_tp = 0, rows_G = 0;
+  {
+    const int nt_all = (swiglu ? 2 : 1) * ((N + 15) / 16);
+    const long long wb = (long long)nt_all * 16 * K * 2;
+    if (g_rows && M > 64 && M <= 128 && x_f32 && !lnw && !rope && !sout1 && !rstats1 && splitk <= 1 &&
+        wb >= ((long long)g_xsk_min_mb << 20) && (ldx % 4) == 0 && !xpk.p0 && !xp32k.p0 && !g_force_nt &&
+        !g_force_nw && (!swiglu || nt_all % 2 == 0)) {
+      const int cus = num_cus();
+      if (g_rows != 2) {   // k_gemm_rows: the waves split the rows
+        if (swiglu) {   // gate/up: whole (gate, up) pairs per workgroup, every workgroup the same count, one K pass
+          const int units = nt_all / 2, per = (units + cus - 1) / cus;
+          rows_tp = 2 * per;
+          rows_G = (units + per - 1) / per;
+          rows_S = 1;
+        } else {        // long-K (down): <= 8 tiles per workgroup and K split until the grid covers the CUs
+          const int g8 = (nt_all + 7) / 8;
+          rows_S = max(1, min(8, (cus + g8 / 2) / g8));
+          const int gw = max(1, cus / rows_S);
+          rows_tp = min(8, (nt_all + gw - 1) / gw);
+          rows_G = (nt_all + rows_tp - 1) / rows_tp;
+        }
+      } else {             // (probe) k_gemm_wrow: one tile per wave; gate/up 10 waves (5 pairs), one K pass; long-K 14 / 8
+        rows_tp = swiglu ? ((nt_all / 2) % 5 == 0 ? 10 : 8) : (nt_all % 14 == 0 ? 14 : 8);
+        rows_G = (nt_all + rows_tp - 1) / rows_tp;
+        rows_S = swiglu ? 1 : max(1, min(16, cus / rows_G));
+      }
+      const long long need = (long long)rows_S * 128 * nt_all * 16;
+      rows_ok = rows_tp <= (g_rows == 2 ? 14 : (swiglu ? 12 : 8)) && need <= ws_floats && ws != nullptr &&
+                (K >> 5) >= rows_S;
+    }
+  }
   {
     const long long wb = (long long)(swiglu ? 2 : 1) * ((N + 15) / 16) * 16 * K * 2;
     const bool big = wb >= ((long long)g_xsk_min_mb << 20) || (K >= 8192 && wb >= (32ll << 20));
     // (and the plain >= 8 MB projections -- the Qwen2 o: 57.0 us on 64-row tiles at 72 rows -- whose halves take
     // the one-row-tile split-K kernels + k_gemm_reduce, the same statistics groups)
     const bool mid_w = !swiglu && wb >= (8ll << 20);
-    if (M > 64 && M <= 128 && x_f32 && !lnw && !rope && !sout1 && !rstats1 && splitk <= 1 && (big || mid_w) &&
+    if (!rows_ok && M > 64 && M <= 128 && x_f32 && !lnw && !rope && !sout1 && !rstats1 && splitk <= 1 && (big || mid_w) &&
         xsk_mode() && !g_force_nt && !g_force_nw && !xpk.p0 && !ypk.p0 && !yp32k.p0 && !xp32k.p0 && (K >> 5) >= 56 &&
         (ldx % 4) == 0 && ((swiglu ? 2 : 1) * ((N + 15) / 16)) % 2 == 0 && g_row_split) {
       const int M0 = (M + 1) / 2, grp = (N + 255) / 256;
@@ -1793,6 +2134,40 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.rKVH = rope->rKVH;
     a.rhd = rope->rhd;
     a.rPS = rope->rPS;
+  }
+  if (rows_ok) {
+    a.S = rows_S;
+    a.counters = nullptr;
+    if (sgroups) *sgroups = (N + 255) / 256;
+    const int total = rows_S * rows_G;
+    const dim3 grid(8 * ((total + 7) / 8));
+    // (instantiated tile counts: the Qwen2 gate/up's 5 pairs and down's 7 tiles per workgroup, else the slot count)
+#define FO_ROWS(NWV_, RPW_, NTC_, DW_, DX_, PR_, XL_)                                                               \
+  hipLaunchKernelGGL((k_gemm_rows<NWV_, RPW_, NTC_, DW_, DX_, false, PR_, XL_>), grid, dim3(NWV_ * 64), 0, stream, a, \
+                     rows_G, rows_tp)
+#define FO_WROW(NWV_, DW_, DXS_) \
+  hipLaunchKernelGGL((k_gemm_wrow<NWV_, 8, DW_, DXS_>), grid, dim3(NWV_ * 64), 0, stream, a, rows_G)
+    if (g_rows == 2) {   // (probe) k_gemm_wrow
+      if (rows_tp == 10) FO_WROW(10, 12, 4);
+      else if (rows_tp == 14) FO_WROW(14, 8, 4);
+      else FO_WROW(8, 12, 4);
+    } else if (swiglu && rows_tp <= 10) {
+      FO_ROWS(8, 1, 10, 5, 4, 0, 1);
+    } else if (swiglu) {
+      FO_ROWS(8, 1, 12, 5, 3, 0, 1);
+    } else if (rows_tp <= 7) {
+      FO_ROWS(8, 1, 7, 7, 4, 0, 1);
+    } else {
+      FO_ROWS(8, 1, 8, 7, 4, 0, 1);
+    }
+#undef FO_WROW
+#undef FO_ROWS
+    int rc = fo::check_launch("fo_gemm/rows");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, 128);
+    fo::count_launch(FO_L_GEMM_ROWS);
+    fo::count_launch(FO_L_GEMM_REDUCE);
+    return fo::check_launch("fo_gemm/rows reduce");
   }
   // X-stationary persistent weight stream (k_gemm_xs) for the M <= 16 rows of a listen chunk / text step on
   // K = 3584 layers (Qwen2 q|k|v, o, gate/up, lm_head): no split, no LayerNorm-on-load
@@ -2148,6 +2523,13 @@ int fo_gemm_set_xsk_min_mb(int mb) {
   FO_REQUIRE(mb >= 0, "fo_gemm_set_xsk_min_mb: %d", mb);
   const int prev = g_xsk_min_mb;
   g_xsk_min_mb = mb;
+  return prev;
+}
+
+int fo_gemm_set_rows(int on) {
+  FO_REQUIRE(on >= 0 && on <= 2, "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows) or 2 (probe: k_gemm_wrow)");
+  const int prev = g_rows;
+  g_rows = on;
   return prev;
 }
 

@@ -425,7 +425,7 @@ def h2d(a, device, dtype=None):
 # ---------------------------------------------------------------- launch counters (include/fo_hip.h FoLaunchKind)
 LAUNCH_KINDS = ("gemm_xs", "gemm_xsk", "gemm_xp", "gemm_reduce", "gemm_ln", "gemm_xp32", "gemm_ypack", "gemm_ypack32",
                 "gemm_mid", "gemm_rope4", "gemm_pipe", "gemm_other", "attn_mfma", "attn_decode", "attn_opack", "relpos",
-                "subsample", "attn_o", "enc_block")
+                "subsample", "attn_o", "enc_block", "gemm_rows")
 
 
 def launch_counts():

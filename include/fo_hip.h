@@ -96,6 +96,11 @@ int fo_gemm_set_xs_variant(int v);
 /* probe hook: the weight size (MiB) from which 17..64-row fp32 GEMMs take k_gemm_xsk (default 128; long-K >= 32 MiB
  * layers always).  Process-global; returns the previous value. */
 int fo_gemm_set_xsk_min_mb(int mb);
+/* probe hook: 65..128-row GEMMs on >= 128 MiB weights through k_gemm_rows (1, default: the waves split the rows, the
+ * weights through an LDS-DMA ring) or as two row-half launches of the <= 64-row kernels (0); 2 = the probe form
+ * k_gemm_wrow (one tile per wave, X staged once per workgroup).  Unset, FO_GEMM_ROWS decides.  Process-global; returns
+ * the previous setting. */
+int fo_gemm_set_rows(int on);
 /* probe (scripts/seam_probe.py): the Qwen2 o -> gate/up seam at <= 16 rows as one launch (k_seam_o_gu); xo [M][3584]
  * attention output, wo / wgu packed o and SwiGLU-paired gate/up weights, x the residual stream (updated), yg / sout the
  * next norm's input and partial sums of squares ([M][112]), h the SwiGLU output [M][n_gu_out]; ready: a zeroed int
@@ -165,6 +170,7 @@ enum FoLaunchKind {
   FO_L_SUBSAMPLE = 16,  /* fo_subsample: the encoder front end (conv1 stencil + conv2 implicit GEMM + transpose) */
   FO_L_ATTN_O = 17,     /* k_attn_decode_o: decode attention + o projection + residual + next-norm statistics */
   FO_L_ENC_BLOCK = 18,  /* k_enc_attn_block: the attention half of a speech-encoder block */
+  FO_L_GEMM_ROWS = 19,  /* k_gemm_rows: 65..128 rows, the waves split the rows, weights shared through an LDS ring */
   FO_LAUNCH_KINDS = 24
 };
 int fo_launch_counts(long long* out, int n);

@@ -119,13 +119,27 @@ def test_gemm_mid_rows(dev, M, N, K, sw):
         assert torch.equal(out2.cpu().double(), y)
 
 
-@pytest.mark.parametrize("M", [65, 72, 128])
+@pytest.mark.parametrize("M", [65, 72, 100, 128])
 @pytest.mark.parametrize("producer", ["down", "o"])
-def test_gemm_row_halves_on_qwen2_streams(dev, M, producer):
+@pytest.mark.parametrize("rows", [1, 0])
+def test_gemm_65_to_128_rows_on_qwen2_streams(dev, M, producer, rows):
     """65..128 rows on the Qwen2 down (136 MB) or o (26 MB) projection (residual + the next RMSNorm's statistics) and
-    the gate/up (272 MB, SwiGLU + the RMSNorm consumer): each as two launches on the row halves (a duplex tick with
-    chat prefixes; k_gemm_xsk for down and gate/up, the one-row-tile split-K kernels for o), whose statistics groups
-    tile one [M][groups] layout; vs an fp64 residual -> RMSNorm -> SwiGLU reference."""
+    the gate/up (272 MB, SwiGLU + the RMSNorm consumer).  rows 1 (default): down and gate/up through k_gemm_rows (the
+    4 waves split the rows, the weights stream once through an LDS-DMA ring; k_gemm_reduce runs the epilogue); rows 0
+    (fo_gemm_set_rows): two launches on the row halves (k_gemm_xsk).  o always on the row halves (the one-row-tile
+    split-K kernels), whose statistics groups tile one [M][groups] layout with the reduce's; vs an fp64 residual ->
+    RMSNorm -> SwiGLU reference."""
+    from fo import _lib, ops
+    from fo.ops import PackedLinear
+    lib = _lib.load()
+    prev = lib.fo_gemm_set_rows(rows)
+    try:
+        _qwen2_65_128(dev, M, producer, rows)
+    finally:
+        lib.fo_gemm_set_rows(prev)
+
+
+def _qwen2_65_128(dev, M, producer, rows):
     from fo import ops
     from fo.ops import PackedLinear
     g = torch.Generator().manual_seed(M)
@@ -145,8 +159,12 @@ def test_gemm_row_halves_on_qwen2_streams(dev, M, producer):
     out = gu(yg, norm=(st, 1e-6))
     torch.cuda.synchronize()
     c = ops.launch_counts()
-    assert c["gemm_xsk"] == (4 if producer == "down" else 2), c   # two row halves per GEMM
-    assert c["gemm_reduce"] == 4, c
+    if rows:
+        assert c["gemm_rows"] == (2 if producer == "down" else 1) and c["gemm_xsk"] == 0, c
+        assert c["gemm_reduce"] == (2 if producer == "down" else 3), c
+    else:
+        assert c["gemm_xsk"] == (4 if producer == "down" else 2) and c["gemm_rows"] == 0, c   # two row halves each
+        assert c["gemm_reduce"] == 4, c
     y = res.double() + hin.double() @ wd.double().t()
     torch.testing.assert_close(x.cpu().double(), y, rtol=1e-5, atol=1e-4)
     h = y * torch.rsqrt((y * y).mean(-1, keepdim=True) + 1e-6) * gamma.double()

@@ -193,8 +193,8 @@ def _group_pipe(eng, feats_seq, n_users, C, decide=None):
 @pytest.mark.parametrize("C,n_chunks", [(2, 9), (4, 10), (3, 3)])
 def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
     """C consecutive chunks per Qwen2 stage (fo.engine.ListenGroupGraph, the offline input's listen): every chunk's
-    state probabilities (1e-4) and last hidden row (2e-4 of the row's scale) equal the one-chunk-per-stage pipe's to fp32
-    rounding (the encoder and Qwen2 GEMMs tile C x the rows), its pe_index and the context lengths exactly; a partial
+    state probabilities (1e-4) and last hidden row (1e-3, the oracle-parity bound) equal the one-chunk-per-stage
+    pipe's (the encoder and Qwen2 GEMMs tile C x the rows), its pe_index and the context lengths exactly; a partial
     last group (n_chunks % C) is flushed."""
     g = np.load(os.path.join(G, "fbank.npz"))
     n_users = 3
@@ -203,14 +203,20 @@ def test_listen_group_pipe_matches_one_chunk_per_stage(eng, dev, C, n_chunks):
     ref, lens_ref, _ = _group_pipe(eng, seq, n_users, 1)
     got, lens, _ = _group_pipe(eng, seq, n_users, C)
     assert len(got) == len(ref) == n_chunks and lens == lens_ref
+    worst = 0.0
     for (pr, hr, qr), (pg, hg, qg) in zip(ref, got):
         assert qr == qg
         # (the batched-vs-single bound of tests/test_duplex_gpu.py: the two pipes' graphs tile the Qwen2 stage and its
         # attention splits differently)
         np.testing.assert_allclose(np.array(pg), np.array(pr), atol=1e-4)
         for a, b in zip(hg, hr):
-            # (the grouped encoder runs its norms and GEMMs over C x the rows: other kernels, fp32 rounding apart)
-            np.testing.assert_allclose(a, b, atol=2e-4 * float(np.abs(b).max()), rtol=1e-4)
+            # (the grouped encoder and Qwen2 stage run their norms and GEMMs over C x the rows: other kernels, other fp32
+            # summation orders, amplified through the encoder and Qwen2 blocks; test_grouped_encoder_pass_equals_chunk_by_
+            # chunk holds the encoder alone to 2e-5.  The bound is the oracle-parity tolerance of these rows,
+            # tests/test_parity_r02_gpu.py: atol 1e-3)
+            worst = max(worst, float(np.abs(a - b).max()))
+            np.testing.assert_allclose(a, b, atol=1e-3, rtol=1e-4)
+    print(f"[listen group C={C}] worst hidden-row deviation {worst:.2e} abs")
 
 
 def test_listen_group_pipe_decide_rolls_back_the_rest(eng, dev):

@@ -438,3 +438,45 @@ def test_load_checkpoint_binds_final_pt(pipe, tmp_path):
         pipe.model.engine.src = orig_src
         pipe.model.engine.rebind_audiollm({})
         pipe.model.rebind()
+
+
+@pytest.mark.parametrize("kind", ["tiny", "real2"])
+def test_grouped_encoder_pass_equals_chunk_by_chunk(dev, kind):
+    """SpeechEncoderEngine.run(chunks=m) against m one-chunk infer() calls on twin caches: full groups of 4 and a
+    partial 2 of 3 sessions, from an empty ring into a trimmed one.  The grouped pass runs its GEMMs and norms over m x
+    the rows (other tilings, so other fp32 summation orders) -- the rows agree to 2e-5 of the output scale, i.e. to
+    fp32 rounding; a ring or metadata slip would show at the 1e-1 level."""
+    from fo.speech import SpeechEncoderEngine
+    from fo.weights import SynthSource
+    cfg = configs.get("tiny") if kind == "tiny" else T2
+    src = SynthSource(cfg["seed"], encoder_shapes(cfg, "user"), dev, cfg["overrides"])
+    enc = SpeechEncoderEngine(src, cfg, "user", dev, max_sessions=8)
+    B, R = 3, 19
+    T = enc.dims(R)[2]
+    rng = np.random.default_rng(5)
+    seq, grp = [enc.new_cache() for _ in range(B)], [enc.new_cache() for _ in range(B)]
+    pe_s, pe_g = [0] * B, [0] * B
+    worst = 0.0
+    for m in (4, 4, 2, 4):
+        feats = [torch.from_numpy((rng.standard_normal((B, R, 80)) * 3).astype(np.float32)).to(dev) for _ in range(m)]
+        want = []
+        for j in range(m):
+            out, _, pe_s = enc.infer(feats[j], seq, pe_s)
+            want.append(out.clone())
+        bufs = enc.buffers(m * B, R)
+        metas = []
+        for j in range(m):
+            meta, pe_g = enc.host_meta(grp, pe_g)
+            metas.append(meta)
+            enc.advance(grp, T)
+        bufs["meta"].copy_(torch.from_numpy(np.concatenate(metas)).to(dev))
+        got, _ = enc.run(torch.cat(feats).contiguous(), B, R, bufs, chunks=m)
+        torch.cuda.synchronize()
+        assert pe_g == pe_s
+        for j in range(m):
+            g, w = got[j * B * T:(j + 1) * B * T], want[j]
+            d = float((g - w).abs().max() / w.abs().max())
+            worst = max(worst, d)
+            assert d < 2e-5, (m, j, d)
+        assert [(c.start, c.len) for c in seq] == [(c.start, c.len) for c in grp]
+    print(f"[grouped encoder {kind}] worst row deviation {worst:.2e} of the output scale")
