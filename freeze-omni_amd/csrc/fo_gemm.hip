@@ -1529,19 +1529,21 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int
 
 // ---- 65..128-row weight streams (k_gemm_rows): the weights once, every row block on the matrix cores.
 // A listen group of C chunks x 8 users x 2 tokens puts 128 rows through every Qwen2 GEMM (fo.engine.ListenGroupGraph,
-// C = 8); the X-stationary kernels hold one row block per 16 K-slice waves and run 65..128 rows as two 64-row launches
-// (the weights twice, k_gemm_xsk's per-unit cross-wave reduction each time).  Here the 4 waves of a workgroup split the
-// ROWS instead (wave w: row blocks RPW w .. RPW w + RPW - 1) and share each k-step's weight fragments through LDS, so
-// there is no cross-wave reduction and each weight byte is read from HBM once:
+// C = 8); the X-stationary kernels hold X per K-slice wave and ran 65..128 rows as two 64-row launches (the weights
+// twice, k_gemm_xsk's per-unit cross-wave reduction each time).  Here the NWV waves of a workgroup split the ROWS
+// (wave w: row blocks RPW w .. RPW w + RPW - 1; shipped: 8 waves x 1 row block) and share each k-step's weight
+// fragments through LDS, so there is no cross-wave reduction and each weight byte is read from HBM once:
 //  * one LDS-DMA loader ring per workgroup (global_load_lds_dwordx4, issued by every wave for its share): DW k-steps
-//    of the workgroup's <= 4 TPW weight tiles ahead, DX k-steps of its fp32 X rows ahead (X comes from L2);
+//    of the workgroup's NTC weight tiles ahead, DX k-steps of its fp32 X rows ahead (X comes from L2; XL = 1: each X
+//    load fetches 8 whole rows, laid out so the consumers' reads stay conflict-free);
 //  * per k-step: one s_waitcnt on this wave's own DMA (the count of the DX - 1 younger k-steps' loads, fixed by
 //    padding every k-step to the same number of loads), one workgroup barrier (every wave's loads landed, and every
-//    wave is past the slot the next loads overwrite), then the wave's X fragments split into bf16 hi / lo and
+//    wave is past the slot the next loads overwrite), then the wave's X fragment split into bf16 hi / lo and
 //    2 RPW MFMAs per tile;
 //  * workgroups = S K-splits x G tile groups (XCD-aware as k_gemm_xsk); each writes its fp32 partial tiles to split
-//    S's slab and k_gemm_reduce (the next launch) sums the slabs in split order and runs every epilogue (SwiGLU, the
-//    RMSNorm rstd, residual, row statistics).  Gate/up: S = 1 (one slab: the reduce is the epilogue pass).
+//    sp's slab and k_gemm_reduce (the next launch) sums the slabs in split order and runs every epilogue (SwiGLU, the
+//    RMSNorm rstd, residual, row statistics).  A workgroup's X over its K range passes through the CU beside its
+//    weights, so the host splits K until the two are comparable (gemm_impl: gate/up thirds, down 16 slices).
 // The loads are asm (the compiler's own wait placement treats an LDS-DMA as aliasing every later LDS read and drains
 // the whole ring before each one); nothing else in the loop touches vector memory, so the manual counts are exact.
 template <bool NT = false>   // NT: the streaming (non-temporal) policy -- weights that must not evict X from L2
@@ -1692,9 +1694,6 @@ __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int t
         xp[r][1] = xr[i % PX][wave * RPW + r][xh0][xs1];
       }
     }
-    bf16x8 wf[NTC];
-#pragma unroll
-    for (int t = 0; t < NTC; ++t) wf[t] = wr[i % PW][t][lane];
     bf16x8 xh[RPW], xl[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
@@ -1707,15 +1706,28 @@ __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int t
         xl[r][e] = (__bf16)(f[e] - (float)h);
       }
     }
-    // hi products of every (tile, row block), then the lo ones: no accumulator is read right after it is written
+    // the weight fragments in groups of TG (all of them up to 20 tiles: VGPRs), each group's hi products of every
+    // (tile, row block) and then the lo ones: no accumulator is read right after it is written
+    constexpr int TG = NTC <= 20 ? NTC : (NTC + 1) / 2;
 #pragma unroll
-    for (int t = 0; t < NTC; ++t)
+    for (int t0 = 0; t0 < NTC; t0 += TG) {
+      bf16x8 wf[TG];
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[r], wf[t], acc[t][r], 0, 0, 0);
+      for (int t = 0; t < TG; ++t)
+        if (t0 + t < NTC) wf[t] = wr[i % PW][t0 + t][lane];
 #pragma unroll
-    for (int t = 0; t < NTC; ++t)
+      for (int t = 0; t < TG; ++t)
+        if (t0 + t < NTC)
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) acc[t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl[r], wf[t], acc[t][r], 0, 0, 0);
+          for (int r = 0; r < RPW; ++r)
+            acc[t0 + t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[r], wf[t], acc[t0 + t][r], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+        if (t0 + t < NTC)
+#pragma unroll
+          for (int r = 0; r < RPW; ++r)
+            acc[t0 + t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl[r], wf[t], acc[t0 + t][r], 0, 0, 0);
+    }
   }
   wait_vm<0>();   // (the padding loads past the last k-step) nothing of this workgroup's DMA outlives it
   const int Ncols = a.ntiles * 16;
@@ -2013,22 +2025,27 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   {
     const int nt_all = (swiglu ? 2 : 1) * ((N + 15) / 16);
     const long long wb = (long long)nt_all * 16 * K * 2;
-    if (g_rows && M > 64 && M <= 128 && x_f32 && !lnw && !rope && !sout1 && !rstats1 && splitk <= 1 &&
-        wb >= ((long long)g_xsk_min_mb << 20) && (ldx % 4) == 0 && !xpk.p0 && !xp32k.p0 && !g_force_nt &&
+    // (>= 16 MiB: the Qwen2 q|k|v -- RoPE + paged-KV append in the reduce -- and o too, which at 128 rows ran 64-row
+    // tiles re-reading the weights per row tile (q|k|v 80 us, r06q) or two row halves (o 2 x 22.8 us))
+    if (g_rows && M > 64 && M <= 128 && x_f32 && !lnw && !sout1 && !rstats1 && splitk <= 1 &&
+        wb >= (16ll << 20) && (ldx % 4) == 0 && !xpk.p0 && !xp32k.p0 && !g_force_nt &&
         !g_force_nw && (!swiglu || nt_all % 2 == 0)) {
       const int cus = num_cus();
-      if (g_rows != 2) {   // k_gemm_rows: the waves split the rows
-        if (swiglu) {   // gate/up: whole (gate, up) pairs per workgroup, every workgroup the same count, one K pass
-          const int units = nt_all / 2, per = (units + cus - 1) / cus;
+      if (g_rows != 2) {   // k_gemm_rows: the waves split the rows.  The workgroup's X (all rows over its K range)
+        // comes through the CU beside its weights, so K is split until a workgroup's tiles carry about as many bytes
+        // as its X: gate/up 3 K thirds x 14 (gate, up) pairs (28 tiles), one round of <= 256 workgroups; down 16 K
+        // slices x 14 tiles (profiles/r06o_gemm_rows_split.txt, r06p: gate/up at 128 rows 129.4 us on one K pass of
+        // 10 tiles, 102.7-110.0 on K halves of 20, 101.9 on thirds; down 68.9 on 8 slices of 7 tiles, 59.6-63.9)
+        const int ks = g_rows == 3 ? 2 : 3;   // (probe 3: K halves, 10 pairs)
+        if (swiglu) {
+          const int units = nt_all / 2, per = (ks * units + cus - 1) / cus;
           rows_tp = 2 * per;
           rows_G = (units + per - 1) / per;
-          rows_S = 1;
-        } else {        // long-K (down): <= 8 tiles per workgroup and K split until the grid covers the CUs
-          const int g8 = (nt_all + 7) / 8;
-          rows_S = max(1, min(8, (cus + g8 / 2) / g8));
-          const int gw = max(1, cus / rows_S);
-          rows_tp = min(8, (nt_all + gw - 1) / gw);
+          rows_S = ks;
+        } else {
+          rows_tp = nt_all % 14 == 0 ? 14 : 16;
           rows_G = (nt_all + rows_tp - 1) / rows_tp;
+          rows_S = max(1, min(16, cus / rows_G));
         }
       } else {             // (probe) k_gemm_wrow: one tile per wave; gate/up 10 waves (5 pairs), one K pass; long-K 14 / 8
         rows_tp = swiglu ? ((nt_all / 2) % 5 == 0 ? 10 : 8) : (nt_all % 14 == 0 ? 14 : 8);
@@ -2036,7 +2053,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
         rows_S = swiglu ? 1 : max(1, min(16, cus / rows_G));
       }
       const long long need = (long long)rows_S * 128 * nt_all * 16;
-      rows_ok = rows_tp <= (g_rows == 2 ? 14 : (swiglu ? 12 : 8)) && need <= ws_floats && ws != nullptr &&
+      rows_ok = rows_tp <= (swiglu ? 30 : 16) && need <= ws_floats && ws != nullptr &&
                 (K >> 5) >= rows_S;
     }
   }
@@ -2141,7 +2158,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     if (sgroups) *sgroups = (N + 255) / 256;
     const int total = rows_S * rows_G;
     const dim3 grid(8 * ((total + 7) / 8));
-    // (instantiated tile counts: the Qwen2 gate/up's 5 pairs and down's 7 tiles per workgroup, else the slot count)
+    // (instantiated tile counts: the Qwen2 gate/up's 14 pairs and down's 14 tiles per workgroup, else the next size)
 #define FO_ROWS(NWV_, RPW_, NTC_, DW_, DX_, PR_, XL_)                                                               \
   hipLaunchKernelGGL((k_gemm_rows<NWV_, RPW_, NTC_, DW_, DX_, false, PR_, XL_>), grid, dim3(NWV_ * 64), 0, stream, a, \
                      rows_G, rows_tp)
@@ -2151,14 +2168,14 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
       if (rows_tp == 10) FO_WROW(10, 12, 4);
       else if (rows_tp == 14) FO_WROW(14, 8, 4);
       else FO_WROW(8, 12, 4);
-    } else if (swiglu && rows_tp <= 10) {
-      FO_ROWS(8, 1, 10, 5, 4, 0, 1);
+    } else if (swiglu && rows_tp > 20) {
+      FO_ROWS(8, 1, 30, 3, 1, 0, 1);
     } else if (swiglu) {
-      FO_ROWS(8, 1, 12, 5, 3, 0, 1);
-    } else if (rows_tp <= 7) {
-      FO_ROWS(8, 1, 7, 7, 4, 0, 1);
+      FO_ROWS(8, 1, 20, 3, 2, 0, 1);    // (probe 3)
+    } else if (rows_tp == 14) {
+      FO_ROWS(8, 1, 14, 5, 3, 0, 1);
     } else {
-      FO_ROWS(8, 1, 8, 7, 4, 0, 1);
+      FO_ROWS(8, 1, 16, 4, 3, 0, 1);
     }
 #undef FO_WROW
 #undef FO_ROWS
@@ -2527,7 +2544,7 @@ int fo_gemm_set_xsk_min_mb(int mb) {
 }
 
 int fo_gemm_set_rows(int on) {
-  FO_REQUIRE(on >= 0 && on <= 2, "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows) or 2 (probe: k_gemm_wrow)");
+  FO_REQUIRE(on >= 0 && on <= 3, "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows), probes 2 (k_gemm_wrow), 3 (K halves)");
   const int prev = g_rows;
   g_rows = on;
   return prev;

@@ -27,7 +27,7 @@ for M in Ms:
     og = [torch.empty(M, I, device=dev) for _ in range(copies)]
     od = [torch.zeros(M, D, device=dev) for _ in range(copies)]
     res = {}
-    for on in (1, 2, 0):
+    for on in (1, 3, 2, 0):
         lib.fo_gemm_set_rows(on)
         yg = gus[0](xg, M=M).clone()
         yd = torch.zeros(M, D, device=dev)
@@ -39,7 +39,7 @@ for M in Ms:
         td = min(graph_time(lambda: (lambda i: downs[i](xd, out=od[i], residual=True, M=M))(next(it) % copies), 8)
                  for _ in range(2))
         res[on] = (tg, td, yg, yd)
-        name = {1: "k_gemm_rows", 2: "k_gemm_wrow (probe)", 0: "row halves / xsk"}[on]
+        name = {1: "k_gemm_rows", 3: "rows, gate/up K halves", 2: "k_gemm_wrow (probe)", 0: "row halves / xsk"}[on]
         print(f"M={M:4d} {name:18s} gate/up {tg:7.2f} us ({2 * I * D * 2 / tg / 1e6:4.2f} TB/s)  "
               f"down {td:7.2f} us ({I * D * 2 / td / 1e6:4.2f} TB/s)", flush=True)
     lib.fo_gemm_set_rows(1)
