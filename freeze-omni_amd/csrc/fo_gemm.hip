@@ -789,17 +789,17 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a) {
 
 // Sum of the S partial slabs + epilogue for the split-K path.  Grid (ceil(N/256), M): one row
 // chunk of 256 columns per block, which is also the statistics group for a fused normalisation.
-__global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mrows) {
+template <int SQ>   // slabs whose loads are issued up front (8; 16 for the 16-slab k_gemm_rows down / o)
+__global__ __launch_bounds__(256) void k_gemm_reduce_t(GemmArgs a, int sw, int Mrows) {
   __shared__ float red_s[4];
   const int Ncols = a.ntiles * 16;
   const size_t slab = (size_t)Mrows * Ncols;
   const int m = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
-  // Every load of the launch is issued up front -- up to 8 slabs' partials, the epilogue operands and the
+  // Every load of the launch is issued up front -- up to SQ slabs' partials, the epilogue operands and the
   // producer's RMSNorm partial sums -- so the kernel pays ONE dependent memory round trip before its sum
   // (the slabs are still summed in slab order: the same result bit for bit).  The epilogue operand loads are
   // branch-free (g_zeros when an operand does not apply), so no divergent branch makes the compiler's vmcnt
   // accounting wait early.
-  constexpr int SQ = 8;
   const bool rope = a.rq != nullptr;
   const int ncol = rope ? a.N / 2 : a.N;
   const bool live = n < ncol;
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       v += tv[j];
       u += tu[j];
     }
-  for (int q = SQ; q < a.S; ++q) {   // more than 8 slabs (not used by the policies in fo_gemm)
+  for (int q = SQ; q < a.S; ++q) {   // more than SQ slabs (not used by the policies in fo_gemm)
     v += p[q * slab];
     if (pair) u += p[q * slab + 16];
   }
@@ -886,6 +886,13 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs a, int sw, int Mro
       if (a.ypkh) xpack_store(a.ypkh, a.ypkl, m, n, vg, a.prb);
     }
   }
+}
+
+// (the partials of more than 8 slabs prefetched only when there are: the 16 registers cost the paired (SwiGLU / RoPE)
+// 3-slab gate/up reduce 15.5 -> 17.4 us, r06t)
+inline void launch_reduce(const GemmArgs& a, int sw, int Mrows, int N, int M, hipStream_t stream) {
+  if (a.S > 8) hipLaunchKernelGGL(k_gemm_reduce_t<16>, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, sw, Mrows);
+  else hipLaunchKernelGGL(k_gemm_reduce_t<8>, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, sw, Mrows);
 }
 
 template <int NT, int RB, bool XF32, int NW, int U, bool SW>
@@ -2027,7 +2034,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     const long long wb = (long long)nt_all * 16 * K * 2;
     // (>= 16 MiB: the Qwen2 q|k|v -- RoPE + paged-KV append in the reduce -- and o too, which at 128 rows ran 64-row
     // tiles re-reading the weights per row tile (q|k|v 80 us, r06q) or two row halves (o 2 x 22.8 us))
-    if (g_rows && M > 64 && M <= 128 && x_f32 && !lnw && !sout1 && !rstats1 && splitk <= 1 &&
+    if (g_rows && M > (g_rows == 4 ? 32 : 64) && M <= 128 && x_f32 && !lnw && !sout1 && !rstats1 && splitk <= 1 &&
         wb >= (16ll << 20) && (ldx % 4) == 0 && !xpk.p0 && !xp32k.p0 && !g_force_nt &&
         !g_force_nw && (!swiglu || nt_all % 2 == 0)) {
       const int cus = num_cus();
@@ -2036,7 +2043,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
         // as its X: gate/up 3 K thirds x 14 (gate, up) pairs (28 tiles), one round of <= 256 workgroups; down 16 K
         // slices x 14 tiles (profiles/r06o_gemm_rows_split.txt, r06p: gate/up at 128 rows 129.4 us on one K pass of
         // 10 tiles, 102.7-110.0 on K halves of 20, 101.9 on thirds; down 68.9 on 8 slices of 7 tiles, 59.6-63.9)
-        const int ks = g_rows == 3 ? 2 : 3;   // (probe 3: K halves, 10 pairs)
+        const int ks = (g_rows == 3 || M <= 64) ? 2 : 3;   // (probe 3: K halves, 10 pairs)
         if (swiglu) {
           const int units = nt_all / 2, per = (ks * units + cus - 1) / cus;
           rows_tp = 2 * per;
@@ -2181,7 +2188,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
 #undef FO_ROWS
     int rc = fo::check_launch("fo_gemm/rows");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, 128);
+    launch_reduce(a, swiglu, 128, N, M, stream);
     fo::count_launch(FO_L_GEMM_ROWS);
     fo::count_launch(FO_L_GEMM_REDUCE);
     return fo::check_launch("fo_gemm/rows reduce");
@@ -2245,7 +2252,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     else hipLaunchKernelGGL((k_gemm_xsk<8, 3, 4, 4>), grid, dim3(512), 0, stream, a, units, G);
     int rc = fo::check_launch("fo_gemm/xsk");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, RBk * 16);
+    launch_reduce(a, swiglu, RBk * 16, N, M, stream);
     fo::count_launch(FO_L_GEMM_XSK);
     fo::count_launch(FO_L_GEMM_REDUCE);
     if (a.ypkh) fo::count_launch(FO_L_GEMM_YPACK);
@@ -2463,7 +2470,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   if (S > 1 && !merged) {
     int rc = fo::check_launch("fo_gemm/split");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gemm_reduce, dim3((N + 255) / 256, M), dim3(256), 0, stream, a, swiglu, mt * RB * 16);
+    launch_reduce(a, swiglu, mt * RB * 16, N, M, stream);
     fo::count_launch(FO_L_GEMM_REDUCE);
   }
   return fo::check_launch("fo_gemm");
@@ -2544,7 +2551,8 @@ int fo_gemm_set_xsk_min_mb(int mb) {
 }
 
 int fo_gemm_set_rows(int on) {
-  FO_REQUIRE(on >= 0 && on <= 3, "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows), probes 2 (k_gemm_wrow), 3 (K halves)");
+  FO_REQUIRE(on >= 0 && on <= 4,
+             "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows), probes 2 (k_gemm_wrow), 3 (K halves), 4 (from 33 rows)");
   const int prev = g_rows;
   g_rows = on;
   return prev;
