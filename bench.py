@@ -1153,10 +1153,12 @@ def main():
                   "first_audio_ms": round((s1["first"][0] - s1["t_ss"]) * 1e3, 2),
                   "first_pcm_ms": round((s1["first_pcm"][0] - s1["t_ss"]) * 1e3, 2),
                   "rtf_per_user": round(a1 / (s1["last"][0] - s1["t_ss"]), 3)}
-    # the dominant kernel by time in the turn: with C >= 2 chunks per listen stage the listen's gate/up and down run at
-    # 2 x users x C rows on the split-K stream (k_gemm_xsk), ahead of the text steps' <= 16-row gate/up (k_gemm_xs)
+    # the dominant kernel by time in the turn (r06v rocprof: 12.9 % of kernel time): the text steps' gate/up SwiGLU at
+    # `users` rows (k_gemm_xs, 33 steps x 28 layers), ahead of the grouped listen's gate/up (k_gemm_rows at
+    # 2 x users x C rows, 8 stages x 28 layers: 6.4 %), which is reported beside it (listen_kernel)
     group_rows = 2 * args.users * args.listen_chunks if args.pipeline else 2 * args.users
-    probe = gemm_probe(eng, group_rows, down=16 < group_rows <= 128)
+    probe = gemm_probe(eng, args.users)
+    probe_l = gemm_probe(eng, group_rows, down=16 < group_rows <= 64) if group_rows > 16 else None
     codec_ok, codec_n = codec_ids_check(eng)
     n_chunks = int(math.ceil(n_samp / 2560))
     roof_ms, roof_units = turn_roofline(eng, args.users, n_chunks, args.text_tokens,
@@ -1177,22 +1179,30 @@ def main():
         # VAR 0, spelled out in the kernel name since round 5; the probe variants 1-4 never run in the bench); with
         # listen groups of 17..64 rows the split-K stream of their gate/up and down, RB = ceil(rows / 16)
         rb = (group_rows + 15) // 16
-        if group_rows <= 16:
-            kre = r"k_gemm_xs<\d+, \d+(, 0)?>"
-            kname = "k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M=16, all 28 layers in turn)"
-        elif group_rows <= 64:
-            kre = rf"k_gemm_xsk<\d+, \d+, {rb}, \d+>"
-            kname = (f"k_gemm_xsk<8,KPW,{rb},UA> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and down "
-                     f"split-K weight streams, M={group_rows}, all 28 layers in turn; per launch = the mean of a "
-                     f"gate/up and a down, reduce included)")
+        kre = r"k_gemm_xs<\d+, \d+(, 0)?>"
+        kname = (f"k_gemm_xs<16,7> (Qwen2 gate/up SwiGLU X-stationary weight stream, M={args.users}: the text steps, "
+                 f"all 28 layers in turn)")
+        if group_rows <= 64:
+            kre_l = rf"k_gemm_xsk<\d+, \d+, {rb}, \d+>"
+            kname_l = (f"k_gemm_xsk<8,KPW,{rb},UA> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and "
+                       f"down split-K weight streams, M={group_rows}; per launch = the mean of a gate/up and a down)")
         else:
-            kre = r"k_gemm_rows<"
-            kname = (f"k_gemm_rows<8,1,NTC,DW,DX> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU and "
-                     f"down weight streams at M={group_rows}: 8 waves split the rows, the weight fragments shared "
-                     f"through an LDS-DMA ring; all 28 layers in turn; per launch = the mean of a gate/up and a down, "
-                     f"reduce included)")
+            kre_l = r"k_gemm_rows<8, 1, 30,"
+            kname_l = (f"k_gemm_rows<8,1,30,3,1> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU weight "
+                       f"stream at M={group_rows}: 8 waves split the rows, the weight fragments shared through an "
+                       f"LDS-DMA ring, K in thirds; all 28 layers in turn, reduce included)")
         traffic, traffic_src = recorded_traffic(kre)
         rp_us, rp_calls, rp_src = recorded_kernel_avg_us(kre)
+        listen_kernel = None
+        if probe_l is not None:
+            tr_l, _ = recorded_traffic(kre_l)
+            rl_us, rl_calls, _ = recorded_kernel_avg_us(kre_l)
+            listen_kernel = {"kernel": kname_l, "achieved": round(probe_l["gbps"], 1), "unit": "GB/s",
+                             "frac": round(probe_l["gbps"] / 8000.0, 4), "bytes_per_launch": probe_l["bytes"],
+                             "avg_launch_us": round(probe_l["seconds"] * 1e6, 2),
+                             "traffic": None if tr_l is None else round(tr_l),
+                             "rocprof_avg_launch_us": None if rl_us is None else round(rl_us, 2),
+                             "rocprof_calls": rl_calls}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -1236,9 +1246,10 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": kname,
                          "bytes_per_launch": probe["bytes"], "avg_launch_us": round(probe["seconds"] * 1e6, 2),
-                         "frac_source": "live: HIP events around every layer's gate/up (and down) launch on the engine "
-                                        "stream (gemm_probe); rocprof_* = the committed rocprofv3 summary of this "
-                                        "command (split-K: the stream kernel alone, its reduce not included)",
+                         "frac_source": "live: HIP events around every layer's gate/up launch on the engine stream "
+                                        "(gemm_probe); rocprof_* = the committed rocprofv3 summary of this command "
+                                        "(split-K kernels: the stream kernel alone, its reduce not included)",
+                         "listen_kernel": listen_kernel,
                          "rocprof_avg_launch_us": None if rp_us is None else round(rp_us, 2),
                          "rocprof_calls": rp_calls,
                          "rocprof_frac": None if rp_us is None else round(probe["bytes"] / (rp_us * 1e-6) / 1e9 / peak, 4),

@@ -49,7 +49,7 @@ for S in "$@"; do
              > ${O}_quick.log 2>&1; rc=$?; [ $rc -eq 0 ] && line ${O}_quick.log ;;
     prof)  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOTD/${O}_prof -o bench -f csv -- \
              python3 $ROOTD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-single-user) > ${O}_prof.log 2>&1; rc=$? ;;
-    fetch) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gemm_xs -d $ROOTD/${O}_pmc \
+    fetch) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_gemm_xs|k_gemm_rows" -d $ROOTD/${O}_pmc \
              -o fetch -f csv -- python3 $ROOTD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-single-user) \
              > ${O}_pmc.log 2>&1; rc=$? ;;
     fetchdup) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_gemm_xsk|k_subsample|k_enc" \
