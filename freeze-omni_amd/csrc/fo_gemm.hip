@@ -1587,7 +1587,10 @@ __device__ __forceinline__ void wait_vm_barrier() {
 // (each load touches 16 rows x half a line); 1: load h fetches rows 8 h .. 8 h + 7 whole (8 full 128-B lines), lane
 // f = 8 c + (r & 7) + 8 h (mod 64) holding chunk c of row r, which keeps the consumer's two ds_read_b128 free of
 // bank conflicts (its 16-lane groups read 16 consecutive 16-B slots)
-template <int NWV, int RPW, int NTC, int DW, int DX, bool WNT = false, int PROBE = 0, int XL = 0>
+// CM: the consumer map.  0: wave w computes row block w (RPW of them) for every tile; 1 (8 waves, RPW 1): wave w
+// computes row blocks 2 (w & 3) and 2 (w & 3) + 1 for half the tiles (w >> 2) -- each weight fragment is read from LDS
+// by 4 waves instead of 8 (the loads are distributed as for CM 0)
+template <int NWV, int RPW, int NTC, int DW, int DX, bool WNT = false, int PROBE = 0, int XL = 0, int CM = 0>
 __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int tiles_per) {
   constexpr int RB = NWV * RPW;
   constexpr int LPW = (NTC + NWV - 1) / NWV;   // weight loads per wave per k-step (tile t: wave t % NWV)
@@ -1666,11 +1669,16 @@ __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int t
       }
     }
   };
-  f32x4 acc[NTC][RPW];
+  static_assert(CM == 0 || (NWV == 8 && RPW == 1), "k_gemm_rows: the split consumer map is for 8 waves x 1 block");
+  constexpr int RBW = CM ? 2 : RPW;                 // row blocks a wave computes
+  constexpr int NTW = CM ? (NTC + 1) / 2 : NTC;     // tiles a wave computes
+  const int rbw0 = CM ? 2 * (wave & 3) : wave * RPW;
+  const int tw0 = CM ? (wave >> 2) * NTW : 0;
+  f32x4 acc[NTW][RBW];
 #pragma unroll
-  for (int t = 0; t < NTC; ++t)
+  for (int t = 0; t < NTW; ++t)
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < RBW; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
   // prologue in the loop's issue order (k-step j - DW's weights, then k-step j - DX's X, for j = 0 .. DW - 1) so every
   // k-step's wait below sees the same number of younger loads; X of negative k-steps: padding loads
   for (int j = 0; j < DW; ++j) {
@@ -1690,20 +1698,20 @@ __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int t
     issue_x(i + DX);
     // every read of the k-step issued before the first MFMA (one latency per k-step); tiles past the workgroup's nt
     // and row blocks past M are computed on whatever the slots hold and never stored (no branch in the loop)
-    float4 xp[RPW][2];
+    float4 xp[RBW][2];
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) {
+    for (int r = 0; r < RBW; ++r) {
       if constexpr (XL == 0) {
-        xp[r][0] = xr[i % PX][wave * RPW + r][0][lane];
-        xp[r][1] = xr[i % PX][wave * RPW + r][1][lane];
+        xp[r][0] = xr[i % PX][rbw0 + r][0][lane];
+        xp[r][1] = xr[i % PX][rbw0 + r][1][lane];
       } else {
-        xp[r][0] = xr[i % PX][wave * RPW + r][xh0][xs0];
-        xp[r][1] = xr[i % PX][wave * RPW + r][xh0][xs1];
+        xp[r][0] = xr[i % PX][rbw0 + r][xh0][xs0];
+        xp[r][1] = xr[i % PX][rbw0 + r][xh0][xs1];
       }
     }
-    bf16x8 xh[RPW], xl[RPW];
+    bf16x8 xh[RBW], xl[RBW];
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) {
+    for (int r = 0; r < RBW; ++r) {
       const float f[8] = {xp[r][0].x, xp[r][0].y, xp[r][0].z, xp[r][0].w,
                           xp[r][1].x, xp[r][1].y, xp[r][1].z, xp[r][1].w};
 #pragma unroll
@@ -1715,24 +1723,24 @@ __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int t
     }
     // the weight fragments in groups of TG (all of them up to 20 tiles: VGPRs), each group's hi products of every
     // (tile, row block) and then the lo ones: no accumulator is read right after it is written
-    constexpr int TG = NTC <= 20 ? NTC : (NTC + 1) / 2;
+    constexpr int TG = NTW * RBW <= 20 ? NTW : (NTW + 1) / 2;
 #pragma unroll
-    for (int t0 = 0; t0 < NTC; t0 += TG) {
+    for (int t0 = 0; t0 < NTW; t0 += TG) {
       bf16x8 wf[TG];
 #pragma unroll
       for (int t = 0; t < TG; ++t)
-        if (t0 + t < NTC) wf[t] = wr[i % PW][t0 + t][lane];
+        if (t0 + t < NTW) wf[t] = wr[i % PW][min(tw0 + t0 + t, NTC - 1)][lane];
 #pragma unroll
       for (int t = 0; t < TG; ++t)
-        if (t0 + t < NTC)
+        if (t0 + t < NTW)
 #pragma unroll
-          for (int r = 0; r < RPW; ++r)
+          for (int r = 0; r < RBW; ++r)
             acc[t0 + t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh[r], wf[t], acc[t0 + t][r], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < TG; ++t)
-        if (t0 + t < NTC)
+        if (t0 + t < NTW)
 #pragma unroll
-          for (int r = 0; r < RPW; ++r)
+          for (int r = 0; r < RBW; ++r)
             acc[t0 + t][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl[r], wf[t], acc[t0 + t][r], 0, 0, 0);
     }
   }
@@ -1741,14 +1749,14 @@ __global__ __launch_bounds__(NWV * 64) void k_gemm_rows(GemmArgs a, int G, int t
   const int ROWS = RB * 16;
   float* slab = a.ws + (size_t)sp * ROWS * Ncols;
 #pragma unroll
-  for (int t = 0; t < NTC; ++t)
-    if (t < nt)
+  for (int t = 0; t < NTW; ++t)
+    if (tw0 + t < nt && tw0 + t < NTC)
 #pragma unroll
-      for (int r = 0; r < RPW; ++r)
+      for (int r = 0; r < RBW; ++r)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int row = (wave * RPW + r) * 16 + 4 * (lane >> 4) + e;
-          if (row < a.M) slab[(size_t)row * Ncols + (tb + t) * 16 + (lane & 15)] = acc[t][r][e];
+          const int row = (rbw0 + r) * 16 + 4 * (lane >> 4) + e;
+          if (row < a.M) slab[(size_t)row * Ncols + (tb + tw0 + t) * 16 + (lane & 15)] = acc[t][r][e];
         }
 }
 
@@ -2038,12 +2046,17 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
         wb >= (16ll << 20) && (ldx % 4) == 0 && !xpk.p0 && !xp32k.p0 && !g_force_nt &&
         !g_force_nw && (!swiglu || nt_all % 2 == 0)) {
       const int cus = num_cus();
-      if (g_rows != 2) {   // k_gemm_rows: the waves split the rows.  The workgroup's X (all rows over its K range)
+      if (g_rows >= 5) {   // (probes 5 / 6) the one-K-pass 10-tile partition
+        const int units = nt_all / 2, per = (units + cus - 1) / cus;
+        rows_tp = 2 * per;
+        rows_G = (units + per - 1) / per;
+        rows_S = 1;
+      } else if (g_rows != 2) {   // k_gemm_rows: the waves split the rows.  The workgroup's X (all rows over its K range)
         // comes through the CU beside its weights, so K is split until a workgroup's tiles carry about as many bytes
         // as its X: gate/up 3 K thirds x 14 (gate, up) pairs (28 tiles), one round of <= 256 workgroups; down 16 K
         // slices x 14 tiles (profiles/r06o_gemm_rows_split.txt, r06p: gate/up at 128 rows 129.4 us on one K pass of
         // 10 tiles, 102.7-110.0 on K halves of 20, 101.9 on thirds; down 68.9 on 8 slices of 7 tiles, 59.6-63.9)
-        const int ks = (g_rows == 3 || M <= 64) ? 2 : 3;   // (probe 3: K halves, 10 pairs)
+        const int ks = M <= 64 ? 2 : 3;
         if (swiglu) {
           const int units = nt_all / 2, per = (ks * units + cus - 1) / cus;
           rows_tp = 2 * per;
@@ -2166,23 +2179,36 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     const int total = rows_S * rows_G;
     const dim3 grid(8 * ((total + 7) / 8));
     // (instantiated tile counts: the Qwen2 gate/up's 14 pairs and down's 14 tiles per workgroup, else the next size)
-#define FO_ROWS(NWV_, RPW_, NTC_, DW_, DX_, PR_, XL_)                                                               \
-  hipLaunchKernelGGL((k_gemm_rows<NWV_, RPW_, NTC_, DW_, DX_, false, PR_, XL_>), grid, dim3(NWV_ * 64), 0, stream, a, \
-                     rows_G, rows_tp)
+#define FO_ROWS(NWV_, RPW_, NTC_, DW_, DX_, PR_, XL_)                                                                  \
+  do {                                                                                                                \
+    if (g_rows == 3 && PR_ == 0) /* (probe 3: the split consumer map, r06y: 79.3 vs 76.8 us, kept off) */            \
+      hipLaunchKernelGGL((k_gemm_rows<NWV_, RPW_, NTC_, DW_, DX_, false, PR_, XL_, 1>), grid, dim3(NWV_ * 64), 0,       \
+                         stream, a, rows_G, rows_tp);                                                                 \
+    else                                                                                                              \
+      hipLaunchKernelGGL((k_gemm_rows<NWV_, RPW_, NTC_, DW_, DX_, false, PR_, XL_, 0>), grid, dim3(NWV_ * 64), 0,       \
+                         stream, a, rows_G, rows_tp);                                                                 \
+  } while (0)
 #define FO_WROW(NWV_, DW_, DXS_) \
   hipLaunchKernelGGL((k_gemm_wrow<NWV_, 8, DW_, DXS_>), grid, dim3(NWV_ * 64), 0, stream, a, rows_G)
-    if (g_rows == 2) {   // (probe) k_gemm_wrow
+    if (g_rows >= 5) {   // (probes 5 / 6: the 10-tile gate/up without X loads -- WRONG results: the weight ring's
+                         // rate at 7 vs 11 k-steps of depth)
+      if (g_rows == 5) FO_ROWS(8, 1, 10, 7, 1, 1, 1);
+      else FO_ROWS(8, 1, 10, 11, 1, 1, 1);
+    } else if (g_rows == 2) {   // (probe) k_gemm_wrow
       if (rows_tp == 10) FO_WROW(10, 12, 4);
       else if (rows_tp == 14) FO_WROW(14, 8, 4);
       else FO_WROW(8, 12, 4);
     } else if (swiglu && rows_tp > 20) {
-      FO_ROWS(8, 1, 30, 3, 1, 0, 1);
+      // the weights and X the same number of k-steps ahead: vmcnt retires in order, so the wait for a k-step's X also
+      // waits for every weight load issued before it -- an X lead shorter than the weights' caps their depth at it
+      // (r06w: 7 or 11 k-steps of weights alone, 85 us either way; with X 1 ahead the ring held ~1 k-step)
+      FO_ROWS(8, 1, 30, 2, 2, 0, 1);
     } else if (swiglu) {
-      FO_ROWS(8, 1, 20, 3, 2, 0, 1);    // (probe 3)
+      FO_ROWS(8, 1, 20, 3, 3, 0, 1);
     } else if (rows_tp == 14) {
-      FO_ROWS(8, 1, 14, 5, 3, 0, 1);
+      FO_ROWS(8, 1, 14, 4, 4, 0, 1);
     } else {
-      FO_ROWS(8, 1, 16, 4, 3, 0, 1);
+      FO_ROWS(8, 1, 16, 3, 3, 0, 1);
     }
 #undef FO_WROW
 #undef FO_ROWS
@@ -2551,8 +2577,9 @@ int fo_gemm_set_xsk_min_mb(int mb) {
 }
 
 int fo_gemm_set_rows(int on) {
-  FO_REQUIRE(on >= 0 && on <= 4,
-             "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows), probes 2 (k_gemm_wrow), 3 (K halves), 4 (from 33 rows)");
+  FO_REQUIRE(on >= 0 && on <= 6,
+             "fo_gemm_set_rows: 0 (row halves), 1 (k_gemm_rows), probes 2 (k_gemm_wrow), 3 (split consumer map), "
+             "4 (from 33 rows), 5 / 6 (the weight ring alone)");
   const int prev = g_rows;
   g_rows = on;
   return prev;

@@ -96,10 +96,11 @@ int fo_gemm_set_xs_variant(int v);
 /* probe hook: the weight size (MiB) from which 17..64-row fp32 GEMMs take k_gemm_xsk (default 128; long-K >= 32 MiB
  * layers always).  Process-global; returns the previous value. */
 int fo_gemm_set_xsk_min_mb(int mb);
-/* probe hook: 65..128-row GEMMs on >= 128 MiB weights through k_gemm_rows (1, default: the waves split the rows, the
+/* probe hook: 65..128-row GEMMs on >= 16 MiB weights through k_gemm_rows (1, default: the waves split the rows, the
  * weights through an LDS-DMA ring) or as two row-half launches of the <= 64-row kernels (0); probes: 2 = k_gemm_wrow
- * (one tile per wave, X staged once per workgroup), 3 = k_gemm_rows with the gate/up K split in halves instead of
- * thirds.  Unset, FO_GEMM_ROWS decides.  Process-global; returns the previous setting. */
+ * (one tile per wave, X staged once per workgroup), 3 = k_gemm_rows with each wave computing two row blocks for half
+ * the tiles, 4 = k_gemm_rows from 33 rows, 5 / 6 = its weight ring alone (no X loads: WRONG results, timing bounds).
+ * Unset, FO_GEMM_ROWS decides.  Process-global; returns the previous setting. */
 int fo_gemm_set_rows(int on);
 /* probe (scripts/seam_probe.py): the Qwen2 o -> gate/up seam at <= 16 rows as one launch (k_seam_o_gu); xo [M][3584]
  * attention output, wo / wgu packed o and SwiGLU-paired gate/up weights, x the residual stream (updated), yg / sout the

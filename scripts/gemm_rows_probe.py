@@ -27,7 +27,7 @@ for M in Ms:
     og = [torch.empty(M, I, device=dev) for _ in range(copies)]
     od = [torch.zeros(M, D, device=dev) for _ in range(copies)]
     res = {}
-    for on in ((4, 0) if M <= 64 else (1, 3, 2, 0)):
+    for on in ((4, 0) if M <= 64 else ((5, 6, 1) if os.environ.get('ROWS_DEPTH') else (1, 3, 2, 0))):
         lib.fo_gemm_set_rows(on)
         yg = gus[0](xg, M=M).clone()
         yd = torch.zeros(M, D, device=dev)
@@ -39,11 +39,13 @@ for M in Ms:
         td = min(graph_time(lambda: (lambda i: downs[i](xd, out=od[i], residual=True, M=M))(next(it) % copies), 8)
                  for _ in range(2))
         res[on] = (tg, td, yg, yd)
-        name = {1: "k_gemm_rows", 3: "rows, gate/up K halves", 2: "k_gemm_wrow (probe)", 4: "k_gemm_rows (33+ rows)",
+        name = {1: "k_gemm_rows", 3: "rows, split consumer map", 2: "k_gemm_wrow (probe)", 4: "k_gemm_rows (33+ rows)", 5: "PROBE W only, 7 deep", 6: "PROBE W only, 11 deep",
                 0: "row halves / xsk"}[on]
         print(f"M={M:4d} {name:18s} gate/up {tg:7.2f} us ({2 * I * D * 2 / tg / 1e6:4.2f} TB/s)  "
               f"down {td:7.2f} us ({I * D * 2 / td / 1e6:4.2f} TB/s)", flush=True)
     lib.fo_gemm_set_rows(1)
+    if 0 not in res:
+        continue
     k1 = 4 if M <= 64 else 1
     dg = float((res[k1][2] - res[0][2]).abs().max() / res[0][2].abs().max())
     dd = float((res[k1][3] - res[0][3]).abs().max() / res[0][3].abs().max())
