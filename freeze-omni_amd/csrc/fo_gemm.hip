@@ -59,6 +59,7 @@ struct GemmArgs {
   float* rk;
   float* rv;
   int rH, rKVH, rhd, rPS;
+  int rkvb;   // K / V rounded to bf16 as they are appended (fo_set_kv_bf16: the reference's autocast k_proj / v_proj A/B)
   // LayerNorm on load (the pre-norm of a speech-encoder block, models/encoder/transformer.py:103-130):
   // X rows are normalised ((x - mean) * rstd * lnw + lnb) as they are loaded, before the bf16 hi/lo
   // split; mean and variance come from the producer GEMM's per-row partial sums of Y and Y^2
@@ -158,15 +159,19 @@ __device__ __forceinline__ void rope_store(const GemmArgs& a, int m, int n, floa
   if (h < a.rH + a.rKVH) {
     const int p = a.rpos[m];
     const float c = a.rcos[(size_t)p * half + i], sn = a.rsin[(size_t)p * half + i];
-    const float o1 = x1 * c - x2 * sn, o2 = x2 * c + x1 * sn;
+    float o1 = x1 * c - x2 * sn, o2 = x2 * c + x1 * sn;
+    if (a.rkvb && h >= a.rH) {
+      o1 = bf2f(f2bf(o1));
+      o2 = bf2f(f2bf(o2));
+    }
     float* d = h < a.rH ? a.rq + (size_t)m * a.rH * hd + (size_t)h * hd
                         : a.rk + (((size_t)page * a.rKVH + (h - a.rH)) * a.rPS + off) * hd;
     d[i] = o1;
     d[i + half] = o2;
   } else {
     float* d = a.rv + (((size_t)page * a.rKVH + (h - a.rH - a.rKVH)) * a.rPS + off) * hd;
-    d[i] = x1;
-    d[i + half] = x2;
+    d[i] = a.rkvb ? bf2f(f2bf(x1)) : x1;
+    d[i + half] = a.rkvb ? bf2f(f2bf(x2)) : x2;
   }
 }
 // rope_store with the bias already added and the slot / cos / sin loaded ahead (gemm_body EPRE)
@@ -184,6 +189,10 @@ __device__ __forceinline__ void rope_store_pre(const GemmArgs& a, int m, int n, 
                  : a.rk + (((size_t)page * a.rKVH + (h - a.rH)) * a.rPS + off) * hd;
   } else {
     d = a.rv + (((size_t)page * a.rKVH + (h - a.rH - a.rKVH)) * a.rPS + off) * hd;
+  }
+  if (a.rkvb && h >= a.rH) {
+    x1 = bf2f(f2bf(x1));
+    x2 = bf2f(f2bf(x2));
   }
   d[i] = x1;
   d[i + half] = x2;
@@ -1883,6 +1892,12 @@ const bool g_row_split = [] {
   const char* e = getenv("FO_GEMM_ROW_SPLIT");
   return !(e && e[0] == '0');
 }();
+// paged K / V appended by the RoPE epilogues rounded to bf16 (the values a bf16 cache would hold; storage stays fp32):
+// the A/B of a bf16 KV against the fp32 default (FO_KV_BF16=1 or fo_set_kv_bf16)
+int g_kv_bf16 = [] {
+  const char* e = getenv("FO_KV_BF16");
+  return (e && e[0] == '1') ? 1 : 0;
+}();
 // 65..128-row GEMMs on the >= 128 MB weight streams take k_gemm_rows (FO_GEMM_ROWS=0: the row halves above)
 // (probe, fo_gemm_set_rows: 2 = k_gemm_wrow, one tile per wave)
 int g_rows = [] {
@@ -2133,6 +2148,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
   a.rcos = a.rsin = nullptr;
   a.rq = a.rk = a.rv = nullptr;
   a.rH = a.rKVH = a.rhd = a.rPS = 0;
+  a.rkvb = 0;
   a.lnw = lnw;
   a.lnb = lnb;
   a.lneps = lneps;
@@ -2171,6 +2187,7 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     a.rKVH = rope->rKVH;
     a.rhd = rope->rhd;
     a.rPS = rope->rPS;
+    a.rkvb = g_kv_bf16;
   }
   if (rows_ok) {
     a.S = rows_S;
@@ -2573,6 +2590,13 @@ int fo_gemm_set_xsk_min_mb(int mb) {
   FO_REQUIRE(mb >= 0, "fo_gemm_set_xsk_min_mb: %d", mb);
   const int prev = g_xsk_min_mb;
   g_xsk_min_mb = mb;
+  return prev;
+}
+
+int fo_set_kv_bf16(int on) {
+  FO_REQUIRE(on == 0 || on == 1, "fo_set_kv_bf16: 0 or 1");
+  const int prev = g_kv_bf16;
+  g_kv_bf16 = on;
   return prev;
 }
 

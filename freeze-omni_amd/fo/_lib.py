@@ -82,6 +82,7 @@ _SIGS = {
     "fo_attn_max_rows": (c_int, [c_int]),
     "fo_gemm_set_xsk_min_mb": (c_int, [c_int]),
     "fo_gemm_set_rows": (c_int, [c_int]),
+    "fo_set_kv_bf16": (c_int, [c_int]),
     "fo_conv_set_trace": (c_int, [c_vp]),
     "fo_attention_set_trace": (c_int, [c_vp]),
     "fo_subsample": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -102,6 +102,11 @@ int fo_gemm_set_xsk_min_mb(int mb);
  * the tiles, 4 = k_gemm_rows from 33 rows, 5 / 6 = its weight ring alone (no X loads: WRONG results, timing bounds).
  * Unset, FO_GEMM_ROWS decides.  Process-global; returns the previous setting. */
 int fo_gemm_set_rows(int on);
+/* A/B of a bf16 paged KV (verdict r05 item 6; the reference's k_proj / v_proj outputs under torch.autocast(bf16),
+ * models/pipeline.py:67-68): 1 = the q|k|v RoPE epilogues round every appended K / V element to bf16 (storage stays
+ * fp32, so the numerics are a bf16 cache's and the layout is unchanged), 0 = fp32 (default).  Unset, FO_KV_BF16
+ * decides.  Process-global; returns the previous setting. */
+int fo_set_kv_bf16(int on);
 /* probe (scripts/seam_probe.py): the Qwen2 o -> gate/up seam at <= 16 rows as one launch (k_seam_o_gu); xo [M][3584]
  * attention output, wo / wgu packed o and SwiGLU-paired gate/up weights, x the residual stream (updated), yg / sout the
  * next norm's input and partial sums of squares ([M][112]), h the SwiGLU output [M][n_gu_out]; ready: a zeroed int
