@@ -1188,7 +1188,7 @@ def main():
                        f"down split-K weight streams, M={group_rows}; per launch = the mean of a gate/up and a down)")
         else:
             kre_l = r"k_gemm_rows<8, 1, 30,"
-            kname_l = (f"k_gemm_rows<8,1,30,3,1> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU weight "
+            kname_l = (f"k_gemm_rows<8,1,30,2,2> + its k_gemm_reduce (the listen group's Qwen2 gate/up SwiGLU weight "
                        f"stream at M={group_rows}: 8 waves split the rows, the weight fragments shared through an "
                        f"LDS-DMA ring, K in thirds; all 28 layers in turn, reduce included)")
         traffic, traffic_src = recorded_traffic(kre)
