@@ -106,3 +106,30 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     default: return v;
   }
 }
+
+// ---------------------------------------------------------------- LDS-DMA by asm (k_gemm_rows, k_conv_cl)
+// One 16-B-per-lane global -> LDS load the compiler does not see: its own wait placement treats an LDS-DMA as
+// aliasing every later LDS read and drains all of them before each one, so these kernels count their DMA with
+// explicit s_waitcnt instead (the guide's recipe: M0 saved, set, s_nop, load, restored in one statement).
+template <bool NT = false>   // NT: the streaming (non-temporal) policy -- weights that must not evict X from L2
+__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte)
+                 : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte)
+                 : "memory");
+}
+template <typename T>
+__device__ __forceinline__ unsigned lds_addr(T* p) {
+  return (unsigned)(size_t)((__attribute__((address_space(3))) char*)(p));
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}

@@ -1562,28 +1562,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_xsk(GemmArgs a, int units, int
 //    weights, so the host splits K until the two are comparable (gemm_impl: gate/up thirds, down 16 slices).
 // The loads are asm (the compiler's own wait placement treats an LDS-DMA as aliasing every later LDS read and drains
 // the whole ring before each one); nothing else in the loop touches vector memory, so the manual counts are exact.
-template <bool NT = false>   // NT: the streaming (non-temporal) policy -- weights that must not evict X from L2
-__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_byte) {
-  unsigned keep;
-  if constexpr (NT)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_byte)
-                 : "memory");
-  else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_byte)
-                 : "memory");
-}
-template <typename T>
-__device__ __forceinline__ unsigned lds_addr(T* p) {
-  return (unsigned)(size_t)((__attribute__((address_space(3))) char*)(p));
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
+// (dma16 / lds_addr / wait_vm: fo_common.h)
 // this wave's DMA down to N outstanding and its LDS reads done, then the workgroup barrier -- one opaque statement, so
 // the compiler moves no LDS access across it (a bare s_barrier builtin orders no memory)
 template <int N>

@@ -57,7 +57,11 @@ constexpr int CONV_KMAX = 11;
 __host__ __device__ constexpr int nks_per_chunk(int K, int CK) { return ((K * CK + 31) / 32 + 1) & ~1; }
 __host__ __device__ constexpr int conv_wmax(int CK) { return nks_per_chunk(CONV_KMAX, CK); }
 
-template <int MTW, int NTW, int CK, bool TR = false>   // TR: the probe build with per-workgroup clocks (mc.trc)
+// PF: the next Cin chunk's activation window is loaded into registers while this chunk's MFMAs run (issued after the
+// chunk's barrier, converted into LDS after the next one), and the weight fragments come by asm LDS-DMA
+// (fo_common.h dma16) counted by hand -- the builtin's conservative waits would drain the prefetch before the first
+// LDS read of the compute.  Without PF the chunk is staged, then computed (r05o: staging 56-59 % of the chunk loop).
+template <int MTW, int NTW, int CK, bool TR = false, bool PF = false>   // TR: per-workgroup clocks (mc.trc, probes)
 __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
   constexpr int TW = 64 * NTW;     // time steps per workgroup (4 waves x 16*NTW)
   constexpr int ROWS = TW + HALO;
@@ -159,14 +163,65 @@ __global__ __launch_bounds__(256) void k_conv_cl(ConvMulti mc) {
       }
     };
     const int nchunks = a.Cin / CK;
-    for (int c = 0; c < nchunks; ++c) {
-      const unsigned long long c0 = tr ? clock64() : 0;
-      stage(c);
-      const unsigned long long c1 = tr ? clock64() : 0;
-      for (int s = 0; s < a.nks_c; ++s) comp(s);
-      if (tr) {
-        t_stage += c1 - c0;
-        t_comp += clock64() - c1;
+    if constexpr (PF) {
+      float4 v[MAXL];
+      auto load_x = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < MAXL; ++i) {
+          const int e = threadIdx.x + 256 * i;
+          const int row = e / (CK / 4), c4 = e % (CK / 4);
+          const int ti = t0 - a.pad + row;
+          v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (e < span * (CK / 4) && ti >= 0 && ti < a.Tin)
+            v[i] = *reinterpret_cast<const float4*>(xb + (size_t)ti * a.Cin + c * CK + c4 * 4);
+        }
+      };
+      load_x(0);
+      for (int c = 0; c < nchunks; ++c) {
+        const unsigned long long c0 = tr ? clock64() : 0;
+        __syncthreads();  // the previous chunk's (or convolution's) reads of xh / xl / wl are done
+        for (int f = wave; f < MTW * a.nks_c; f += 4) {
+          const int m = f / a.nks_c, st = f - m * a.nks_c;
+          dma16(a.wp + ((size_t)(ct0 + m) * nks + c * a.nks_c + st) * 512 + lane * 8,
+                __builtin_amdgcn_readfirstlane(lds_addr(&wl[f * 512])));
+        }
+#pragma unroll
+        for (int i = 0; i < MAXL; ++i) {
+          const int e = threadIdx.x + 256 * i;
+          if (e >= span * (CK / 4)) continue;   // (no break: a fully unrolled loop keeps v in registers)
+          const int row = e / (CK / 4), c4 = e % (CK / 4);
+          float f[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+          __attribute__((ext_vector_type(4))) __bf16 h4, l4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (a.pre_act) f[q] = f[q] < 0.f ? f[q] * a.slope : f[q];
+            const __bf16 h = (__bf16)f[q];
+            h4[q] = h;
+            l4[q] = (__bf16)(f[q] - (float)h);
+          }
+          *reinterpret_cast<decltype(h4)*>(&xh[row][c4 * 4]) = h4;
+          *reinterpret_cast<decltype(l4)*>(&xl[row][c4 * 4]) = l4;
+        }
+        wait_vm<0>();     // this wave's weight DMA (and the window loads) have landed
+        __syncthreads();  // ... every wave's
+        if (c + 1 < nchunks) load_x(c + 1);   // in flight under this chunk's MFMAs
+        const unsigned long long c1 = tr ? clock64() : 0;
+        for (int s = 0; s < a.nks_c; ++s) comp(s);
+        if (tr) {
+          t_stage += c1 - c0;
+          t_comp += clock64() - c1;
+        }
+      }
+    } else {
+      for (int c = 0; c < nchunks; ++c) {
+        const unsigned long long c0 = tr ? clock64() : 0;
+        stage(c);
+        const unsigned long long c1 = tr ? clock64() : 0;
+        for (int s = 0; s < a.nks_c; ++s) comp(s);
+        if (tr) {
+          t_stage += c1 - c0;
+          t_comp += clock64() - c1;
+        }
       }
     }
   }
@@ -651,10 +706,16 @@ static int conv_launch(ConvMulti& mc, int Tq_max, hipStream_t s) {
   if (halft && MTW <= 2 && NTW == 8 / MTW && CK <= 32) NTW /= 2;
   dim3 grid((Tq_max + 64 * NTW - 1) / (64 * NTW), Cout / (16 * MTW), B * zg);
   if (MTW == 1 && CK == 64) grid.x = (Tq_max + 255) / 256;
-#define FO_CONV(A, B, C)                                                                       \
-  do {                                                                                         \
-    if (mc.trc) hipLaunchKernelGGL((k_conv_cl<A, B, C, true>), grid, dim3(256), 0, s, mc);     \
-    else hipLaunchKernelGGL((k_conv_cl<A, B, C, false>), grid, dim3(256), 0, s, mc);           \
+  static int pf = -1;   // FO_CONV_PREFETCH=0 / 1: the staged / prefetching chunk loop (A/B)
+  if (pf < 0) {
+    const char* e = getenv("FO_CONV_PREFETCH");
+    pf = (e && e[0] == '1') ? 1 : 0;
+  }
+#define FO_CONV(A, B, C)                                                                        \
+  do {                                                                                          \
+    if (mc.trc) hipLaunchKernelGGL((k_conv_cl<A, B, C, true, false>), grid, dim3(256), 0, s, mc); \
+    else if (pf) hipLaunchKernelGGL((k_conv_cl<A, B, C, false, true>), grid, dim3(256), 0, s, mc); \
+    else hipLaunchKernelGGL((k_conv_cl<A, B, C, false, false>), grid, dim3(256), 0, s, mc);      \
   } while (0)
   if (MTW == 2 && NTW == 2 && CK == 64) FO_CONV(2, 2, 64);
   else if (MTW == 2 && NTW == 2 && CK == 32) FO_CONV(2, 2, 32);
