@@ -2037,7 +2037,8 @@ static int gemm_impl(const void* X, int x_f32, int ldx, int M, int K, const void
     // (>= 16 MiB: the Qwen2 q|k|v -- RoPE + paged-KV append in the reduce -- and o too, which at 128 rows ran 64-row
     // tiles re-reading the weights per row tile (q|k|v 80 us, r06q) or two row halves (o 2 x 22.8 us))
     if (g_rows && M > (g_rows == 4 ? 32 : 64) && M <= 128 && x_f32 && !lnw && !sout1 && !rstats1 && splitk <= 1 &&
-        wb >= (16ll << 20) && (ldx % 4) == 0 && !xpk.p0 && !xp32k.p0 && !g_force_nt &&
+        wb >= (16ll << 20) && (ldx % 4) == 0 && ((unsigned long long)X & 15) == 0 && !xpk.p0 && !xp32k.p0 &&
+        !g_force_nt &&
         !g_force_nw && (!swiglu || nt_all % 2 == 0)) {
       const int cus = num_cus();
       if (g_rows >= 5) {   // (probes 5 / 6) the one-K-pass 10-tile partition
