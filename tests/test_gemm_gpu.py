@@ -355,3 +355,34 @@ def test_gemm_split_merge_in_launch_bit_exact(dev, M, N, K):
     torch.testing.assert_close(y0.double(), ref, rtol=5e-5, atol=5e-5)
     torch.testing.assert_close(s0.double(), (ref ** 2).sum(1), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(g0.double(), ref * gamma.cpu().double(), rtol=5e-5, atol=5e-5)
+
+
+@pytest.mark.parametrize("M,N,K,sw", [(97, 2320, 4096, False), (128, 4624, 2048, False), (66, 2208, 3584, True),
+                                      (113, 3056, 4096, True)])
+def test_gemm_rows_ragged_tile_groups(dev, M, N, K, sw):
+    """k_gemm_rows on shapes whose tile count is no multiple of its tiles per workgroup (the last group ragged, its
+    padding weight loads and tiles never stored) and whose K splits are uneven, plain (bias + residual) and SwiGLU;
+    vs an fp64 reference (hi / lo accuracy), and the launch counter shows the kernel ran."""
+    from fo import ops
+    from fo.ops import PackedLinear
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g)
+    ops.launch_counts_reset()
+    if sw:
+        u = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+        lin = PackedLinear(w.to(dev), swiglu_up=u.to(dev))
+        y = lin(x.to(dev)).cpu().double()
+        ref = torch.nn.functional.silu(x.double() @ w.double().t()) * (x.double() @ u.double().t())
+    else:
+        b = torch.randn(N, generator=g)
+        r = torch.randn(M, N, generator=g)
+        lin = PackedLinear(w.to(dev), b.to(dev))
+        out = r.clone().to(dev)
+        lin(x.to(dev), out=out, residual=True)
+        y = out.cpu().double()
+        ref = x.double() @ w.double().t() + b.double() + r.double()
+    torch.cuda.synchronize()
+    assert ops.launch_counts()["gemm_rows"] == 1
+    err = (y - ref).abs().max().item()
+    assert err < 2e-4 * ref.abs().max().item(), err
