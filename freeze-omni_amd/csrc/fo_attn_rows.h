@@ -197,6 +197,15 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   unsigned long long* const tr =
       TR ? a.trc + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
   if (tr && tid == 0) tr[0] = wall_clock64();
+  // a split slot past the item's own split count leaves before its q / block-table loads: a captured graph's grid
+  // carries nsplit slots per item for the longest context it will see, so at short contexts most are empty (the text
+  // step: 16 slots, 1-2 used).  Split 0 always runs and keeps the loads-first order below.
+  if (a.cnt && sp > 0 && !(TR)) {
+    int Lm = 0;
+    for (int i = 0; i < tn; ++i) Lm = max(Lm, a.tok_nvis[t0 + i]);
+    const int need = (Lm + MAXPG * a.PS - 1) / (MAXPG * a.PS);
+    if (sp >= min(a.nsplit, max(need, max(1, (Lm + a.kps - 1) / a.kps)))) return;
+  }
   // this lane's q row slices, requested before anything that waits (they depend only on t0)
   float4 qraw[RT][2 * DC];
 #pragma unroll
