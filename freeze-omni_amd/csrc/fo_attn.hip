@@ -820,7 +820,7 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
   FO_REQUIRE(max_rows >= 1 && max_rows <= rows_max, "fo_attention: %d query rows per item (max %d)", max_rows,
              rows_max);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
-  FO_REQUIRE(!tickets || keys_per_split >= KT, "fo_attention: keys_per_split %d < %d", keys_per_split, KT);
+  FO_REQUIRE(!tickets || keys_per_split >= 32, "fo_attention: keys_per_split %d < 32", keys_per_split);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
              tickets, keys_per_split, items ? 1 : T / n_items, oph, opl, (T + 15) / 16, g_attn_trc};
   const bool dec = max_rows == 1 && (long long)maxb * PS <= DEC_MAXK;
@@ -836,7 +836,11 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
     return fo::check_launch("fo_attention/decode");
   }
   dim3 grid(n_items, KVH, nsplit);
-  if (hd == 128 && attn_waves() == 8 && max_rows > 16) hipLaunchKernelGGL((k_attn_mfma<128, 8, 2>), grid, dim3(512), 0, s, a);
+  // splits under 64 keys (the text step's short contexts spread over more CUs: a split's K / V arrive at one CU's
+  // memory parallelism) take the 2-wave form with 32-key tiles
+  const bool small = hd == 128 && tickets && keys_per_split < 64 && max_rows <= 16 && !a.trc;
+  if (small) hipLaunchKernelGGL((k_attn_mfma<128, 2>), grid, dim3(128), 0, s, a);
+  else if (hd == 128 && attn_waves() == 8 && max_rows > 16) hipLaunchKernelGGL((k_attn_mfma<128, 8, 2>), grid, dim3(512), 0, s, a);
   else if (hd == 128 && attn_waves() == 8 && a.trc) hipLaunchKernelGGL((k_attn_mfma<128, 8, 1, true>), grid, dim3(512), 0, s, a);
   else if (hd == 128 && attn_waves() == 8) hipLaunchKernelGGL((k_attn_mfma<128, 8>), grid, dim3(512), 0, s, a);
   else if (hd == 128) hipLaunchKernelGGL((k_attn_mfma<128>), grid, dim3(256), 0, s, a);

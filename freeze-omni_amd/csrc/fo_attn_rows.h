@@ -177,7 +177,8 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   constexpr int VP = HD + 2;             // V row pitch: the 4 key groups of a B fragment hit distinct banks
   constexpr int VL = KT * HD / 4 / NTH;  // float4 of V per thread per tile
   __shared__ float v_s[KT][VP];
-  __shared__ float p_s[16 * RT][KT + 4];
+  // (at least 64 + 4 wide: attn_arrive_and_merge reuses it as its [16][64 + 4] weight table)
+  __shared__ float p_s[16 * RT][(KT > 64 ? KT : 64) + 4];
   __shared__ float mx_s[NW][16 * RT];
   __shared__ float l_s[NW][16 * RT];
   __shared__ int nvis_s[16 * RT];
@@ -337,6 +338,10 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   // 256-key split waits for one round of memory, not two
   FO_ATTN_LOAD(kA, vA, c0)
   if (c0 + KT < c1) FO_ATTN_LOAD(kB, vB, c0 + KT)
+  if constexpr (TR) {   // probe: when this wave's first tiles have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tr && tid == 0) tr[6] = wall_clock64();
+  }
   auto tile = [&](float4 (&kreg)[2 * DC], float4 (&vreg)[VL], const int k0) {
     __syncthreads();  // the previous tile's p_s / v_s readers are done
 #pragma unroll

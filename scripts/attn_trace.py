@@ -20,7 +20,8 @@ pool = KVPool(1, KVH, hd, 8192, 16, dev)
 g = torch.Generator(device=dev).manual_seed(0)
 trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
 f = lambda v: f"med {np.median(v):6.2f} max {v.max():6.2f}"  # noqa: E731
-for L in (200, 500, 800):
+flush = torch.empty(1 << 28, device=dev)   # 1 GiB: evicts L2 and the Infinity Cache
+for L in (150, 200, 500, 800):
     seqs = [KVSeq(pool) for _ in range(B)]
     for s in seqs:
         s.reserve(L)
@@ -41,6 +42,10 @@ for L in (200, 500, 800):
                           pool.k[0], pool.v[0], H, KVH, hd, hd ** -0.5, ns, ws["ml"], ws["o"], out, tickets=ws["t"])
         us = graph_time(run, 50)
         trace.zero_()
+        cold = os.environ.get("ATTN_TRACE_COLD") == "1"
+        if cold:
+            flush.fill_(1.0)
+            torch.cuda.synchronize()
         with torch.cuda.stream(ops.engine_stream(dev)):
             _lib.call("fo_attention_set_trace", trace.data_ptr())
             run()
@@ -52,8 +57,9 @@ for L in (200, 500, 800):
         rel = (t - t0) / CLK
         merge = (t[:, 4] - t[:, 3]) / CLK
         last = merge > np.median(merge) + 0.5
-        print(f"L={L:4d} tokens/session={tok}: {us:6.2f} us/launch (graph), {len(t)} WGs, splits {int(t[0, 5]) - 1}; "
-              f"start {f(rel[:, 0])} | staged +{f((t[:, 1] - t[:, 0]) / CLK)} | tiles +{f((t[:, 2] - t[:, 1]) / CLK)} | "
+        print(f"{'cold' if cold else 'warm'} L={L:4d} tokens/session={tok}: {us:6.2f} us/launch (graph), {len(t)} WGs, splits {int(t[0, 5]) - 1}; "
+              f"start {f(rel[:, 0])} | staged +{f((t[:, 1] - t[:, 0]) / CLK)} | loads landed +{f((t[:, 6] - t[:, 1]) / CLK)} | "
+              f"tiles +{f((t[:, 2] - t[:, 1]) / CLK)} | "
               f"stored +{f((t[:, 3] - t[:, 2]) / CLK)} | arrive/merge +{f(merge)} (merging WGs {int(last.sum())}) | "
               f"end {f(rel[:, 4])}", flush=True)
     for s in seqs:

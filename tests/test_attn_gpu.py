@@ -31,13 +31,14 @@ def _reference(q, pool, seqs, meta_host, H, KVH, hd, scale):
 
 @pytest.mark.parametrize("H,KVH,hd", [(28, 4, 128), (14, 14, 64), (4, 2, 32)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("nsplit,kps", [(None, 0), (1, 0), (3, 0), (8, 64), (16, 256), (2, 64)])
+@pytest.mark.parametrize("nsplit,kps", [(None, 0), (1, 0), (3, 0), (8, 64), (16, 256), (2, 64), (16, 32)])
 @pytest.mark.parametrize("wide", [False, True])
 def test_attention_matches_reference(dev, H, KVH, hd, causal, nsplit, kps, wide):
     """kps > 0: splits sized per item from its key count (<= nsplit), merged in the same launch by the
     last split to arrive (tickets must come back zeroed for the next launch / graph replay).  wide: work items
     of ops.attn_max_rows(hd) query rows (Qwen2's 28 / 4 heads at 128: 4 tokens x 7 = 28 rows in two row tiles
-    sharing the K / V loads, k_attn_mfma<128, 8, 2>); else 16."""
+    sharing the K / V loads, k_attn_mfma<128, 8, 2>); else 16.  kps 32 at head dim 128 and 16 rows: the 2-wave
+    32-key-tile form (k_attn_mfma<128, 2>)."""
     g = torch.Generator().manual_seed(H * 1000 + hd + causal)
     pool = KVPool(1, KVH, hd, 256, 16, dev)
     pool.k.copy_(torch.randn(pool.k.shape, generator=g))
