@@ -60,7 +60,15 @@ __global__ __launch_bounds__(256) void k_rope_kv_write(const float* qkv, int ldq
 
 template <int HD, int NW = 4, int RT = 1, bool TR = false>
 __global__ __launch_bounds__(NW * 64) void k_attn_mfma(AttnArgs a) {
-  attn_rows_body<HD, NW, RT, TR>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  if constexpr (TR) {
+#pragma nounroll
+    for (int rep = 0; rep < (a.reps > 1 ? a.reps : 1); ++rep) {
+      attn_rows_body<HD, NW, RT, TR>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+      __syncthreads();
+    }
+  } else {
+    attn_rows_body<HD, NW, RT, TR>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  }
 }
 
 // Single-row decode attention (the AR speech decoder's step, models/decoder/decoder.py:341-349: one
@@ -821,8 +829,12 @@ int fo_attention(const float* q, int T, const int* items, int n_items, int max_r
              rows_max);
   FO_REQUIRE(nsplit >= 1 && (nsplit == 1 || (part_ml && part_o)), "fo_attention: bad split buffers");
   FO_REQUIRE(!tickets || keys_per_split >= 32, "fo_attention: keys_per_split %d < 32", keys_per_split);
+  // the in-launch merge reads the partials back through 32-bit buffer offsets (ld_sc1)
+  FO_REQUIRE(!tickets || nsplit == 1 || (long long)T * H * nsplit * hd * 4 < (1ll << 31),
+             "fo_attention: %d tokens x %d heads x %d splits of partials exceed the merge's 2 GiB window", T, H, nsplit);
   AttnArgs a{q, items, tok_nvis, block_table, kc, vc, part_ml, part_o, out, H, KVH, PS, maxb, nsplit, scale,
-             tickets, keys_per_split, items ? 1 : T / n_items, oph, opl, (T + 15) / 16, g_attn_trc};
+             tickets, keys_per_split, items ? 1 : T / n_items, oph, opl, (T + 15) / 16, g_attn_trc,
+             g_attn_trc && getenv("FO_ATTN_TRACE_REPS") ? atoi(getenv("FO_ATTN_TRACE_REPS")) : 1};
   const bool dec = max_rows == 1 && (long long)maxb * PS <= DEC_MAXK;
   FO_REQUIRE(!a.oph || (T <= 64 && (dec || nsplit == 1 || tickets)),
              "fo_attention: packed output needs <= 64 tokens and no combine launch");

@@ -25,7 +25,10 @@ struct AttnArgs {
   uint16_t* oph;
   uint16_t* opl;
   int prb;         // its row blocks: ceil(T / 16)
-  unsigned long long* trc;   // probes (fo_attention_set_trace): per workgroup {start, staged, tiles done, stored, end}
+  unsigned long long* trc;   // probes (fo_attention_set_trace): per workgroup {start, staged, tiles done, stored, end,
+                             // ran, loads landed}
+  int reps;                  // probe build only: the body runs reps times in a row (FO_ATTN_TRACE_REPS; the stamps
+                             // are the last pass's: the same code again, its instructions already fetched)
 };
 
 constexpr int KT = 64;      // keys per LDS tile (one key per lane in the score phase)
@@ -41,25 +44,41 @@ __device__ __forceinline__ void split8(const float* f, bf16x8& hi, bf16x8& lo) {
   }
 }
 
-// sum / max over the 16 lanes of a row group (lanes l, l^1, l^2, l^4, l^8)
+// sum / max over the 16 lanes of a row group by DPP within the 16-lane row (VALU, no LDS round trip): lanes l^1, l^2
+// (quad_perm), then the other quad (row_half_mirror) and the other half (row_mirror) -- after the quad steps every lane
+// of a quad holds the same value, so each step adds the same operands in the same order as the l^4 / l^8 butterfly
+// (the same result bit for bit)
+template <int CTRL>
+__device__ __forceinline__ float dpp16(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ float row16_max(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp16<0xB1>(v));    // quad_perm [1, 0, 3, 2]
+  v = fmaxf(v, dpp16<0x4E>(v));    // quad_perm [2, 3, 0, 1]
+  v = fmaxf(v, dpp16<0x141>(v));   // row_half_mirror
+  return fmaxf(v, dpp16<0x140>(v));  // row_mirror
 }
 __device__ __forceinline__ float row16_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp16<0xB1>(v);
+  v += dpp16<0x4E>(v);
+  v += dpp16<0x141>(v);
+  return v + dpp16<0x140>(v);
 }
 
 // Split `sp` of work item `it` has written its partial (part_o / part_ml): publish it and take an
 // arrival ticket; the split that draws ns - 1 merges all ns partials of the item's R rows with
 // k_attn_combine's arithmetic and resets the ticket for the next launch.  Protocol: every wave drains
-// its stores, lane 0 releases at agent scope before the relaxed ticket add, the merging split acquires
-// at agent scope before reading (correct for any placement of the splits over XCDs).
+// its stores and lane 0 takes the ticket behind a workgroup barrier (correct for any placement of the splits
+// over XCDs).  SC (the 8-wave kernel: one workgroup per CU): the partials were stored write-through (st_wt) and
+// are read back with sc1 loads, no fences (fo_common.h); otherwise lane 0 releases at agent scope before the
+// relaxed ticket add and the merging split acquires at agent scope before plain reads.
 // last_s / w_s: the kernel's existing LDS (no second __shared__ object for the flag).
-template <int HD>
+template <bool SC>
+__device__ __forceinline__ void st_part(float* p, float v) {
+  if constexpr (SC) st_wt(p, v);
+  else *p = v;
+}
+template <int HD, bool SC>
 __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns, int t0, int R, int G,
                                       int& last_s, float* w_s) {
   const int tid = threadIdx.x;
@@ -67,19 +86,27 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (!SC) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_s = old == ns - 1;
   }
   __syncthreads();
   if (!last_s) return;
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (!SC) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  const __amdgpu_buffer_rsrc_t rml = rsrc_of(a.part_ml), rpo = rsrc_of(a.part_o);
+  // a partial's element: an sc1 load (SC) or a plain one after the acquire
+  auto ml_at = [&](size_t off) { return SC ? ld_sc1(rml, off) : a.part_ml[off]; };
+  auto po_at = [&](size_t off) { return SC ? ld_sc1(rpo, off) : a.part_o[off]; };
   // per row: split weights exp(m_q - M) (0 for empty splits) and 1 / l into LDS (w_s: [16][KT + 4], the kernel's P
   // tile, ns <= KT).  The partials were written by other XCDs' workgroups, so every read is a memory-side round trip:
   // the loads are issued in groups of MQ splits (x EU outputs per thread below) before any of them is used, and the
@@ -87,12 +114,13 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
   constexpr int MQ = 8, EU = 4;
   for (int r = tid; r < R; r += blockDim.x) {
     const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-    const float2* ml = reinterpret_cast<const float2*>(a.part_ml + th * a.nsplit * 2);
+    const size_t mlo = th * a.nsplit * 2;
     float M = -INFINITY;
     for (int q0 = 0; q0 < ns; q0 += MQ) {
       float2 v[MQ];
 #pragma unroll
-      for (int j = 0; j < MQ; ++j) v[j] = q0 + j < ns ? ml[q0 + j] : make_float2(0.f, 0.f);
+      for (int j = 0; j < MQ; ++j)
+        v[j] = q0 + j < ns ? make_float2(ml_at(mlo + 2 * (q0 + j)), ml_at(mlo + 2 * (q0 + j) + 1)) : make_float2(0.f, 0.f);
 #pragma unroll
       for (int j = 0; j < MQ; ++j)
         if (v[j].y > 0.f) M = fmaxf(M, v[j].x);
@@ -101,7 +129,8 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
     for (int q0 = 0; q0 < ns; q0 += MQ) {   // (second pass: cache hits)
       float2 v[MQ];
 #pragma unroll
-      for (int j = 0; j < MQ; ++j) v[j] = q0 + j < ns ? ml[q0 + j] : make_float2(0.f, 0.f);
+      for (int j = 0; j < MQ; ++j)
+        v[j] = q0 + j < ns ? make_float2(ml_at(mlo + 2 * (q0 + j)), ml_at(mlo + 2 * (q0 + j) + 1)) : make_float2(0.f, 0.f);
 #pragma unroll
       for (int j = 0; j < MQ; ++j) {
         if (q0 + j >= ns) break;
@@ -115,7 +144,7 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
   __syncthreads();
   const int RH = R * HD;
   for (int e0 = tid; e0 < RH; e0 += EU * blockDim.x) {
-    const float* po[EU];
+    size_t po[EU];
     const float* w[EU];
     size_t tho[EU];
     float o[EU];
@@ -124,7 +153,7 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
       const int e = min(e0 + u * (int)blockDim.x, RH - 1);
       const int r = e / HD, d = e - (e / HD) * HD;
       const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-      po[u] = a.part_o + th * a.nsplit * HD + d;
+      po[u] = th * a.nsplit * HD + d;
       w[u] = w_s + r * (KT + 4);
       tho[u] = th * HD + d;
       o[u] = 0.f;
@@ -136,7 +165,7 @@ __device__ void attn_arrive_and_merge(const AttnArgs& a, int it, int kvh, int ns
 #pragma unroll
         for (int j = 0; j < MQ; ++j) {
           const int q = q0 + j;
-          pv[u][j] = q < ns && w[u][q] != 0.f ? po[u][(size_t)q * HD] : 0.f;
+          pv[u][j] = q < ns && w[u][q] != 0.f ? po_at(po[u] + (size_t)q * HD) : 0.f;
         }
 #pragma unroll
       for (int u = 0; u < EU; ++u)
@@ -176,6 +205,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   constexpr int NTW = (NTILE + NW - 1) / NW;   // output tiles per wave
   constexpr int VP = HD + 2;             // V row pitch: the 4 key groups of a B fragment hit distinct banks
   constexpr int VL = KT * HD / 4 / NTH;  // float4 of V per thread per tile
+  constexpr bool SC = NW == 8;           // one workgroup per CU: the fence-free split hand-off (attn_arrive_and_merge)
   __shared__ float v_s[KT][VP];
   // (at least 64 + 4 wide: attn_arrive_and_merge reuses it as its [16][64 + 4] weight table)
   __shared__ float p_s[16 * RT][(KT > 64 ? KT : 64) + 4];
@@ -196,7 +226,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   const int grp = lane >> 4, col = lane & 15;
   const int* bt = a.block_table + (size_t)seq * a.maxb;
   unsigned long long* const tr =
-      TR ? a.trc + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+      TR ? a.trc + 32 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
   if (tr && tid == 0) tr[0] = wall_clock64();
   // a split slot past the item's own split count leaves before its q / block-table loads: a captured graph's grid
   // carries nsplit slots per item for the longest context it will see, so at short contexts most are empty (the text
@@ -239,10 +269,10 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
   if (c0 >= c1) {  // empty split: neutral partial
     for (int r = tid; r < R; r += NTH) {
       const size_t o = ((size_t)(t0 + r / G) * a.H + kvh * G + r % G) * a.nsplit + sp;
-      a.part_ml[o * 2] = -INFINITY;
-      a.part_ml[o * 2 + 1] = 0.f;
+      st_part<SC>(a.part_ml + o * 2, -INFINITY);
+      st_part<SC>(a.part_ml + o * 2 + 1, 0.f);
     }
-    if (a.cnt) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
+    if (a.cnt) attn_arrive_and_merge<HD, SC>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
     return;
   }
   const int pb0 = c0 / a.PS, npg = (c1 - 1) / a.PS - pb0 + 1;
@@ -262,13 +292,13 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
     for (int e = tid; e < R * HD; e += NTH) {
       const int r = e / HD, d = e - r * HD;
       const size_t th = (size_t)(t0 + r / G) * a.H + kvh * G + r % G;
-      a.part_o[(th * a.nsplit + sp) * HD + d] = NAN;
+      st_part<SC>(a.part_o + (th * a.nsplit + sp) * HD + d, NAN);
       if (d == 0) {
-        a.part_ml[(th * a.nsplit + sp) * 2] = INFINITY;
-        a.part_ml[(th * a.nsplit + sp) * 2 + 1] = 1.f;
+        st_part<SC>(a.part_ml + (th * a.nsplit + sp) * 2, INFINITY);
+        st_part<SC>(a.part_ml + (th * a.nsplit + sp) * 2 + 1, 1.f);
       }
     }
-    if (a.cnt) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
+    if (a.cnt) attn_arrive_and_merge<HD, SC>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
     return;
   }
   const int pb = whole ? 0 : pb0;  // pg_s holds pages pb..
@@ -357,6 +387,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
                           kreg[2 * c + 1].x, kreg[2 * c + 1].y, kreg[2 * c + 1].z, kreg[2 * c + 1].w};
       split8(f, kh[c], kl[c]);
     }
+    if (tr && tid == 0 && k0 == c0) tr[7] = wall_clock64();
     if (k0 + 2 * KT < c1) FO_ATTN_LOAD(kreg, vreg, k0 + 2 * KT)
     // S[r = 16 rt + 4 grp + i][key = k0 + 16 wave + col]
     f32x4 s[RT];
@@ -387,7 +418,9 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
         for (int i = 0; i < 4; ++i) mx_s[wave][16 * rt + 4 * grp + i] = mw[i];
       }
     }
+    if (tr && lane == 0 && k0 == c0) tr[16 + wave] = wall_clock64();   // each wave's arrival at the max exchange
     __syncthreads();
+    if (tr && tid == 0 && k0 == c0) tr[8] = wall_clock64();
     float alpha[RT][4];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -406,6 +439,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
       }
     }
     __syncthreads();  // p_s and v_s complete
+    if (tr && tid == 0 && k0 == c0) tr[9] = wall_clock64();
     // O[r][d] += P[r][:] V[:][d] for this wave's d tiles (one V fragment split serves every row tile)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -442,6 +476,7 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
         }
       }
     }
+    if (tr && tid == 0 && k0 == c0) tr[10] = wall_clock64();
   };
   for (int k0 = c0; k0 < c1; k0 += 2 * KT) {
     tile(kA, vA, k0);
@@ -480,16 +515,16 @@ __device__ __forceinline__ void attn_rows_body(const AttnArgs& a, const int it, 
         a.out[th * HD + d] = acc[rt][n][i] / l;
         if (a.oph) xpack_store(a.oph, a.opl, (int)(th / a.H), (int)(th % a.H) * HD + d, acc[rt][n][i] / l, a.prb);
       } else {
-        a.part_o[(th * a.nsplit + sp) * HD + d] = acc[rt][n][i];
+        st_part<SC>(a.part_o + (th * a.nsplit + sp) * HD + d, acc[rt][n][i]);
       }
     }
     if (ns > 1 && wave == 0 && col == 0) {
-      a.part_ml[(th * a.nsplit + sp) * 2] = m_run[rt][i];
-      a.part_ml[(th * a.nsplit + sp) * 2 + 1] = l;
+      st_part<SC>(a.part_ml + (th * a.nsplit + sp) * 2, m_run[rt][i]);
+      st_part<SC>(a.part_ml + (th * a.nsplit + sp) * 2 + 1, l);
     }
   }
   if (tr && tid == 0) tr[3] = wall_clock64();
-  if (a.cnt && ns > 1) attn_arrive_and_merge<HD>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
+  if (a.cnt && ns > 1) attn_arrive_and_merge<HD, SC>(a, it, kvh, ns, t0, R, G, nvis_s[0], &p_s[0][0]);
   if (tr && tid == 0) {
     tr[4] = wall_clock64();
     tr[5] = 1 + (unsigned long long)ns;   // (nonzero: this workgroup ran the tile loop)

@@ -104,24 +104,9 @@ __device__ __forceinline__ void load_x(const XT* p, bf16x8& hi, bf16x8& lo) {
   }
 }
 
-// In-launch split-K merge (gemm_body, a.counters set by fo_gemm): each split's partial tile is stored
-// write-through (sc1: a relaxed agent-scope atomic store, so it leaves this XCD's L2 without a release
-// fence), the split drains its stores and takes the tile's ticket; the last split to arrive reads the others
-// back with sc1 buffer loads (past its L1 / L2) and runs the epilogue -- no second launch, no fences.
-typedef __attribute__((address_space(1))) float g_f32;
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store((g_f32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
-  const unsigned long long b = (unsigned long long)base;
-  return __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
-                              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)b)),
-      (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ float ld_sc1(__amdgpu_buffer_rsrc_t r, size_t off_floats) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (unsigned)(off_floats * 4), 0, 16));
-}
+// In-launch split-K merge (gemm_body, a.counters set by fo_gemm): each split's partial tile is stored write-through
+// (st_wt, fo_common.h), the split drains its stores and takes the tile's ticket; the last split to arrive reads the
+// others back with ld_sc1 -- no second launch, no fences.
 
 // Output element (m, n): bias, folded-BN affine, activation or SwiGLU, residual, store.
 __device__ __forceinline__ float epilogue_store(const GemmArgs& a, bool sw, int m, int n, float v, float u) {

@@ -18,7 +18,7 @@ dev = torch.device("cuda:0")
 H, KVH, hd, B, CLK = 28, 4, 128, 8, 100.0
 pool = KVPool(1, KVH, hd, 8192, 16, dev)
 g = torch.Generator(device=dev).manual_seed(0)
-trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
+trace = torch.zeros(32 * 8192, dtype=torch.int64, device=dev)
 f = lambda v: f"med {np.median(v):6.2f} max {v.max():6.2f}"  # noqa: E731
 flush = torch.empty(1 << 28, device=dev)   # 1 GiB: evicts L2 and the Infinity Cache
 for L in (150, 200, 500, 800):
@@ -51,15 +51,19 @@ for L in (150, 200, 500, 800):
             run()
             _lib.call("fo_attention_set_trace", None)
             torch.cuda.synchronize()
-        t = trace.view(-1, 8).cpu().numpy().astype(np.int64)
+        ws["t"].zero_()   # (FO_ATTN_TRACE_REPS > 1: passes of different splits interleave their tickets)
+        t = trace.view(-1, 32).cpu().numpy().astype(np.int64)
         t = t[t[:, 5] != 0]   # the workgroups that ran a tile loop
         t0 = t[:, 0].min()
         rel = (t - t0) / CLK
         merge = (t[:, 4] - t[:, 3]) / CLK
         last = merge > np.median(merge) + 0.5
-        print(f"{'cold' if cold else 'warm'} L={L:4d} tokens/session={tok}: {us:6.2f} us/launch (graph), {len(t)} WGs, splits {int(t[0, 5]) - 1}; "
+        print(f"{'cold' if cold else 'warm'} reps={os.environ.get('FO_ATTN_TRACE_REPS', '1')} L={L:4d} tokens/session={tok}: {us:6.2f} us/launch (graph), {len(t)} WGs, splits {int(t[0, 5]) - 1}; "
               f"start {f(rel[:, 0])} | staged +{f((t[:, 1] - t[:, 0]) / CLK)} | loads landed +{f((t[:, 6] - t[:, 1]) / CLK)} | "
-              f"tiles +{f((t[:, 2] - t[:, 1]) / CLK)} | "
+              f"tiles +{f((t[:, 2] - t[:, 1]) / CLK)} [K split +{f((t[:, 7] - t[:, 1]) / CLK)}, waves at max "
+              f"exchange: first +{f((t[:, 16:24].min(1) - t[:, 1]) / CLK)} last +{f((t[:, 16:24].max(1) - t[:, 1]) / CLK)}, "
+              f"barrier 2 +{f((t[:, 8] - t[:, 1]) / CLK)}, barrier 3 +{f((t[:, 9] - t[:, 1]) / CLK)}, "
+              f"PV done +{f((t[:, 10] - t[:, 1]) / CLK)}] | "
               f"stored +{f((t[:, 3] - t[:, 2]) / CLK)} | arrive/merge +{f(merge)} (merging WGs {int(last.sum())}) | "
               f"end {f(rel[:, 4])}", flush=True)
     for s in seqs:
