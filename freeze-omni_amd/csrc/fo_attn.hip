@@ -16,6 +16,8 @@
 // 2. Encoder rel-pos attention over a per-user ring buffer (models/encoder/attention.py:407-459):
 //    scores = ((q+u).K^T + (q+v).P^T)/sqrt(dk), no mask, no rel_shift; P rows come from a
 //    table of linear_pos(sinusoid(position)) precomputed at load for every position.
+#include <type_traits>
+
 #include "fo_common.h"
 
 namespace {
@@ -174,13 +176,19 @@ __device__ bool attn_decode_row(const AttnArgs& a, const int it, const int h, fl
     acc.z += p * v.z;
     acc.w += p * v.w;
   }
-#pragma unroll
-  for (int o = LPK; o < 64; o <<= 1) {
-    acc.x += __shfl_xor(acc.x, o, 64);
-    acc.y += __shfl_xor(acc.y, o, 64);
-    acc.z += __shfl_xor(acc.z, o, 64);
-    acc.w += __shfl_xor(acc.w, o, 64);
-  }
+  // the wave's keys, lanes LPK apart (lane_xor: no LDS round trip)
+  auto xadd = [&](auto off) {
+    constexpr int O = decltype(off)::value;
+    if constexpr (O >= LPK && O < 64) {
+      acc.x += lane_xor<O>(acc.x);
+      acc.y += lane_xor<O>(acc.y);
+      acc.z += lane_xor<O>(acc.z);
+      acc.w += lane_xor<O>(acc.w);
+    }
+  };
+  xadd(std::integral_constant<int, 8>{});
+  xadd(std::integral_constant<int, 16>{});
+  xadd(std::integral_constant<int, 32>{});
   if (sub == 0) *reinterpret_cast<float4*>(&acc_s[wave][4 * l4]) = acc;
   __syncthreads();
   for (int d = tid; d < HD; d += DEC_NT) {

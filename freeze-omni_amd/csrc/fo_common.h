@@ -93,15 +93,49 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 __host__ __device__ __forceinline__ float round_f16(float f) {
   return (float)(_Float16)f;
 }
+// the value lane (lane ^ O) holds, O a power of two below 64, without an LDS round trip (ds_bpermute): the gfx950
+// half-wave / row swaps for 32 and 16, DPP within the 16-lane row below (row_ror:8; row_shl:4 into banks 0 and 2 and
+// row_shr:4 into banks 1 and 3; quad_perm for 2 and 1).  The whole wave must be active, as for __shfl_xor.
+template <int CTRL, int BANK = 0xF>
+__device__ __forceinline__ float dpp_mov(float old, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, BANK, false));
+}
+template <int O>
+__device__ __forceinline__ float lane_xor(float v) {
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "lane_xor: offset");
+  if constexpr (O == 32 || O == 16) {
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    // {vdst, vsrc} after the swap: a lane of the lower half (row pair) finds its partner in vsrc, of the upper in vdst
+    const auto r = O == 32 ? __builtin_amdgcn_permlane32_swap(u, u, false, false)
+                           : __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (threadIdx.x & O) ? r[0] : r[1]);
+  } else if constexpr (O == 8) {
+    return dpp_mov<0x128>(v, v);
+  } else if constexpr (O == 4) {
+    return dpp_mov<0x114, 0xA>(dpp_mov<0x104, 0x5>(v, v), v);
+  } else if constexpr (O == 2) {
+    return dpp_mov<0x4E>(v, v);
+  } else {
+    return dpp_mov<0xB1>(v, v);
+  }
+}
+// butterflies over the wave in the order 32, 16, ..., 1 (the same operands in the same order as the __shfl_xor form)
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += lane_xor<32>(v);
+  v += lane_xor<16>(v);
+  v += lane_xor<8>(v);
+  v += lane_xor<4>(v);
+  v += lane_xor<2>(v);
+  return v + lane_xor<1>(v);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, lane_xor<32>(v));
+  v = fmaxf(v, lane_xor<16>(v));
+  v = fmaxf(v, lane_xor<8>(v));
+  v = fmaxf(v, lane_xor<4>(v));
+  v = fmaxf(v, lane_xor<2>(v));
+  return fmaxf(v, lane_xor<1>(v));
 }
 // block-wide sum for blockDim.x == 64*NW; lds must hold NW floats
 template <int NW>
